@@ -1,0 +1,592 @@
+// ref_cpu — CPU ORACLE (TEST INFRASTRUCTURE ONLY). See ref_cpu.hpp header.
+// Clients (tests/JNIGridnetVecClient.java, JNIGridnetClient.java,
+// JNIGridnetClientSelfPlay.java, JNIBotClient.java), the WinLoss reward
+// (ai/reward/WinLossRewardFunction.java:16-24), the strict trace replay
+// (test/microrts/TestTracesIntegrity.java:72-127) and the Philox random policy
+// used by bench.py, behind a small C API consumed by ctypes from tests/.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ref_cpu.hpp"
+
+using namespace oref;
+
+static thread_local std::string g_err;
+
+namespace {
+
+enum BotKind { BOT_PASSIVE = 0, BOT_RANDOM_BIASED = 1 };
+
+struct Resp {  // ai/jni/Response.java:12-30 (one reward function: WinLoss)
+    std::vector<int32_t> obs;
+    double reward = 0;
+    uint8_t done = 0;
+};
+
+// WinLossRewardFunction.computeReward (ai/reward/WinLossRewardFunction.java:16-24)
+static void winLoss(const GameState& after, int maxplayer, double& reward, uint8_t& done) {
+    reward = 0.0;
+    done = 0;
+    if (after.gameover()) {
+        done = 1;
+        reward = after.winner() == maxplayer ? 1.0 : -1.0;
+    }
+}
+
+struct Env;
+
+struct World {
+    UnitTypeTable utt;
+    int maxAttackRadius, K;
+    int H = 0, W = 0, C = 6;
+    bool partialObs = false;
+    uint64_t seed = 0;
+    World(int ver, int crs) : utt(ver, crs) {
+        maxAttackRadius = utt.getMaxAttackRange() * 2 + 1;
+        K = maskSlotsPerCell(utt);
+    }
+};
+
+// One game (self-play: 2 external players; bot: 1 external + 1 AI)
+struct Env {
+    World* w;
+    MapTemplate map;
+    bool selfplay;
+    BotKind botKind = BOT_PASSIVE;
+    GSP gs;
+    GSP playergs[2];
+    JavaRandom samplerGen, cancelGen, damageGen;
+    std::unique_ptr<AI> ai2;
+    Resp resp[2];
+
+    Env(World* wd, const MapTemplate& m, bool sp, BotKind bk, uint64_t envSeed)
+        : w(wd), map(m), selfplay(sp), botKind(bk), samplerGen((int64_t)envSeed),
+          cancelGen((int64_t)(envSeed ^ 0x9E3779B97F4A7C15ULL)), damageGen((int64_t)(envSeed ^ 0xC2B2AE3D27D4EB4FULL)) {
+        if (!sp) {
+            if (bk == BOT_PASSIVE) ai2.reset(new PassiveAI());
+            else ai2.reset(new RandomBiasedAI(&samplerGen));
+        }
+        for (auto& r : resp) r.obs.assign((size_t)w->C * w->H * w->W, 0);
+    }
+    GSP makeView(int player) {
+        if (w->partialObs) return std::make_shared<PartiallyObservableGameState>(*gs, player);
+        return gs;
+    }
+    void newGame() {
+        gs = std::make_shared<GameState>(instantiate(map, w->utt), &w->utt);
+        gs->cancelRandom = &cancelGen;
+        gs->damageRandom = &damageGen;
+    }
+    // JNIGridnetClientSelfPlay.reset (tests/JNIGridnetClientSelfPlay.java:221-247)
+    // JNIGridnetClient.reset (tests/JNIGridnetClient.java:235-258)
+    void reset(int player) {
+        newGame();
+        if (selfplay) {
+            for (int i = 0; i < 2; i++) {
+                playergs[i] = makeView(i);
+                resp[i].reward = 0;
+                resp[i].done = 0;
+                playergs[i]->getVectorObservation(i, resp[i].obs.data());
+            }
+        } else {
+            playergs[0] = makeView(player);
+            resp[0].reward = 0;
+            resp[0].done = 0;
+            playergs[0]->getVectorObservation(player, resp[0].obs.data());
+        }
+    }
+    std::vector<int> rowsFromGrid(const int32_t* a) const {  // [HW][7] → Java rows [pos, 7 comps]
+        const int HW = w->H * w->W;
+        std::vector<int> rows((size_t)HW * 8);
+        for (int c = 0; c < HW; c++) {
+            rows[(size_t)c * 8] = c;
+            for (int k = 0; k < 7; k++) rows[(size_t)c * 8 + 1 + k] = a[(size_t)c * 7 + k];
+        }
+        return rows;
+    }
+    // JNIAI.getAction (ai/jni/JNIAI.java:316-320)
+    PlayerAction jniGetAction(int player, const GameState& g, const std::vector<int>& rows) const {
+        int n = (int)(rows.size() / 8);
+        PlayerAction pa = PlayerAction::fromVectorAction(rows, n, g, w->utt, player, w->maxAttackRadius);
+        pa.fillWithNones(g, player, 1);
+        return pa;
+    }
+    // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
+    void stepSelfPlay(const std::vector<int>& rows0, const std::vector<int>& rows1) {
+        const std::vector<int>* rows[2] = {&rows0, &rows1};
+        for (int i = 0; i < 2; i++) {
+            playergs[i] = makeView(i);
+            PlayerAction pa = jniGetAction(i, *playergs[i], *rows[i]);
+            gs->issueSafe(pa);
+        }
+        gs->cycle();
+        for (int i = 0; i < 2; i++) {
+            winLoss(*gs, i, resp[i].reward, resp[i].done);
+            playergs[i]->getVectorObservation(i, resp[i].obs.data());
+        }
+    }
+    // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203)
+    void stepBot(const std::vector<int>& rows, int player) {
+        GSP p1 = makeView(player);
+        GSP p2 = makeView(1 - player);
+        playergs[0] = p1;
+        PlayerAction pa1 = jniGetAction(player, *p1, rows);
+        PlayerAction pa2 = ai2->getAction(1 - player, *p2);
+        gs->issueSafe(pa1);
+        gs->issueSafe(pa2);
+        gs->cycle();
+        winLoss(*gs, player, resp[0].reward, resp[0].done);
+        p1->getVectorObservation(player, resp[0].obs.data());
+    }
+};
+
+// tests/JNIGridnetVecClient.java:17-335
+struct VecClient {
+    std::unique_ptr<World> world;
+    std::vector<std::unique_ptr<Env>> selfPlay;  // one per pair of slots
+    std::vector<std::unique_ptr<Env>> bots;
+    std::vector<int> envSteps;
+    int maxSteps = 2000;
+    int nSlots() const { return (int)(selfPlay.size() * 2 + bots.size()); }
+    Env* slotEnv(int s, int* player) {
+        int nsp = (int)selfPlay.size() * 2;
+        if (s < nsp) {
+            *player = s & 1;
+            return selfPlay[(size_t)s / 2].get();
+        }
+        *player = 0;
+        return bots[(size_t)(s - nsp)].get();
+    }
+    void collect(int32_t* obs, double* reward, uint8_t* done) {
+        const size_t osz = (size_t)world->C * world->H * world->W;
+        for (int s = 0; s < nSlots(); s++) {
+            int p;
+            Env* e = slotEnv(s, &p);
+            Resp& r = e->resp[e->selfplay ? p : 0];
+            if (obs) std::memcpy(obs + (size_t)s * osz, r.obs.data(), osz * sizeof(int32_t));
+            if (reward) reward[s] = r.reward;
+            if (done) done[s] = r.done;
+        }
+    }
+    // reset (:179-211)
+    void reset(const int32_t* players) {
+        for (auto& e : selfPlay) e->reset(0);
+        int nsp = (int)selfPlay.size() * 2;
+        for (size_t j = 0; j < bots.size(); j++) bots[j]->reset(players ? players[nsp + (int)j] : 0);
+        std::fill(envSteps.begin(), envSteps.end(), 0);
+    }
+    // gameStep (:213-297)
+    void step(const int32_t* actions, const int32_t* players) {
+        const size_t asz = (size_t)world->H * world->W * 7;
+        for (size_t i = 0; i < selfPlay.size(); i++) {
+            Env& e = *selfPlay[i];
+            e.stepSelfPlay(e.rowsFromGrid(actions + (2 * i) * asz), e.rowsFromGrid(actions + (2 * i + 1) * asz));
+            envSteps[2 * i] += 1;
+            envSteps[2 * i + 1] += 1;
+            if (e.resp[0].done || envSteps[2 * i] >= maxSteps) {
+                double tr0 = e.resp[0].reward, tr1 = e.resp[1].reward;
+                uint8_t td0 = e.resp[0].done, td1 = e.resp[1].done;
+                e.reset(0);
+                e.resp[0].reward = tr0;
+                e.resp[0].done = td0;
+                e.resp[1].reward = tr1;
+                e.resp[1].done = td1;
+                e.resp[0].done = 1;
+                e.resp[1].done = 1;
+                envSteps[2 * i] = 0;
+                envSteps[2 * i + 1] = 0;
+            }
+        }
+        int nsp = (int)selfPlay.size() * 2;
+        for (size_t j = 0; j < bots.size(); j++) {
+            int s = nsp + (int)j;
+            Env& e = *bots[j];
+            int pl = players ? players[s] : 0;
+            envSteps[(size_t)s] += 1;
+            e.stepBot(e.rowsFromGrid(actions + (size_t)s * asz), pl);
+            if (e.resp[0].done || envSteps[(size_t)s] >= maxSteps) {
+                double tr = e.resp[0].reward;
+                uint8_t td = e.resp[0].done;
+                e.reset(pl);
+                e.resp[0].reward = tr;
+                e.resp[0].done = td;
+                e.resp[0].done = 1;
+                envSteps[(size_t)s] = 0;
+            }
+        }
+    }
+    // getMasks (:307-316) → JNIGridnetClient(SelfPlay).getMasks
+    void masks(int player, uint8_t* out) {
+        const size_t msz = (size_t)world->H * world->W * world->K;
+        int nsp = (int)selfPlay.size() * 2;
+        for (size_t i = 0; i < selfPlay.size(); i++) {
+            computeMasks(*selfPlay[i]->gs, world->utt, 0, out + (2 * i) * msz);
+            computeMasks(*selfPlay[i]->gs, world->utt, 1, out + (2 * i + 1) * msz);
+        }
+        for (size_t j = 0; j < bots.size(); j++) computeMasks(*bots[j]->gs, world->utt, player, out + (size_t)(nsp + (int)j) * msz);
+    }
+};
+
+// ---------------------------------------------------------------- Philox4x32-10 random policy
+struct Philox {
+    static inline uint32_t mulhi(uint32_t a, uint32_t b, uint32_t* lo) {
+        uint64_t p = (uint64_t)a * b;
+        *lo = (uint32_t)p;
+        return (uint32_t)(p >> 32);
+    }
+    static void gen(uint32_t c[4], uint32_t k0, uint32_t k1) {
+        for (int r = 0; r < 10; r++) {
+            uint32_t lo0, lo1;
+            uint32_t hi0 = mulhi(0xD2511F53u, c[0], &lo0);
+            uint32_t hi1 = mulhi(0xCD9E8D57u, c[2], &lo1);
+            uint32_t n0 = hi1 ^ c[1] ^ k0, n1 = lo1, n2 = hi0 ^ c[3] ^ k1, n3 = lo0;
+            c[0] = n0; c[1] = n1; c[2] = n2; c[3] = n3;
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+    }
+};
+static inline int pickBit(uint32_t r, const uint8_t* bits, int n) {  // uniform among set bits (multiply-shift)
+    int cnt = 0;
+    for (int i = 0; i < n; i++) cnt += bits[i] ? 1 : 0;
+    if (cnt == 0) return -1;
+    int k = (int)(((uint64_t)r * (uint32_t)cnt) >> 32);
+    for (int i = 0; i < n; i++)
+        if (bits[i]) {
+            if (k == 0) return i;
+            k--;
+        }
+    return -1;
+}
+
+}  // namespace
+
+// Masked uniform random policy shared bit-for-bit with the GPU kernel
+// (microrts_amd/csrc/mrts_kernels.hip: policy_kernel).  mask = u8[HW][K], out = int32[HW][7].
+extern "C" void oref_policy(const uint8_t* mask, int HW, int K, int n_types, uint64_t seed, uint32_t env_id,
+                            uint32_t step, uint32_t player, int32_t* out) {
+    for (int c = 0; c < HW; c++) {
+        const uint8_t* m = mask + (size_t)c * K;
+        int32_t* a = out + (size_t)c * 7;
+        for (int k = 0; k < 7; k++) a[k] = 0;
+        if (!m[0]) continue;
+        uint32_t ctr[4] = {env_id, step, (uint32_t)c, player};
+        Philox::gen(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        int t = pickBit(ctr[0], m + 1, 6);
+        if (t < 0) continue;
+        a[0] = t;
+        switch (t) {
+            case 1: a[1] = pickBit(ctr[1], m + 7, 4); break;
+            case 2: a[2] = pickBit(ctr[1], m + 11, 4); break;
+            case 3: a[3] = pickBit(ctr[1], m + 15, 4); break;
+            case 4:
+                a[4] = pickBit(ctr[1], m + 19, 4);
+                a[5] = pickBit(ctr[2], m + 23, n_types);
+                break;
+            case 5: a[6] = pickBit(ctr[1], m + 23 + n_types, K - 23 - n_types); break;
+        }
+    }
+}
+
+extern "C" {
+
+const char* oref_last_error() { return g_err.c_str(); }
+
+// map_paths: one per slot (self-play games use map_paths[2i], like :119); bot_kinds: per bot env
+void* oref_create(int n_selfplay_slots, int n_bot_envs, const int32_t* bot_kinds, int max_steps, int partial_obs,
+                  int utt_version, int crs, const char** map_paths, uint64_t seed) {
+    try {
+        if (n_selfplay_slots % 2) throw std::runtime_error("n_selfplay_slots must be even");
+        auto v = new VecClient();
+        v->world.reset(new World(utt_version, crs));
+        v->world->partialObs = partial_obs != 0;
+        v->world->C = partial_obs ? 8 : 6;
+        v->world->seed = seed;
+        v->maxSteps = max_steps;
+        int nslots = n_selfplay_slots + n_bot_envs;
+        std::vector<MapTemplate> maps;
+        for (int s = 0; s < nslots; s++) maps.push_back(loadMapFile(map_paths[s]));
+        v->world->H = maps[0].height;
+        v->world->W = maps[0].width;
+        for (auto& m : maps)
+            if (m.height != v->world->H || m.width != v->world->W) throw std::runtime_error("all maps must share env 0's size");
+        for (int i = 0; i < n_selfplay_slots / 2; i++)
+            v->selfPlay.emplace_back(new Env(v->world.get(), maps[(size_t)(2 * i)], true, BOT_PASSIVE, seed + (uint64_t)(2 * i)));
+        for (int j = 0; j < n_bot_envs; j++)
+            v->bots.emplace_back(new Env(v->world.get(), maps[(size_t)(n_selfplay_slots + j)], false,
+                                         (BotKind)(bot_kinds ? bot_kinds[j] : 0), seed + (uint64_t)(n_selfplay_slots + j)));
+        v->envSteps.assign((size_t)nslots, 0);
+        return v;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+
+void oref_destroy(void* h) { delete (VecClient*)h; }
+
+int oref_dims(void* h, int32_t* slots, int32_t* H, int32_t* W, int32_t* C, int32_t* K) {
+    auto v = (VecClient*)h;
+    *slots = v->nSlots();
+    *H = v->world->H;
+    *W = v->world->W;
+    *C = v->world->C;
+    *K = v->world->K;
+    return 0;
+}
+
+int oref_reset(void* h, const int32_t* players, int32_t* obs, double* reward, uint8_t* done) {
+    try {
+        auto v = (VecClient*)h;
+        v->reset(players);
+        v->collect(obs, reward, done);
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -22;
+    }
+}
+
+int oref_step(void* h, const int32_t* actions, const int32_t* players, int32_t* obs, double* reward, uint8_t* done) {
+    try {
+        auto v = (VecClient*)h;
+        v->step(actions, players);
+        v->collect(obs, reward, done);
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -22;
+    }
+}
+
+int oref_get_masks(void* h, int player, uint8_t* out) {
+    try {
+        ((VecClient*)h)->masks(player, out);
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -22;
+    }
+}
+
+// Canonical dump of the game behind slot s (ref_cpu.hpp dumpState)
+int oref_dump_state(void* h, int slot, int32_t* buf, int cap) {
+    auto v = (VecClient*)h;
+    int p;
+    Env* e = v->slotEnv(slot, &p);
+    auto d = dumpState(*e->gs);
+    if ((int)d.size() > cap) return -(int)d.size();
+    std::memcpy(buf, d.data(), d.size() * sizeof(int32_t));
+    return (int)d.size();
+}
+
+int oref_env_steps(void* h, int slot) { return ((VecClient*)h)->envSteps[(size_t)slot]; }
+int oref_errors(void* h, int slot) {
+    int p;
+    return ((VecClient*)h)->slotEnv(slot, &p)->gs->errors;
+}
+
+// ------------------------------------------------ bot-vs-bot client (config 1; tests/JNIBotClient.java)
+struct BotVec {
+    std::unique_ptr<World> world;
+    MapTemplate map;
+    GSP gs;
+    JavaRandom gen;  // util/Sampler.java:17 — one JVM-global generator shared by both AIs
+    std::unique_ptr<AI> ai1, ai2;
+    int envSteps = 0, maxSteps = 2000;
+};
+
+void* oref_botclient_create(const char* map_path, int ai1, int ai2, int max_steps, int utt_version, int crs, int64_t seed) {
+    try {
+        auto b = new BotVec();
+        b->world.reset(new World(utt_version, crs));
+        b->map = loadMapFile(map_path);
+        b->world->H = b->map.height;
+        b->world->W = b->map.width;
+        b->gen.setSeed(seed);
+        b->maxSteps = max_steps;
+        auto mk = [&](int k) -> AI* { return k == BOT_PASSIVE ? (AI*)new PassiveAI() : (AI*)new RandomBiasedAI(&b->gen); };
+        b->ai1.reset(mk(ai1));
+        b->ai2.reset(mk(ai2));
+        b->gs = std::make_shared<GameState>(instantiate(b->map, b->world->utt), &b->world->utt);
+        return b;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+void oref_botclient_destroy(void* h) { delete (BotVec*)h; }
+// JNIBotClient.gameStep (:108-135) + VecClient bot-only auto-reset (:214-238); returns 0
+int oref_botclient_step(void* h, int player, double* reward, uint8_t* done) {
+    try {
+        auto b = (BotVec*)h;
+        PlayerAction pa1 = b->ai1->getAction(player, *b->gs);
+        PlayerAction pa2 = b->ai2->getAction(1 - player, *b->gs);
+        b->gs->issueSafe(pa1);
+        b->gs->issueSafe(pa2);
+        b->gs->cycle();
+        winLoss(*b->gs, player, *reward, *done);
+        b->envSteps++;
+        if (*done || b->envSteps >= b->maxSteps) {
+            b->gs = std::make_shared<GameState>(instantiate(b->map, b->world->utt), &b->world->utt);
+            *done = 1;
+            b->envSteps = 0;
+        }
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -22;
+    }
+}
+int oref_botclient_dump(void* h, int32_t* buf, int cap) {
+    auto d = dumpState(*((BotVec*)h)->gs);
+    if ((int)d.size() > cap) return -(int)d.size();
+    std::memcpy(buf, d.data(), d.size() * sizeof(int32_t));
+    return (int)d.size();
+}
+
+// ------------------------------------------------ strict trace replay
+// Fixture text (tests/golden/make_trace_fixtures.py): see that script's docstring.
+// Replays like TestTracesIntegrity.testTrace and additionally compares the full
+// PhysicalGameState with each entry's snapshot.  Returns #entries checked (>=0)
+// or -1 with a message.
+int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int msglen) {
+    auto fail = [&](const std::string& s) {
+        std::snprintf(msg, (size_t)msglen, "%s", s.c_str());
+        return -1;
+    };
+    try {
+        UnitTypeTable utt(1, 1);
+        MapTemplate m = loadMapFile(map_path);
+        GameState gs(instantiate(m, utt), &utt);
+        std::istringstream in(fixture);
+        std::string tok;
+        int nentries;
+        in >> tok >> nentries;
+        if (tok != "TRACE") return fail("bad fixture header");
+        bool gameOver = false;
+        int checked = 0;
+        for (int e = 0; e < nentries; e++) {
+            int time, r0, r1, nu;
+            in >> tok >> time;
+            if (tok != "E") return fail("bad entry");
+            in >> tok >> r0 >> r1;
+            in >> tok >> nu;
+            auto tp = std::make_shared<PhysicalGameState>();
+            tp->width = m.width;
+            tp->height = m.height;
+            tp->terrain = gs.pgs->terrain;
+            tp->players.push_back(std::make_shared<Player>(Player{0, r0}));
+            tp->players.push_back(std::make_shared<Player>(Player{1, r1}));
+            std::vector<UnitP> tunits;
+            for (int i = 0; i < nu; i++) {
+                auto u = std::make_shared<Unit>();
+                int t;
+                in >> tok >> t >> u->ID >> u->player >> u->x >> u->y >> u->resources >> u->hitpoints;
+                u->type = utt.getUnitType(t);
+                tp->units.push_back(u);
+            }
+            int na;
+            in >> tok >> na;
+            struct TA { int64_t id; int type, param, x, y, ut; };
+            std::vector<TA> tas((size_t)na);
+            for (auto& a : tas) in >> tok >> a.id >> a.type >> a.param >> a.x >> a.y >> a.ut;
+            // TestTracesIntegrity.java:83-86
+            while (gs.time < time) {
+                if (gameOver) return fail("game over before entry time " + std::to_string(time));
+                gameOver = gs.cycle();
+            }
+            // STRICT: full pgs equality (stronger than the reference's own test)
+            const PhysicalGameState& p = *gs.pgs;
+            std::ostringstream why;
+            if (p.players[0]->resources != r0 || p.players[1]->resources != r1)
+                why << "player resources " << p.players[0]->resources << "," << p.players[1]->resources << " vs " << r0 << "," << r1;
+            else if ((int)p.units.size() != nu)
+                why << "unit count " << p.units.size() << " vs " << nu;
+            else
+                for (int i = 0; i < nu; i++) {
+                    const Unit& a = *p.units[(size_t)i];
+                    const Unit& b = *tp->units[(size_t)i];
+                    if (a.type->ID != b.type->ID || a.player != b.player || a.x != b.x || a.y != b.y || a.hitpoints != b.hitpoints ||
+                        a.resources != b.resources) {
+                        why << "unit " << i << " (" << a.type->name << " p" << a.player << " @" << a.x << "," << a.y << " hp" << a.hitpoints
+                            << " r" << a.resources << ") vs (" << b.type->name << " p" << b.player << " @" << b.x << "," << b.y << " hp"
+                            << b.hitpoints << " r" << b.resources << ")";
+                        break;
+                    }
+                }
+            if (!why.str().empty()) return fail("time " + std::to_string(time) + ": " + why.str());
+            checked++;
+            if (!tas.empty()) {  // :101-125
+                bool containsRealActions = false;
+                PlayerAction p1, p2;
+                for (auto& a : tas) {
+                    UnitP tu;
+                    for (auto& u : tp->units)
+                        if (u->ID == a.id) { tu = u; break; }
+                    if (!tu) return fail("undefined unit ID in trace action");
+                    auto ua = std::make_shared<UnitAction>(a.type, a.param);
+                    ua->x = a.x;
+                    ua->y = a.y;
+                    ua->unitType = a.ut >= 0 ? utt.getUnitType(a.ut) : nullptr;
+                    if (tu->player == 0) p1.addUnitAction(tu, ua);
+                    else if (tu->player == 1) p2.addUnitAction(tu, ua);
+                    else return fail("action for a non-player unit");
+                    containsRealActions = containsRealActions || ua->type != UnitAction::TYPE_NONE;
+                }
+                bool issued = gs.issueSafe(p1);
+                issued = gs.issueSafe(p2) || issued;
+                if (containsRealActions != issued) return fail("containsRealActions != issuedActions at time " + std::to_string(time));
+            }
+        }
+        return checked;
+    } catch (std::exception& e) {
+        return fail(std::string("exception: ") + e.what());
+    }
+}
+
+// ------------------------------------------------ CPU baseline: VecClient + random policy,
+// `threads` std::threads each stepping a disjoint shard of games (cores = threads).
+// Returns env-steps executed; *seconds = wall time of the timed region.
+double oref_bench(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int with_masks) {
+    std::vector<void*> hs((size_t)threads);
+    std::vector<int> per((size_t)threads);
+    for (int t = 0; t < threads; t++) {
+        per[(size_t)t] = n_games / threads + (t < n_games % threads ? 1 : 0);
+        std::vector<const char*> paths((size_t)per[(size_t)t] * 2, map_path);
+        hs[(size_t)t] = oref_create(per[(size_t)t] * 2, 0, nullptr, 2000, 0, 1, 1, paths.data(), seed + (uint64_t)t * 1000003ULL);
+        oref_reset(hs[(size_t)t], nullptr, nullptr, nullptr, nullptr);
+    }
+    auto worker = [&](int t) {
+        void* h = hs[(size_t)t];
+        int32_t S, H, W, C, K;
+        oref_dims(h, &S, &H, &W, &C, &K);
+        std::vector<uint8_t> masks((size_t)S * H * W * K);
+        std::vector<int32_t> acts((size_t)S * H * W * 7), obs((size_t)S * C * H * W);
+        std::vector<double> rew((size_t)S);
+        std::vector<uint8_t> done((size_t)S);
+        for (int k = 0; k < steps; k++) {
+            oref_get_masks(h, 0, masks.data());
+            for (int s = 0; s < S; s++)
+                oref_policy(masks.data() + (size_t)s * H * W * K, H * W, K, 7, seed, (uint32_t)(t * 100000 + s / 2), (uint32_t)k,
+                            (uint32_t)(s & 1), acts.data() + (size_t)s * H * W * 7);
+            oref_step(h, acts.data(), nullptr, obs.data(), rew.data(), done.data());
+        }
+        (void)with_masks;
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; t++) th.emplace_back(worker, t);
+    for (auto& x : th) x.join();
+    auto t1 = std::chrono::steady_clock::now();
+    for (auto h : hs) oref_destroy(h);
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+}  // extern "C"

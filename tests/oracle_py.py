@@ -1,0 +1,125 @@
+"""ctypes binding of the CPU oracle (oracle/build/liboref.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "build", "liboref.so")
+_lib = None
+
+BOT_PASSIVE, BOT_RANDOM_BIASED = 0, 1
+
+
+def build():
+    srcs = [os.path.join(ROOT, "oracle", f) for f in ("ref_cpu.cpp", "ref_cpu.hpp", "oracle_capi.cpp", "Makefile")]
+    if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in srcs):
+        return LIB
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    return LIB
+
+
+def load():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        P, I, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
+        L.oref_create.restype = P
+        L.oref_create.argtypes = [I, I, P, I, I, I, I, P, U64]
+        L.oref_destroy.argtypes = [P]
+        L.oref_dims.argtypes = [P, P, P, P, P, P]
+        L.oref_reset.argtypes = [P, P, P, P, P]
+        L.oref_step.argtypes = [P, P, P, P, P, P]
+        L.oref_get_masks.argtypes = [P, I, P]
+        L.oref_dump_state.argtypes = [P, I, P, I]
+        L.oref_env_steps.argtypes = [P, I]
+        L.oref_errors.argtypes = [P, I]
+        L.oref_last_error.restype = ctypes.c_char_p
+        L.oref_trace_replay.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, I]
+        L.oref_policy.argtypes = [P, I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P]
+        L.oref_botclient_create.restype = P
+        L.oref_botclient_create.argtypes = [ctypes.c_char_p, I, I, I, I, I, ctypes.c_int64]
+        L.oref_botclient_destroy.argtypes = [P]
+        L.oref_botclient_step.argtypes = [P, I, P, P]
+        L.oref_botclient_dump.argtypes = [P, P, I]
+        L.oref_bench.restype = ctypes.c_double
+        L.oref_bench.argtypes = [ctypes.c_char_p, I, I, I, U64, I]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class OracleVecClient:
+    """Mirror of tests.JNIGridnetVecClient (src/tests/JNIGridnetVecClient.java) on the CPU oracle."""
+
+    def __init__(self, n_selfplay_slots, n_bot_envs, max_steps, map_paths, partial_obs=False, utt_version=1, crs=1,
+                 bot_kinds=None, seed=0):
+        L = load()
+        self.L = L
+        paths = (ctypes.c_char_p * len(map_paths))(*[os.path.join(ROOT, p).encode() for p in map_paths])
+        bk = np.asarray(bot_kinds if bot_kinds is not None else [0] * n_bot_envs, dtype=np.int32)
+        self.h = L.oref_create(n_selfplay_slots, n_bot_envs, _ptr(bk) if n_bot_envs else None, max_steps, int(partial_obs),
+                               utt_version, crs, ctypes.cast(paths, ctypes.c_void_p), seed)
+        if not self.h:
+            raise RuntimeError(L.oref_last_error().decode())
+        d = [ctypes.c_int32() for _ in range(5)]
+        L.oref_dims(self.h, *[ctypes.byref(x) for x in d])
+        self.S, self.H, self.W, self.C, self.K = [x.value for x in d]
+        self.obs = np.zeros((self.S, self.C, self.H, self.W), np.int32)
+        self.reward = np.zeros((self.S,), np.float64)
+        self.done = np.zeros((self.S,), np.uint8)
+
+    def _chk(self, r):
+        if r != 0:
+            raise RuntimeError(self.L.oref_last_error().decode())
+
+    def reset(self, players=None):
+        p = np.asarray(players, np.int32) if players is not None else None
+        self._chk(self.L.oref_reset(self.h, _ptr(p), _ptr(self.obs), _ptr(self.reward), _ptr(self.done)))
+        return self.obs.copy(), self.reward.copy(), self.done.copy()
+
+    def step(self, actions, players=None):
+        a = np.ascontiguousarray(actions, dtype=np.int32).reshape(self.S, self.H * self.W, 7)
+        p = np.asarray(players, np.int32) if players is not None else None
+        self._chk(self.L.oref_step(self.h, _ptr(a), _ptr(p), _ptr(self.obs), _ptr(self.reward), _ptr(self.done)))
+        return self.obs.copy(), self.reward.copy(), self.done.copy()
+
+    def get_masks(self, player=0):
+        m = np.zeros((self.S, self.H, self.W, self.K), np.uint8)
+        self._chk(self.L.oref_get_masks(self.h, player, _ptr(m)))
+        return m
+
+    def dump(self, slot):
+        buf = np.zeros(1 << 16, np.int32)
+        n = self.L.oref_dump_state(self.h, slot, _ptr(buf), buf.size)
+        assert n >= 0
+        return buf[:n].copy()
+
+    def env_steps(self, slot):
+        return self.L.oref_env_steps(self.h, slot)
+
+    def close(self):
+        if self.h:
+            self.L.oref_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+
+def policy(mask, seed, env_id, step, player, n_types=7):
+    """Philox masked-uniform policy (bit-identical to the GPU policy kernel). mask: u8[H,W,K]."""
+    L = load()
+    H, W, K = mask.shape
+    m = np.ascontiguousarray(mask, np.uint8)
+    out = np.zeros((H * W, 7), np.int32)
+    L.oref_policy(_ptr(m), H * W, K, n_types, seed, env_id, step, player, _ptr(out))
+    return out
