@@ -1,0 +1,113 @@
+/*
+ * mrts.h — C ABI of libmrts.so, the MI355X (gfx950) vectorised microRTS env step.
+ *
+ * Drop-in boundary for tests.JNIGridnetVecClient (reference src/tests/JNIGridnetVecClient.java:17-335).
+ * Every entry point names the Java member it replaces.  Plain C: no C++ types, no exceptions,
+ * no torch types.  A handle lives on ONE HIP device and owns ONE HIP stream; it is not thread-safe
+ * (the Java client is single-threaded too, JNIGridnetVecClient.java:11-13).
+ *
+ * Slot layout (JNIGridnetVecClient.java:106-142): slots [0, n_selfplay_slots) belong to self-play
+ * games (game i = slots 2i, 2i+1 = players 0, 1; map = map_paths[2i], :119), then one slot per
+ * agent-vs-bot env (map = map_paths[n_selfplay_slots + j], :123).
+ *
+ * Actions (gameStep's int[][][] action, :213): int32 [n_slots][H*W][7], row r = the unit at cell r
+ * (x = r % W, y = r / W); components [type, move dir, harvest dir, return dir, produce dir,
+ * produce type, attack index] (rts/UnitAction.java:663-664,675-709).  This is exactly the Java row
+ * [pos, ...] with pos = r, in ascending cell order — the MicroRTS-Py gridnet contract.
+ *
+ * Errors: 0 on success, a negative errno on failure; mrts_last_error() (thread-local) says why.
+ * Java exceptions of the reference become errors: an out-of-range produce type in a decoded row
+ * (UnitAction.java:697) → -EINVAL after the step; unit-capacity overflow or an addUnit collision
+ * (PhysicalGameState.java:189-201) → -ENOSPC / -EFAULT.  Per-game detail in mrts_error_flags().
+ */
+#ifndef MRTS_H
+#define MRTS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mrts_env mrts_env;
+
+enum { MRTS_BOT_PASSIVE = 0, MRTS_BOT_RANDOM_BIASED = 1 };
+
+/* per-game error flag bits (mrts_error_flags) */
+enum {
+    MRTS_ERR_CAPACITY = 1u << 0,      /* unit slots exhausted (no Java equivalent; env must be reset) */
+    MRTS_ERR_ADDUNIT = 1u << 1,       /* produce into an occupied cell: Java throws (PhysicalGameState.java:192) */
+    MRTS_ERR_PRODUCE_TYPE = 1u << 2,  /* decoded produce type out of range: Java throws (UnitAction.java:697) */
+    MRTS_ERR_OLDER_CONFLICT = 1u << 3,/* issue() older-conflict branch: Java prints (GameState.java:298-317) */
+    MRTS_ERR_NEG_RESOURCES = 1u << 4, /* produce skipped at execution: Java prints (UnitAction.java:457-461) */
+    MRTS_ERR_MOVE_COLLISION = 1u << 5 /* internal invariant (one unit per cell) violated */
+};
+
+typedef struct {
+    int32_t n_selfplay_slots;   /* a_num_selfplayenvs (:106), even */
+    int32_t n_bot_envs;         /* a_num_envs (:106) */
+    int32_t max_steps;          /* a_max_steps (:106) */
+    int32_t partial_obs;        /* partial_obs (:107) — 8 observation planes when set */
+    int32_t utt_version;        /* new UnitTypeTable(version, crs): 1 ORIGINAL, 2 FINETUNED, 3 NON_DETERMINISTIC */
+    int32_t conflict_policy;    /* 1 CANCEL_BOTH, 2 CANCEL_RANDOM, 3 CANCEL_ALTERNATING (UnitTypeTable.java:46-57) */
+    const int32_t* bot_kinds;   /* a_ai2s (:107): per bot env, MRTS_BOT_* ; NULL = all passive */
+    const char* const* map_paths; /* a_mapPaths (:106): one per slot */
+    int32_t device;             /* HIP device ordinal */
+    uint64_t seed;              /* seeds the per-game java.util.Random streams */
+    int32_t slot_id_base;       /* global id of this handle's slot 0 (multi-GPU: disjoint RNG streams) */
+} mrts_config;
+
+typedef struct {               /* ai/jni/Responses.java:12-30 (one reward function: WinLoss) */
+    const int32_t* obs;        /* [n_slots][C][H][W] */
+    const double* reward;      /* [n_slots][1] */
+    const uint8_t* done;       /* [n_slots][1] */
+} mrts_responses;
+
+/* new JNIGridnetVecClient(...) (:106-142).  Parses the XML maps (PhysicalGameState.java:700-726). */
+int mrts_create(const mrts_config* cfg, mrts_env** out);
+/* storage sizes (:127-133): slots, map H/W, observation planes C (6 or 8), mask slots K (79) */
+int mrts_dims(const mrts_env* env, int32_t* n_slots, int32_t* H, int32_t* W, int32_t* C, int32_t* K);
+
+/* Host-pointer API (mirrors the Java reuse semantics: returned arrays are library-owned and valid
+ * until the next call on the handle, GameState.java:923-925 / JNIGridnetClient.java:211-215). */
+int mrts_reset(mrts_env* env, const int32_t* players, mrts_responses* out);                       /* reset(int[]) :179-211 */
+int mrts_step(mrts_env* env, const int32_t* actions, const int32_t* players, mrts_responses* out); /* gameStep :213-297 */
+int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out /* [n_slots][H][W][K] */);          /* getMasks :307-316 */
+
+/* Device-pointer API: same semantics, caller-owned HBM buffers, stream-ordered on `stream`
+ * (a hipStream_t; NULL = the handle's own stream), no host synchronisation. d_players may be NULL
+ * (all zeros).  d_masks may be NULL; when given, the masks getMasks(mask_player) would return after
+ * this call are written too (fused, saves a launch). */
+int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
+                   uint8_t* d_masks, int32_t mask_player, void* stream);
+int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                  uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream);
+int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stream);
+
+/* Synthetic masked-uniform random policy (bench / rollouts): per own idle cell a uniform action
+ * type among the mask's set type bits, then a uniform parameter among that type's set bits
+ * (Philox4x32-10, key = seed, counter = (slot_id_base + slot, step, cell, 0)).  d_masks as written
+ * by the calls above; d_actions = [n_slots][H*W][7]. */
+int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, uint64_t seed, uint32_t step, int32_t* d_actions, void* stream);
+
+/* Canonical state dump of the game behind `slot` (same format as the CPU oracle's dumpState):
+ * [time, 2, res0, res1, n_units, (type, player, x, y, hp, resources)*, n_assignments,
+ *  (unit index, action type, parameter, x, y, unit type or -1, issue time)*] — units in
+ * PhysicalGameState list order, assignments in LinkedHashMap insertion order.  Synchronous.
+ * Returns the number of int32 written, or -(needed) when cap is too small. */
+int mrts_get_state(mrts_env* env, int32_t slot, int32_t* buf, int32_t cap);
+/* per-game error flags (MRTS_ERR_*), one uint32 per slot; synchronous */
+int mrts_error_flags(mrts_env* env, uint32_t* flags);
+/* per-slot envSteps (JNIGridnetVecClient.envSteps, :27); synchronous */
+int mrts_env_steps(mrts_env* env, int32_t* out);
+/* the handle's hipStream_t */
+void* mrts_stream(mrts_env* env);
+/* close() (:318-334) + free */
+void mrts_destroy(mrts_env* env);
+const char* mrts_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRTS_H */

@@ -1,0 +1,84 @@
+"""ctypes binding of libmrts.so (include/mrts.h).  The product path is GPU-only: if the HIP
+library is missing this module raises — there is no CPU fallback."""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmrts.so")
+
+MRTS_BOT_PASSIVE, MRTS_BOT_RANDOM_BIASED = 0, 1
+ERR_BITS = {
+    1 << 0: "CAPACITY", 1 << 1: "ADDUNIT", 1 << 2: "PRODUCE_TYPE", 1 << 3: "OLDER_CONFLICT",
+    1 << 4: "NEG_RESOURCES", 1 << 5: "MOVE_COLLISION",
+}
+
+# every symbol include/mrts.h declares
+EXPORTS = [
+    "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_reset_dev", "mrts_step_dev",
+    "mrts_get_masks_dev", "mrts_policy_dev", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_destroy", "mrts_last_error",
+]
+
+
+class MrtsConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_selfplay_slots", ctypes.c_int32),
+        ("n_bot_envs", ctypes.c_int32),
+        ("max_steps", ctypes.c_int32),
+        ("partial_obs", ctypes.c_int32),
+        ("utt_version", ctypes.c_int32),
+        ("conflict_policy", ctypes.c_int32),
+        ("bot_kinds", ctypes.POINTER(ctypes.c_int32)),
+        ("map_paths", ctypes.POINTER(ctypes.c_char_p)),
+        ("device", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("slot_id_base", ctypes.c_int32),
+    ]
+
+
+class MrtsResponses(ctypes.Structure):
+    _fields_ = [
+        ("obs", ctypes.POINTER(ctypes.c_int32)),
+        ("reward", ctypes.POINTER(ctypes.c_double)),
+        ("done", ctypes.POINTER(ctypes.c_uint8)),
+    ]
+
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load libmrts.so; raises ImportError (loudly) when the HIP extension has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"libmrts.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (no CPU fallback exists)")
+    L = ctypes.CDLL(path)
+    P, I32, U32, U64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+    L.mrts_create.argtypes = [ctypes.POINTER(MrtsConfig), ctypes.POINTER(P)]
+    L.mrts_create.restype = ctypes.c_int
+    L.mrts_dims.argtypes = [P, P, P, P, P, P]
+    L.mrts_reset.argtypes = [P, P, ctypes.POINTER(MrtsResponses)]
+    L.mrts_step.argtypes = [P, P, P, ctypes.POINTER(MrtsResponses)]
+    L.mrts_get_masks.argtypes = [P, I32, P]
+    L.mrts_reset_dev.argtypes = [P, P, P, P, P, P, I32, P]
+    L.mrts_step_dev.argtypes = [P, P, P, P, P, P, P, I32, P]
+    L.mrts_get_masks_dev.argtypes = [P, I32, P, P]
+    L.mrts_policy_dev.argtypes = [P, P, U64, U32, P, P]
+    L.mrts_get_state.argtypes = [P, I32, P, I32]
+    L.mrts_error_flags.argtypes = [P, P]
+    L.mrts_env_steps.argtypes = [P, P]
+    L.mrts_stream.argtypes = [P]
+    L.mrts_stream.restype = P
+    L.mrts_destroy.argtypes = [P]
+    L.mrts_destroy.restype = None
+    L.mrts_last_error.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(f"mrts error {rc}: {load().mrts_last_error().decode()}")

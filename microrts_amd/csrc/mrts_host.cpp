@@ -1,0 +1,694 @@
+// mrts_host.cpp — host runtime behind include/mrts.h: map parsing, unit-type tables, per-game
+// state allocation in HBM, kernel launches, the Java-compatible host-pointer API and the
+// canonical state dump.  Compiled by hipcc into microrts_amd/libmrts.so.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/mrts.h"
+#include "mrts_internal.h"
+
+using namespace mrts;
+
+namespace mrts {
+size_t ldsBytes(int HW, int W, int CAP);
+hipError_t launchEnv(int mode, const KParams& P, hipStream_t stream);
+hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream);
+hipError_t prepareLds(size_t bytes);
+}  // namespace mrts
+
+static thread_local std::string g_err;
+
+namespace {
+
+struct Fail {
+    int code;
+    std::string msg;
+};
+#define HIPCHK(x)                                                                         \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) throw Fail{-EIO, std::string(#x) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+
+// ------------------------------------------------------------------ unit type tables
+// new UnitTypeTable(version, crs) — reference src/rts/units/UnitTypeTable.java:104-289
+static const char* kTypeNames[7] = {"Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"};
+
+DevUtt makeUtt(int version, int crs) {
+    if (version < 1 || version > 3) throw Fail{-EINVAL, "utt_version must be 1, 2 or 3"};
+    if (crs < 1 || crs > 3) throw Fail{-EINVAL, "conflict_policy must be 1, 2 or 3"};
+    DevUtt u;
+    std::memset(&u, 0, sizeof(u));
+    u.ntypes = 7;
+    for (int t = 0; t < 7; t++) {  // UnitType defaults (rts/units/UnitType.java:33-100)
+        u.cost[t] = 1;
+        u.hp[t] = 1;
+        u.minD[t] = u.maxD[t] = 1;
+        u.range[t] = 1;
+        u.produceT[t] = u.moveT[t] = u.attackT[t] = u.harvestT[t] = 10;
+        u.harvestAmt[t] = 1;
+        u.sight[t] = 4;
+        u.flags[t] = F_MOVE | F_ATTACK;
+    }
+    const bool v1 = version == 1, v2 = version == 2, v3 = version == 3;
+    // Resource
+    u.flags[0] = F_RESOURCE;
+    u.sight[0] = 0;
+    // Base
+    u.cost[1] = 10; u.hp[1] = 10;
+    if (v1) u.produceT[1] = 250;
+    else if (v2) u.produceT[1] = 200;
+    u.flags[1] = F_STOCKPILE;
+    u.sight[1] = 5;
+    // Barracks
+    u.cost[2] = 5; u.hp[2] = 4;
+    u.produceT[2] = v1 ? 200 : 100;
+    u.flags[2] = 0;
+    u.sight[2] = 3;
+    // Worker
+    u.cost[3] = 1; u.hp[3] = 1;
+    if (v3) { u.minD[3] = 0; u.maxD[3] = 2; }
+    u.range[3] = 1; u.produceT[3] = 50; u.moveT[3] = 10; u.attackT[3] = 5; u.harvestT[3] = 20;
+    u.flags[3] = F_HARVEST | F_MOVE | F_ATTACK;
+    u.sight[3] = 3;
+    // Light
+    u.cost[4] = 2; u.hp[4] = 4;
+    if (v3) { u.minD[4] = 1; u.maxD[4] = 3; } else { u.minD[4] = u.maxD[4] = 2; }
+    u.produceT[4] = 80; u.moveT[4] = 8; u.attackT[4] = 5;
+    u.flags[4] = F_MOVE | F_ATTACK;
+    u.sight[4] = 2;
+    // Heavy
+    if (v3) { u.minD[5] = 0; u.maxD[5] = 6; } else { u.minD[5] = u.maxD[5] = 4; }
+    u.produceT[5] = 120;
+    if (v1) { u.moveT[5] = 12; u.hp[5] = 4; u.cost[5] = 2; } else { u.moveT[5] = 10; u.hp[5] = 8; u.cost[5] = 3; }
+    u.attackT[5] = 5;
+    u.flags[5] = F_MOVE | F_ATTACK;
+    u.sight[5] = 2;
+    // Ranged
+    u.cost[6] = 2; u.hp[6] = 1;
+    if (v3) { u.minD[6] = 1; u.maxD[6] = 2; }
+    u.range[6] = 3; u.produceT[6] = 100; u.moveT[6] = 10; u.attackT[6] = 5;
+    u.flags[6] = F_MOVE | F_ATTACK;
+    u.sight[6] = 3;
+    // produces lists, in declaration order (:283-288)
+    u.nprod[1] = 1; u.prod[1][0] = 3;
+    u.nprod[2] = 3; u.prod[2][0] = 4; u.prod[2][1] = 5; u.prod[2][2] = 6;
+    u.nprod[3] = 2; u.prod[3][0] = 1; u.prod[3][1] = 2;
+    u.crs = crs;
+    int maxRange = 0;
+    for (int t = 0; t < 7; t++) maxRange = std::max(maxRange, u.range[t]);
+    u.maxAttackRadius = 2 * maxRange + 1;
+    u.K = 1 + 6 + 4 + 4 + 4 + 4 + u.ntypes + u.maxAttackRadius * u.maxAttackRadius;
+    return u;
+}
+
+// ------------------------------------------------------------------ XML map reader
+// rts/PhysicalGameState.java:700-726 (fromXML), :765-777 + :577-607 (terrain, raw or A/B RLE),
+// rts/units/Unit.java:597-620 (unit attributes).
+struct MapDef {
+    int W = 0, H = 0;
+    std::vector<uint8_t> terrain;
+    int res[2] = {0, 0};
+    struct U { int type, player, x, y, res, hp; long long id; };
+    std::vector<U> units;
+};
+
+std::string attrOf(const std::string& tag, const char* name) {
+    const std::string key(name);
+    size_t p = 0;
+    while ((p = tag.find(key, p)) != std::string::npos) {
+        const bool start = p == 0 || isspace((unsigned char)tag[p - 1]);
+        size_t q = p + key.size();
+        while (q < tag.size() && isspace((unsigned char)tag[q])) q++;
+        if (start && q < tag.size() && tag[q] == '=') {
+            q++;
+            while (q < tag.size() && isspace((unsigned char)tag[q])) q++;
+            if (q < tag.size() && tag[q] == '"') {
+                const size_t e = tag.find('"', q + 1);
+                return tag.substr(q + 1, e - q - 1);
+            }
+        }
+        p += key.size();
+    }
+    throw Fail{-EINVAL, std::string("map: missing attribute ") + name};
+}
+
+int toInt(const std::string& s) {
+    try {
+        return std::stoi(s);
+    } catch (...) {
+        throw Fail{-EINVAL, "map: bad integer '" + s + "'"};
+    }
+}
+
+MapDef parseMap(const std::string& path) {
+    std::ifstream f(path);
+    if (!f) throw Fail{-ENOENT, "cannot open map " + path};
+    std::stringstream ss;
+    ss << f.rdbuf();
+    const std::string x = ss.str();
+    MapDef m;
+    size_t p = x.find("<rts.PhysicalGameState");
+    if (p == std::string::npos) throw Fail{-EINVAL, "map: no rts.PhysicalGameState in " + path};
+    size_t e = x.find('>', p);
+    const std::string root = x.substr(p, e - p);
+    m.W = toInt(attrOf(root, "width"));
+    m.H = toInt(attrOf(root, "height"));
+    if (m.W <= 0 || m.H <= 0 || m.W > 250 || m.H > 250) throw Fail{-EINVAL, "map: unsupported size"};
+    const size_t t0 = x.find("<terrain>", e), t1 = x.find("</terrain>", t0);
+    if (t0 == std::string::npos || t1 == std::string::npos) throw Fail{-EINVAL, "map: no terrain"};
+    const std::string ts = x.substr(t0 + 9, t1 - t0 - 9);
+    const int HW = m.W * m.H;
+    std::vector<int> terr;
+    if (ts.find('A') != std::string::npos || ts.find('B') != std::string::npos) {
+        std::string counter;
+        for (char ch : ts) {
+            if (ch == 'A' || ch == 'B') {
+                if (!counter.empty()) {
+                    const int n = toInt(counter);
+                    for (int i = 0; i < n - 1; i++) terr.push_back(terr.back());
+                    counter.clear();
+                }
+                terr.push_back(ch == 'A' ? 0 : 1);
+            } else if (!isspace((unsigned char)ch)) {
+                counter.push_back(ch);
+            }
+        }
+        if (!counter.empty()) {
+            const int n = toInt(counter);
+            for (int i = 0; i < n - 1; i++) terr.push_back(terr.back());
+        }
+    } else {
+        for (char ch : ts)
+            if (!isspace((unsigned char)ch)) terr.push_back(ch - '0');
+    }
+    if ((int)terr.size() < HW) throw Fail{-EINVAL, "map: terrain too short"};
+    m.terrain.resize((size_t)HW);
+    for (int i = 0; i < HW; i++) m.terrain[(size_t)i] = terr[(size_t)i] != 0;
+    const size_t end = x.find("</rts.PhysicalGameState>", t1);
+    size_t q = t1;
+    int np = 0;
+    while (true) {
+        const size_t a = x.find("<rts.Player", q);
+        if (a == std::string::npos || a > end) break;
+        const size_t b = x.find('>', a);
+        const std::string pt = x.substr(a, b - a);
+        const int id = toInt(attrOf(pt, "ID"));
+        if (id != np || np >= 2) throw Fail{-EINVAL, "map: players must be 0 and 1 in order"};
+        m.res[np++] = toInt(attrOf(pt, "resources"));
+        q = b;
+    }
+    if (np != 2) throw Fail{-EINVAL, "map: need exactly 2 players"};
+    q = t1;
+    std::vector<long long> ids;
+    std::vector<uint8_t> occ((size_t)HW, 0);
+    while (true) {
+        const size_t a = x.find("<rts.units.Unit ", q);
+        if (a == std::string::npos || a > end) break;
+        const size_t b = x.find('>', a);
+        const std::string ut = x.substr(a, b - a);
+        MapDef::U u;
+        const std::string tn = attrOf(ut, "type");
+        u.type = -1;
+        for (int t = 0; t < 7; t++)
+            if (tn == kTypeNames[t]) u.type = t;
+        if (u.type < 0) throw Fail{-EINVAL, "map: unknown unit type " + tn};
+        u.id = std::stoll(attrOf(ut, "ID"));
+        u.player = toInt(attrOf(ut, "player"));
+        u.x = toInt(attrOf(ut, "x"));
+        u.y = toInt(attrOf(ut, "y"));
+        u.res = toInt(attrOf(ut, "resources"));
+        u.hp = toInt(attrOf(ut, "hitpoints"));
+        if (u.player < -1 || u.player > 1) throw Fail{-EINVAL, "map: unit player out of range"};
+        if (u.x < 0 || u.y < 0 || u.x >= m.W || u.y >= m.H) throw Fail{-EINVAL, "map: unit off the map"};
+        if (u.res < -32768 || u.res > 32767 || u.hp < -32768 || u.hp > 32767) throw Fail{-EINVAL, "map: value exceeds int16"};
+        if (std::find(ids.begin(), ids.end(), u.id) != ids.end()) throw Fail{-EINVAL, "map: repeated unit ID"};
+        if (occ[(size_t)(u.y * m.W + u.x)]) throw Fail{-EINVAL, "map: two units in one position"};  // addUnit :192
+        occ[(size_t)(u.y * m.W + u.x)] = 1;
+        ids.push_back(u.id);
+        m.units.push_back(u);
+        q = b;
+    }
+    return m;
+}
+
+}  // namespace
+
+struct mrts_env {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int H = 0, W = 0, HW = 0, CAP = 0, C = 6, K = 79;
+    int nSlots = 0, nGames = 0, nSpGames = 0, maxSteps = 0, partialObs = 0;
+    uint32_t slotIdBase = 0;
+    DevUtt utt;
+    std::vector<int> tmplOffHost;
+    int32_t* d_state = nullptr;
+    int32_t* d_tmpl = nullptr;
+    int32_t* d_tmplOff = nullptr;
+    int32_t* d_botKind = nullptr;
+    // library-owned buffers for the host-pointer API
+    int32_t* d_actions = nullptr;
+    int32_t* d_players = nullptr;
+    int32_t* d_obs = nullptr;
+    double* d_reward = nullptr;
+    uint8_t* d_done = nullptr;
+    uint8_t* d_masks = nullptr;
+    int32_t* h_obs = nullptr;
+    double* h_reward = nullptr;
+    uint8_t* h_done = nullptr;
+    std::vector<int32_t> h_stateScratch;
+
+    KParams params() const {
+        KParams P;
+        std::memset(&P, 0, sizeof(P));
+        P.utt = utt;
+        P.H = H;
+        P.W = W;
+        P.HW = HW;
+        P.CAP = CAP;
+        P.n_games = nGames;
+        P.n_sp_games = nSpGames;
+        P.max_steps = maxSteps;
+        P.C = C;
+        P.state = d_state;
+        P.tmpl = d_tmpl;
+        P.tmpl_off = d_tmplOff;
+        P.bot_kind = d_botKind;
+        return P;
+    }
+    int gameOfSlot(int slot, int* player) const {
+        if (slot < 2 * nSpGames) {
+            *player = slot & 1;
+            return slot / 2;
+        }
+        *player = 0;
+        return nSpGames + (slot - 2 * nSpGames);
+    }
+};
+
+namespace {
+
+int fail(const Fail& f) {
+    g_err = f.msg;
+    return f.code;
+}
+
+hipStream_t pickStream(mrts_env* env, void* s) { return s ? (hipStream_t)s : env->stream; }
+
+void checkFlagsAfter(mrts_env* env) {  // Java exceptions → error codes
+    std::vector<uint32_t> fl((size_t)env->nSlots);
+    mrts_error_flags(env, fl.data());
+    uint32_t all = 0;
+    for (auto f : fl) all |= f;
+    if (all & (MRTS_ERR_PRODUCE_TYPE)) throw Fail{-EINVAL, "decoded produce type out of range (Java: IndexOutOfBoundsException)"};
+    if (all & (MRTS_ERR_CAPACITY)) throw Fail{-ENOSPC, "unit capacity exhausted"};
+    if (all & (MRTS_ERR_ADDUNIT | MRTS_ERR_MOVE_COLLISION)) throw Fail{-EFAULT, "two units in one position (Java: addUnit exception)"};
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* mrts_last_error(void) { return g_err.c_str(); }
+
+int mrts_create(const mrts_config* cfg, mrts_env** out) {
+    mrts_env* env = nullptr;
+    try {
+        if (!cfg || !out) throw Fail{-EINVAL, "null argument"};
+        if (cfg->n_selfplay_slots < 0 || (cfg->n_selfplay_slots & 1)) throw Fail{-EINVAL, "n_selfplay_slots must be even"};
+        if (cfg->n_bot_envs < 0) throw Fail{-EINVAL, "n_bot_envs < 0"};
+        const int nSlots = cfg->n_selfplay_slots + cfg->n_bot_envs;
+        if (nSlots <= 0) throw Fail{-EINVAL, "no environments"};
+        if (cfg->partial_obs) throw Fail{-ENOTSUP, "partial observability is not implemented yet on the GPU path"};
+        if (!cfg->map_paths) throw Fail{-EINVAL, "map_paths is null"};
+        env = new mrts_env();
+        env->device = cfg->device;
+        HIPCHK(hipSetDevice(cfg->device));
+        HIPCHK(hipStreamCreateWithFlags(&env->stream, hipStreamNonBlocking));
+        env->utt = makeUtt(cfg->utt_version, cfg->conflict_policy);
+        env->K = env->utt.K;
+        env->C = cfg->partial_obs ? 8 : 6;
+        env->partialObs = cfg->partial_obs;
+        env->maxSteps = cfg->max_steps;
+        env->nSlots = nSlots;
+        env->nSpGames = cfg->n_selfplay_slots / 2;
+        env->nGames = env->nSpGames + cfg->n_bot_envs;
+        env->slotIdBase = (uint32_t)cfg->slot_id_base;
+        for (int j = 0; j < cfg->n_bot_envs; j++) {
+            const int k = cfg->bot_kinds ? cfg->bot_kinds[j] : MRTS_BOT_PASSIVE;
+            if (k != MRTS_BOT_PASSIVE) throw Fail{-ENOTSUP, "only PassiveAI opponents are implemented on the GPU path"};
+        }
+        // maps: one template per distinct path
+        std::map<std::string, int> tmplIndex;
+        std::vector<MapDef> maps;
+        std::vector<int> gameTmpl((size_t)env->nGames);
+        for (int g = 0; g < env->nGames; g++) {
+            const int slot = g < env->nSpGames ? 2 * g : 2 * env->nSpGames + (g - env->nSpGames);
+            const char* p = cfg->map_paths[slot];
+            if (!p) throw Fail{-EINVAL, "null map path"};
+            auto it = tmplIndex.find(p);
+            if (it == tmplIndex.end()) {
+                maps.push_back(parseMap(p));
+                it = tmplIndex.emplace(p, (int)maps.size() - 1).first;
+            }
+            gameTmpl[(size_t)g] = it->second;
+        }
+        env->H = maps[0].H;
+        env->W = maps[0].W;
+        env->HW = env->H * env->W;
+        for (auto& m : maps)
+            if (m.H != env->H || m.W != env->W) throw Fail{-EINVAL, "all maps must share env 0's size (JNIGridnetVecClient.java:127-133)"};
+        // capacity: one live unit per cell, plus slack for the step's births over its deaths
+        env->CAP = env->HW + std::max(64, env->HW / 4);
+        if (env->CAP > 0xFFF0) throw Fail{-EINVAL, "map too large"};
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, cfg->device));
+        const size_t lds = ldsBytes(env->HW, env->W, env->CAP);
+        if (lds > 160 * 1024) throw Fail{-EINVAL, "map too large for LDS"};
+        if (lds > 64 * 1024) HIPCHK(prepareLds(lds));
+        // templates blob
+        std::vector<int32_t> blob;
+        std::vector<int> off;
+        for (auto& m : maps) {
+            off.push_back((int)blob.size());
+            const int nu = (int)m.units.size();
+            blob.push_back(m.H);
+            blob.push_back(m.W);
+            blob.push_back(m.res[0]);
+            blob.push_back(m.res[1]);
+            blob.push_back(nu);
+            for (auto& u : m.units)
+                blob.push_back((int32_t)((uint32_t)u.x | ((uint32_t)u.y << 8) | ((uint32_t)u.type << 16) | ((uint32_t)(u.player + 1) << 20)));
+            for (auto& u : m.units) blob.push_back(u.hp);
+            for (auto& u : m.units) blob.push_back(u.res);
+            std::vector<int32_t> terr((size_t)(env->HW + 3) / 4, 0);
+            std::memcpy(terr.data(), m.terrain.data(), (size_t)env->HW);
+            blob.insert(blob.end(), terr.begin(), terr.end());
+        }
+        env->tmplOffHost.resize((size_t)env->nGames);
+        for (int g = 0; g < env->nGames; g++) env->tmplOffHost[(size_t)g] = off[(size_t)gameTmpl[(size_t)g]];
+        const size_t sw = (size_t)stateWords(env->CAP);
+        HIPCHK(hipMalloc(&env->d_state, sw * env->nGames * 4));
+        HIPCHK(hipMalloc(&env->d_tmpl, blob.size() * 4));
+        HIPCHK(hipMalloc(&env->d_tmplOff, (size_t)env->nGames * 4));
+        HIPCHK(hipMalloc(&env->d_botKind, (size_t)env->nGames * 4));
+        HIPCHK(hipMemcpy(env->d_tmpl, blob.data(), blob.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(env->d_tmplOff, env->tmplOffHost.data(), (size_t)env->nGames * 4, hipMemcpyHostToDevice));
+        std::vector<int32_t> bk((size_t)env->nGames, 0);
+        HIPCHK(hipMemcpy(env->d_botKind, bk.data(), bk.size() * 4, hipMemcpyHostToDevice));
+        // headers: java.util.Random seeds per game (same derivation as the CPU oracle)
+        std::vector<int32_t> hdr(sw * env->nGames, 0);
+        auto scramble = [](uint64_t s) { return (s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); };
+        for (int g = 0; g < env->nGames; g++) {
+            const int slot = g < env->nSpGames ? 2 * g : 2 * env->nSpGames + (g - env->nSpGames);
+            const uint64_t es = cfg->seed + (uint64_t)(env->slotIdBase + (uint32_t)slot);
+            int32_t* h = &hdr[(size_t)g * sw];
+            const uint64_t rc = scramble(es ^ 0x9E3779B97F4A7C15ULL), rd = scramble(es ^ 0xC2B2AE3D27D4EB4FULL), rs = scramble(es);
+            h[H_RNG_CANCEL] = (int32_t)(uint32_t)rc;
+            h[H_RNG_CANCEL + 1] = (int32_t)(uint32_t)(rc >> 32);
+            h[H_RNG_DAMAGE] = (int32_t)(uint32_t)rd;
+            h[H_RNG_DAMAGE + 1] = (int32_t)(uint32_t)(rd >> 32);
+            h[H_RNG_SAMPLER] = (int32_t)(uint32_t)rs;
+            h[H_RNG_SAMPLER + 1] = (int32_t)(uint32_t)(rs >> 32);
+        }
+        HIPCHK(hipMemcpy(env->d_state, hdr.data(), hdr.size() * 4, hipMemcpyHostToDevice));
+        // host-API buffers
+        const size_t S = (size_t)nSlots;
+        HIPCHK(hipMalloc(&env->d_actions, S * env->HW * 7 * 4));
+        HIPCHK(hipMalloc(&env->d_players, S * 4));
+        HIPCHK(hipMalloc(&env->d_obs, S * env->C * env->HW * 4));
+        HIPCHK(hipMalloc(&env->d_reward, S * 8));
+        HIPCHK(hipMalloc(&env->d_done, S));
+        HIPCHK(hipMalloc(&env->d_masks, S * env->HW * env->K));
+        HIPCHK(hipHostMalloc(&env->h_obs, S * env->C * env->HW * 4, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&env->h_reward, S * 8, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&env->h_done, S, hipHostMallocDefault));
+        HIPCHK(hipMemset(env->d_players, 0, S * 4));
+        // initial state = reset (the Java constructor loads the maps)
+        KParams P = env->params();
+        HIPCHK(launchEnv(1, P, env->stream));
+        HIPCHK(hipStreamSynchronize(env->stream));
+        *out = env;
+        return 0;
+    } catch (const Fail& f) {
+        if (env) mrts_destroy(env);
+        return fail(f);
+    } catch (const std::exception& e) {
+        if (env) mrts_destroy(env);
+        return fail(Fail{-EINVAL, e.what()});
+    }
+}
+
+int mrts_dims(const mrts_env* env, int32_t* n_slots, int32_t* H, int32_t* W, int32_t* C, int32_t* K) {
+    if (!env) return -EINVAL;
+    if (n_slots) *n_slots = env->nSlots;
+    if (H) *H = env->H;
+    if (W) *W = env->W;
+    if (C) *C = env->C;
+    if (K) *K = env->K;
+    return 0;
+}
+
+void* mrts_stream(mrts_env* env) { return env ? (void*)env->stream : nullptr; }
+
+int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
+                   uint8_t* d_masks, int32_t mask_player, void* stream) {
+    try {
+        HIPCHK(hipSetDevice(env->device));
+        KParams P = env->params();
+        P.players = d_players;
+        P.obs = d_obs;
+        P.reward = d_reward;
+        P.done = d_done;
+        P.masks = d_masks;
+        P.mask_player = mask_player;
+        HIPCHK(launchEnv(1, P, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                  uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream) {
+    try {
+        if (!d_actions) throw Fail{-EINVAL, "actions is null"};
+        HIPCHK(hipSetDevice(env->device));
+        KParams P = env->params();
+        P.actions = d_actions;
+        P.players = d_players;
+        P.obs = d_obs;
+        P.reward = d_reward;
+        P.done = d_done;
+        P.masks = d_masks;
+        P.mask_player = mask_player;
+        HIPCHK(launchEnv(0, P, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stream) {
+    try {
+        if (!d_out) throw Fail{-EINVAL, "out is null"};
+        HIPCHK(hipSetDevice(env->device));
+        KParams P = env->params();
+        P.masks = d_out;
+        P.mask_player = player;
+        HIPCHK(launchEnv(2, P, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, uint64_t seed, uint32_t step, int32_t* d_actions, void* stream) {
+    try {
+        HIPCHK(hipSetDevice(env->device));
+        PolicyParams Q;
+        Q.HW = env->HW;
+        Q.K = env->K;
+        Q.ntypes = env->utt.ntypes;
+        Q.n_slots = env->nSlots;
+        Q.slot_id_base = env->slotIdBase;
+        Q.step = step;
+        Q.seed = seed;
+        Q.masks = d_masks;
+        Q.actions = d_actions;
+        HIPCHK(launchPolicy(Q, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+static void fillResponses(mrts_env* env, mrts_responses* out) {
+    const size_t S = (size_t)env->nSlots;
+    HIPCHK(hipMemcpyAsync(env->h_obs, env->d_obs, S * env->C * env->HW * 4, hipMemcpyDeviceToHost, env->stream));
+    HIPCHK(hipMemcpyAsync(env->h_reward, env->d_reward, S * 8, hipMemcpyDeviceToHost, env->stream));
+    HIPCHK(hipMemcpyAsync(env->h_done, env->d_done, S, hipMemcpyDeviceToHost, env->stream));
+    HIPCHK(hipStreamSynchronize(env->stream));
+    if (out) {
+        out->obs = env->h_obs;
+        out->reward = env->h_reward;
+        out->done = env->h_done;
+    }
+}
+
+int mrts_reset(mrts_env* env, const int32_t* players, mrts_responses* out) {
+    try {
+        HIPCHK(hipSetDevice(env->device));
+        const size_t S = (size_t)env->nSlots;
+        if (players) HIPCHK(hipMemcpyAsync(env->d_players, players, S * 4, hipMemcpyHostToDevice, env->stream));
+        else HIPCHK(hipMemsetAsync(env->d_players, 0, S * 4, env->stream));
+        int r = mrts_reset_dev(env, env->d_players, env->d_obs, env->d_reward, env->d_done, nullptr, 0, env->stream);
+        if (r) return r;
+        fillResponses(env, out);
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_step(mrts_env* env, const int32_t* actions, const int32_t* players, mrts_responses* out) {
+    try {
+        if (!actions) throw Fail{-EINVAL, "actions is null"};
+        HIPCHK(hipSetDevice(env->device));
+        const size_t S = (size_t)env->nSlots;
+        HIPCHK(hipMemcpyAsync(env->d_actions, actions, S * env->HW * 7 * 4, hipMemcpyHostToDevice, env->stream));
+        if (players) HIPCHK(hipMemcpyAsync(env->d_players, players, S * 4, hipMemcpyHostToDevice, env->stream));
+        else HIPCHK(hipMemsetAsync(env->d_players, 0, S * 4, env->stream));
+        int r = mrts_step_dev(env, env->d_actions, env->d_players, env->d_obs, env->d_reward, env->d_done, nullptr, 0, env->stream);
+        if (r) return r;
+        fillResponses(env, out);
+        checkFlagsAfter(env);
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out) {
+    try {
+        if (!out) throw Fail{-EINVAL, "out is null"};
+        int r = mrts_get_masks_dev(env, player, env->d_masks, env->stream);
+        if (r) return r;
+        HIPCHK(hipMemcpyAsync(out, env->d_masks, (size_t)env->nSlots * env->HW * env->K, hipMemcpyDeviceToHost, env->stream));
+        HIPCHK(hipStreamSynchronize(env->stream));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_get_state(mrts_env* env, int32_t slot, int32_t* buf, int32_t cap) {
+    try {
+        if (slot < 0 || slot >= env->nSlots) throw Fail{-EINVAL, "slot out of range"};
+        int pl;
+        const int g = env->gameOfSlot(slot, &pl);
+        const size_t sw = (size_t)stateWords(env->CAP);
+        std::vector<int32_t> s(sw);
+        HIPCHK(hipStreamSynchronize(env->stream));
+        HIPCHK(hipMemcpy(s.data(), env->d_state + (size_t)g * sw, sw * 4, hipMemcpyDeviceToHost));
+        const int CAP = env->CAP;
+        const int32_t* A = s.data() + H_WORDS;
+        const int nu = s[H_NU];
+        std::vector<int32_t> d;
+        d.push_back(s[H_TIME]);
+        d.push_back(2);
+        d.push_back(s[H_RES0]);
+        d.push_back(s[H_RES1]);
+        d.push_back(nu);
+        struct Asg { int seq, unit; };
+        std::vector<Asg> asg;
+        for (int i = 0; i < nu; i++) {
+            const uint32_t c = (uint32_t)A[A_UC * CAP + i];
+            d.push_back((int32_t)((c >> 16) & 0xF));
+            d.push_back((int32_t)((c >> 20) & 3) - 1);
+            d.push_back((int32_t)(c & 0xFF));
+            d.push_back((int32_t)((c >> 8) & 0xFF));
+            d.push_back(A[A_HP * CAP + i]);
+            d.push_back(A[A_RES * CAP + i]);
+            if ((uint32_t)A[A_UA * CAP + i] & UA_PRESENT) asg.push_back({A[A_AS * CAP + i], i});
+        }
+        std::sort(asg.begin(), asg.end(), [](const Asg& a, const Asg& b) { return a.seq < b.seq; });
+        d.push_back((int32_t)asg.size());
+        for (auto& e : asg) {
+            const uint32_t a = (uint32_t)A[A_UA * CAP + e.unit];
+            const int t = (int)(a & 0xF);
+            d.push_back(e.unit);
+            d.push_back(t);
+            d.push_back(t == 5 ? -1 : A[A_PAR * CAP + e.unit]);
+            d.push_back(t == 5 ? (int32_t)((a >> 8) & 0xFF) : 0);
+            d.push_back(t == 5 ? (int32_t)((a >> 16) & 0xFF) : 0);
+            d.push_back(t == 4 ? (int32_t)((a >> 4) & 0xF) : -1);
+            d.push_back(A[A_AT * CAP + e.unit]);
+        }
+        if ((int)d.size() > cap) return -(int)d.size();
+        std::memcpy(buf, d.data(), d.size() * 4);
+        return (int)d.size();
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+static int readHeaderWord(mrts_env* env, int word, int32_t* out_per_slot) {
+    const size_t sw = (size_t)stateWords(env->CAP);
+    HIPCHK(hipStreamSynchronize(env->stream));
+    std::vector<int32_t> w((size_t)env->nGames);
+    HIPCHK(hipMemcpy2D(w.data(), 4, env->d_state + word, sw * 4, 4, (size_t)env->nGames, hipMemcpyDeviceToHost));
+    for (int s = 0; s < env->nSlots; s++) {
+        int pl;
+        out_per_slot[s] = w[(size_t)env->gameOfSlot(s, &pl)];
+    }
+    return 0;
+}
+
+int mrts_error_flags(mrts_env* env, uint32_t* flags) {
+    try {
+        return readHeaderWord(env, H_ERR, (int32_t*)flags);
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_env_steps(mrts_env* env, int32_t* out) {
+    try {
+        return readHeaderWord(env, H_STEPS, out);
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+void mrts_destroy(mrts_env* env) {
+    if (!env) return;
+    (void)hipSetDevice(env->device);
+    if (env->stream) (void)hipStreamSynchronize(env->stream);
+    (void)hipFree(env->d_state);
+    (void)hipFree(env->d_tmpl);
+    (void)hipFree(env->d_tmplOff);
+    (void)hipFree(env->d_botKind);
+    (void)hipFree(env->d_actions);
+    (void)hipFree(env->d_players);
+    (void)hipFree(env->d_obs);
+    (void)hipFree(env->d_reward);
+    (void)hipFree(env->d_done);
+    (void)hipFree(env->d_masks);
+    (void)hipHostFree(env->h_obs);
+    (void)hipHostFree(env->h_reward);
+    (void)hipHostFree(env->h_done);
+    if (env->stream) (void)hipStreamDestroy(env->stream);
+    delete env;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// Internal layouts shared by the HIP kernels (mrts_kernels.hip) and the host runtime (mrts_host.cpp).
+#pragma once
+#include <stdint.h>
+
+namespace mrts {
+
+constexpr int MAX_TYPES = 8;
+constexpr int MAX_PRODUCES = 4;
+
+// UnitTypeTable constants (reference src/rts/units/UnitTypeTable.java:104-289), passed by value as
+// kernel arguments so that handles with different tables never share device globals.
+struct DevUtt {
+    int32_t ntypes;
+    int32_t cost[MAX_TYPES], hp[MAX_TYPES], minD[MAX_TYPES], maxD[MAX_TYPES], range[MAX_TYPES];
+    int32_t produceT[MAX_TYPES], moveT[MAX_TYPES], attackT[MAX_TYPES], harvestT[MAX_TYPES], harvestAmt[MAX_TYPES];
+    int32_t sight[MAX_TYPES];
+    uint32_t flags[MAX_TYPES];  // F_* below
+    int32_t nprod[MAX_TYPES];
+    int32_t prod[MAX_TYPES][MAX_PRODUCES];  // type.produces, list order
+    int32_t crs;                // move-conflict resolution strategy 1/2/3
+    int32_t maxAttackRadius;    // 2 * max attack range + 1 (JNIGridnetClient.java:125)
+    int32_t K;                  // mask slots per cell (JNIGridnetClient.java:138)
+};
+enum : uint32_t { F_RESOURCE = 1, F_STOCKPILE = 2, F_HARVEST = 4, F_MOVE = 8, F_ATTACK = 16 };
+
+// ---- per-game state block in HBM (int32 words) -------------------------------------------------
+// header
+enum {
+    H_TIME = 0,       // GameState.time
+    H_NU = 1,         // unit slots in use (== live units between steps; list order == slot order)
+    H_RES0 = 2,       // Player 0 resources
+    H_RES1 = 3,       // Player 1 resources
+    H_SEQ = 4,        // next assignment sequence number (LinkedHashMap insertion order)
+    H_STEPS = 5,      // VecClient envSteps
+    H_ERR = 6,        // MRTS_ERR_* flags (sticky until reset by the host)
+    H_CANCEL_CNT = 7, // GameState.unitCancelationCounter
+    H_RNG_CANCEL = 8, // 2 words: java.util.Random for CANCEL_RANDOM (GameState.r)
+    H_RNG_DAMAGE = 10,// 2 words: java.util.Random for non-deterministic damage (UnitAction.r)
+    H_RNG_SAMPLER = 12,// 2 words: java.util.Random for RandomBiasedAI (Sampler.generator)
+    H_WORDS = 16
+};
+// followed by 7 SoA arrays of CAP int32: UC, HP, RES, UA, PAR, AT, AS (see mrts_kernels.hip)
+enum { A_UC = 0, A_HP = 1, A_RES = 2, A_UA = 3, A_PAR = 4, A_AT = 5, A_AS = 6, N_ARRAYS = 7 };
+constexpr int stateWords(int cap) { return H_WORDS + N_ARRAYS * cap; }  // constexpr: host + device
+
+// unit core word
+constexpr uint32_t UC_DEAD = 1u << 31;
+// assignment word
+constexpr uint32_t UA_PRESENT = 1u << 24, UA_READY = 1u << 25, UA_PA = 1u << 26;
+constexpr int ACT_INVALID = 7;  // action type / direction outside the Java ranges
+
+// ---- map templates (one per distinct map), int32 words --------------------------------------------
+// [0] H [1] W [2] res0 [3] res1 [4] nu [5..5+nu) uc [..+nu) hp [..+nu) res [..+ceil(HW/4)) terrain (u8 x4)
+enum { T_H = 0, T_W = 1, T_RES0 = 2, T_RES1 = 3, T_NU = 4, T_UNITS = 5 };
+
+struct KParams {
+    DevUtt utt;
+    int32_t H, W, HW, CAP;
+    int32_t n_games, n_sp_games;   // games [0, n_sp_games) are self-play, the rest agent-vs-bot
+    int32_t max_steps, C;
+    int32_t mask_player;           // player whose masks bot-env slots receive
+    int32_t* state;                // [n_games][stateWords(CAP)]
+    const int32_t* tmpl;           // template blob
+    const int32_t* tmpl_off;       // [n_games] word offset of each game's template
+    const int32_t* bot_kind;       // [n_games]
+    const int32_t* actions;        // [n_slots][HW][7]
+    const int32_t* players;        // [n_slots] or null
+    int32_t* obs;                  // [n_slots][C][HW] or null
+    double* reward;                // [n_slots] or null
+    uint8_t* done;                 // [n_slots] or null
+    uint8_t* masks;                // [n_slots][HW][K] or null
+};
+
+struct PolicyParams {
+    int32_t HW, K, ntypes, n_slots;
+    uint32_t slot_id_base, step;
+    uint64_t seed;
+    const uint8_t* masks;
+    int32_t* actions;
+};
+
+}  // namespace mrts

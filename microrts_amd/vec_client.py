@@ -1,0 +1,250 @@
+"""Host-side mirror of the reference's env-client interface over the libmrts C ABI.
+
+* ``JNIGridnetVecClient`` mirrors ``tests.JNIGridnetVecClient`` (reference
+  src/tests/JNIGridnetVecClient.java:17-335): same constructor arguments, ``reset`` / ``gameStep``
+  / ``getMasks`` / ``close``, host numpy arrays that are library-owned views reused by the next
+  call (like the Java ``Response`` buffers, GameState.java:923-925).
+* ``DeviceVecEnv`` is the zero-copy rollout form: every buffer is a torch tensor in HBM and all
+  calls are stream-ordered on the handle's HIP stream (no host sync).
+
+There is no CPU fallback: constructing either class without a GPU or without libmrts.so raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class UnitTypeTable:
+    """rts.units.UnitTypeTable(version, crs) (src/rts/units/UnitTypeTable.java:22-349)."""
+
+    EMPTY_TYPE_TABLE = -1
+    VERSION_ORIGINAL = 1
+    VERSION_ORIGINAL_FINETUNED = 2
+    VERSION_NON_DETERMINISTIC = 3
+    MOVE_CONFLICT_RESOLUTION_CANCEL_BOTH = 1
+    MOVE_CONFLICT_RESOLUTION_CANCEL_RANDOM = 2
+    MOVE_CONFLICT_RESOLUTION_CANCEL_ALTERNATING = 3
+    TYPES = ["Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"]
+
+    def __init__(self, version=VERSION_ORIGINAL, crs=MOVE_CONFLICT_RESOLUTION_CANCEL_BOTH):
+        if version not in (1, 2, 3) or crs not in (1, 2, 3):
+            raise ValueError("unsupported UnitTypeTable version / conflict policy")
+        self.version, self.crs = version, crs
+
+    def getMaxAttackRange(self):
+        return 3
+
+
+class Responses:
+    """ai.jni.Responses (src/ai/jni/Responses.java:12-30)."""
+
+    def __init__(self, observation, reward, done):
+        self.observation, self.reward, self.done = observation, reward, done
+
+
+def _bot_kind(ai):
+    name = ai if isinstance(ai, str) else type(ai).__name__
+    if name in ("PassiveAI", "passive"):
+        return _lib.MRTS_BOT_PASSIVE
+    if name in ("RandomBiasedAI", "random_biased"):
+        return _lib.MRTS_BOT_RANDOM_BIASED
+    raise NotImplementedError(f"opponent AI {name!r} has no native implementation (only PassiveAI / RandomBiasedAI)")
+
+
+def _check_rfs(rfs):
+    names = [r if isinstance(r, str) else type(r).__name__ for r in (rfs or ["WinLossRewardFunction"])]
+    if names != ["WinLossRewardFunction"]:
+        raise NotImplementedError("only [WinLossRewardFunction] is implemented on the GPU path")
+
+
+class _Handle:
+    def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base):
+        L = _lib.load()
+        self.L = L
+        self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
+        kinds = [_bot_kind(a) for a in (ai2s or [])][:n_bot]
+        kinds += [_lib.MRTS_BOT_PASSIVE] * (n_bot - len(kinds))
+        self._kinds = (ctypes.c_int32 * max(1, n_bot))(*(kinds or [0]))
+        cfg = _lib.MrtsConfig(n_selfplay, n_bot, max_steps, int(bool(partial_obs)), utt.version, utt.crs,
+                              ctypes.cast(self._kinds, ctypes.POINTER(ctypes.c_int32)),
+                              ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base)
+        h = ctypes.c_void_p()
+        _lib.check(L.mrts_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self.h = h
+        d = [ctypes.c_int32() for _ in range(5)]
+        L.mrts_dims(self.h, *[ctypes.byref(x) for x in d])
+        self.S, self.H, self.W, self.C, self.K = [x.value for x in d]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mrts_destroy(self.h)
+            self.h = None
+
+    def dump(self, slot):
+        buf = np.zeros(1 << 16, np.int32)
+        n = self.L.mrts_get_state(self.h, slot, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+        if n < 0:
+            raise RuntimeError(self.L.mrts_last_error().decode())
+        return buf[:n].copy()
+
+    def error_flags(self):
+        f = np.zeros(self.S, np.uint32)
+        _lib.check(self.L.mrts_error_flags(self.h, f.ctypes.data_as(ctypes.c_void_p)))
+        return f
+
+    def env_steps(self):
+        f = np.zeros(self.S, np.int32)
+        _lib.check(self.L.mrts_env_steps(self.h, f.ctypes.data_as(ctypes.c_void_p)))
+        return f
+
+
+def _resolve(micrortsPath, p):
+    if micrortsPath:
+        return os.path.join(micrortsPath, p)
+    return p if os.path.isabs(p) or os.path.exists(p) else os.path.join(ROOT, p)
+
+
+class JNIGridnetVecClient:
+    """tests.JNIGridnetVecClient (src/tests/JNIGridnetVecClient.java:106-142) on MI355X."""
+
+    def __init__(self, a_num_selfplayenvs, a_num_envs, a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai2s=None,
+                 a_utt=None, partial_obs=False, device=0, seed=0, slot_id_base=0):
+        _check_rfs(a_rfs)
+        utt = a_utt or UnitTypeTable()
+        paths = [_resolve(a_micrortsPath, p) for p in a_mapPaths]
+        self._h = _Handle(a_num_selfplayenvs, a_num_envs, a_max_steps, paths, a_ai2s, utt, partial_obs, device, seed,
+                          slot_id_base)
+        self.maxSteps = a_max_steps
+        self.utt = utt
+        self.partialObs = partial_obs
+        self.mapPaths = list(a_mapPaths)
+        h = self._h
+        self.num_slots, self.height, self.width, self.num_planes, self.mask_slots = h.S, h.H, h.W, h.C, h.K
+        self._resp = _lib.MrtsResponses()
+
+    def _responses(self):
+        h, r = self._h, self._resp
+        obs = np.ctypeslib.as_array(r.obs, shape=(h.S, h.C, h.H, h.W))
+        rew = np.ctypeslib.as_array(r.reward, shape=(h.S, 1))
+        done = np.ctypeslib.as_array(r.done, shape=(h.S, 1)).view(np.bool_)
+        return Responses(obs, rew, done)
+
+    def reset(self, players=None):
+        """reset(int[] players) (:179-211)."""
+        p = None if players is None else np.ascontiguousarray(players, np.int32)
+        _lib.check(self._h.L.mrts_reset(self._h.h, None if p is None else p.ctypes.data_as(ctypes.c_void_p),
+                                        ctypes.byref(self._resp)))
+        return self._responses()
+
+    def gameStep(self, action, players=None):
+        """gameStep(int[][][] action, int[] players) (:213-297); action = [slots][H*W][7]."""
+        a = np.ascontiguousarray(action, np.int32).reshape(self._h.S, self._h.H * self._h.W, 7)
+        p = None if players is None else np.ascontiguousarray(players, np.int32)
+        _lib.check(self._h.L.mrts_step(self._h.h, a.ctypes.data_as(ctypes.c_void_p),
+                                       None if p is None else p.ctypes.data_as(ctypes.c_void_p), ctypes.byref(self._resp)))
+        return self._responses()
+
+    def getMasks(self, player=0):
+        """getMasks(int player) (:307-316) → uint8 [slots][H][W][79]."""
+        h = self._h
+        m = np.empty((h.S, h.H, h.W, h.K), np.uint8)
+        _lib.check(h.L.mrts_get_masks(h.h, player, m.ctypes.data_as(ctypes.c_void_p)))
+        return m
+
+    @property
+    def envSteps(self):
+        return self._h.env_steps()
+
+    def dump_state(self, slot):
+        return self._h.dump(slot)
+
+    def error_flags(self):
+        return self._h.error_flags()
+
+    def close(self):
+        """close() (:318-334)."""
+        self._h.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceVecEnv:
+    """Zero-copy rollout backend: torch HBM tensors, stream-ordered on the handle's HIP stream."""
+
+    def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
+                 device=0, seed=0, slot_id_base=0, with_masks=True):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("DeviceVecEnv needs an MI355X (torch.cuda is unavailable); there is no CPU fallback")
+        utt = utt or UnitTypeTable()
+        paths = [_resolve("", p) for p in map_paths]
+        self._h = _Handle(num_selfplay_slots, num_bot_envs, max_steps, paths, ai2s, utt, partial_obs, device, seed,
+                          slot_id_base)
+        h = self._h
+        dev = torch.device("cuda", device)
+        self.device = dev
+        self.stream = torch.cuda.ExternalStream(h.L.mrts_stream(h.h), device=dev)
+        S, H, W, C, K = h.S, h.H, h.W, h.C, h.K
+        self.obs = torch.zeros((S, C, H, W), dtype=torch.int32, device=dev)
+        self.reward = torch.zeros((S,), dtype=torch.float64, device=dev)
+        self.done = torch.zeros((S,), dtype=torch.uint8, device=dev)
+        self.masks = torch.zeros((S, H, W, K), dtype=torch.uint8, device=dev) if with_masks else None
+        self.actions = torch.zeros((S, H * W, 7), dtype=torch.int32, device=dev)
+        self.players = torch.zeros((S,), dtype=torch.int32, device=dev)
+        self.mask_player = 0
+        torch.cuda.synchronize(dev)
+
+    @staticmethod
+    def _p(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def reset(self):
+        h = self._h
+        _lib.check(h.L.mrts_reset_dev(h.h, self._p(self.players), self._p(self.obs), self._p(self.reward),
+                                      self._p(self.done), self._p(self.masks), self.mask_player, None))
+
+    def step(self, actions=None):
+        h = self._h
+        a = self.actions if actions is None else actions
+        _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self.reward),
+                                     self._p(self.done), self._p(self.masks), self.mask_player, None))
+
+    def get_masks(self, out=None):
+        h = self._h
+        out = self.masks if out is None else out
+        _lib.check(h.L.mrts_get_masks_dev(h.h, self.mask_player, self._p(out), None))
+        return out
+
+    def random_policy(self, seed, step, masks=None, out=None):
+        h = self._h
+        m = self.masks if masks is None else masks
+        out = self.actions if out is None else out
+        _lib.check(h.L.mrts_policy_dev(h.h, self._p(m), seed, step, self._p(out), None))
+        return out
+
+    def synchronize(self):
+        self.stream.synchronize()
+
+    def dump_state(self, slot):
+        return self._h.dump(slot)
+
+    def error_flags(self):
+        return self._h.error_flags()
+
+    @property
+    def dims(self):
+        h = self._h
+        return h.S, h.H, h.W, h.C, h.K
+
+    def close(self):
+        self._h.close()

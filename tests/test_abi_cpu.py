@@ -1,0 +1,60 @@
+"""CPU-side checks of the drop-in boundary: libmrts.so loads and exports every symbol include/mrts.h
+declares; the Python mirror validates its arguments (no GPU compute is called here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from microrts_amd import _lib
+from microrts_amd.vec_client import UnitTypeTable, _check_rfs, _bot_kind
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "mrts.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mrts_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_matches_python_exports():
+    assert header_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_loads_and_exports_every_symbol():
+    L = _lib.load()
+    for name in header_symbols():
+        assert hasattr(L, name), name
+        assert ctypes.cast(getattr(L, name), ctypes.c_void_p).value
+
+
+def test_config_struct_layout():
+    # mrts_config: 6 int32, pointer, pointer, int32, uint64, int32 (natural alignment)
+    assert ctypes.sizeof(_lib.MrtsConfig) == 6 * 4 + 8 + 8 + 4 + 4 + 8 + 8
+    assert _lib.MrtsConfig.seed.offset == 48
+
+
+def test_argument_validation():
+    with pytest.raises(NotImplementedError):
+        _check_rfs(["AttackRewardFunction"])
+    _check_rfs(["WinLossRewardFunction"])
+    with pytest.raises(NotImplementedError):
+        _bot_kind("WorkerRush")
+    assert _bot_kind("PassiveAI") == 0
+    with pytest.raises(ValueError):
+        UnitTypeTable(4)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(ImportError):
+        _lib.load.__wrapped__(str(tmp_path / "nope.so")) if hasattr(_lib.load, "__wrapped__") else _load_missing(tmp_path)
+
+
+def _load_missing(tmp_path):
+    saved = _lib._lib
+    _lib._lib = None
+    try:
+        _lib.load(str(tmp_path / "nope.so"))
+    finally:
+        _lib._lib = saved
