@@ -1,0 +1,190 @@
+#!/usr/bin/env python3
+"""Headline benchmark: vectorised microRTS env-steps/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2]): maps/16x16/basesWorkers16x16.xml, 4096
+self-play games per GPU (8192 player slots), UTT VERSION_ORIGINAL + CANCEL_BOTH, max_steps 2000,
+masked uniform random policy (Philox, seed 0x5EEDC0DE), legal-action masks and observations written
+every step.  One "step" = one batched gameStep of every game on every GPU: the policy kernel reads
+the masks and writes the int32 action tensor, then the fused step kernel (decode -> issueSafe ->
+cycle -> WinLoss -> auto-reset -> observation -> masks) consumes it.  An env-step is one game-cycle
+(a self-play game counts once, not twice).  Inputs are resident in HBM; nothing crosses PCIe in
+the timed region.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank steps its own disjoint shard of
+games (weak scaling, no collective in the step); barrier + synchronize bracket the timed region and
+the max time over ranks is reported.  --gather-obs adds the north-star RCCL all-gather of the int32
+observation tensor each step (reported in the JSON, not the default).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/s (random policy) at N envs/GPU, 1/2/4/8 MI355X; bit-exact vs Java"
+MAP = "maps/16x16/basesWorkers16x16.xml"
+SEED = 0x5EEDC0DE
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--burnin", type=int, default=1000,
+                    help="untimed steps from reset before warmup: the timed window sees mid-episode unit counts")
+    ap.add_argument("--envs", type=int, default=4096, help="self-play games per GPU")
+    ap.add_argument("--map", default=MAP)
+    ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of observations each step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pmc-traffic", type=float, default=None,
+                    help="HBM bytes per step-kernel launch from a rocprofv3 --pmc pass (profiles/), for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(map_path, threads, burnin):
+    """The CPU oracle (C++ restatement of the Java engine; the JVM is not available) running the
+    same workload: VecClient self-play + getMasks + the same Philox policy, std::thread shards."""
+    from tests import oracle_py
+
+    L = oracle_py.load()
+    games_per_thread, steps = 48, 300
+    games = games_per_thread * threads
+    secs = L.oref_bench(map_path.encode(), games, steps, threads, SEED, burnin)
+    one = L.oref_bench(map_path.encode(), games_per_thread, steps, 1, SEED, burnin)
+    return {
+        "value": games * steps / secs,
+        "unit": "env-steps/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{games} self-play games x {steps} timed steps after {burnin} untimed, {threads} threads (same map/policy/masks; "
+                  f"1 thread: {games_per_thread * steps / one:.0f} env-steps/s)",
+    }
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from microrts_amd import DeviceVecEnv
+
+    E = a.envs
+    env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, a.map)] * (2 * E), device=local, seed=SEED,
+                       slot_id_base=rank * 2 * E)
+    S, H, W, C, K = env.dims
+    stream = env.stream
+    gather_buf = None
+    if a.gather_obs and world > 1:
+        gather_buf = torch.empty((world,) + tuple(env.obs.shape), dtype=torch.int16, device=env.device)
+
+    def one_step(k, ev=None):
+        env.random_policy(SEED, k)
+        if ev is not None:
+            ev[0].record(stream)
+        env.step()
+        if ev is not None:
+            ev[1].record(stream)
+        if gather_buf is not None:
+            with torch.cuda.stream(stream):
+                dist.all_gather_into_tensor(gather_buf.view(-1), env.obs.to(torch.int16).view(-1))
+
+    env.reset()
+    for k in range(a.burnin + a.warmup):
+        one_step(k)
+    env.synchronize()
+    # rows decoded per step (sum of mask[...,0]) and live units, for the algorithmic-byte count
+    rows = float(env.masks[..., 0].sum().item()) / S
+    units = []
+    for s in range(0, min(S, 64), 2):
+        units.append(env.dump_state(s)[4])
+    mean_units = float(np.mean(units))
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(env.device)
+    env.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        one_step(a.burnin + a.warmup + k, evs[k])
+    env.synchronize()
+    torch.cuda.synchronize(env.device)
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([t], dtype=torch.float64, device=env.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+    step_ms = [s.elapsed_time(e) for s, e in evs]
+    kern_ms = float(np.mean(step_ms))
+    flags = env.error_flags()
+    assert not flags.any(), f"engine error flags set: {np.unique(flags)}"
+
+    # B per player slot = A + O + M + S_slot, A = HW*7*4, O = C*HW*4, M = HW*K,
+    # S = 2*(16*U + 2*HW + 16) per game (read + write), split over its two slots.
+    HW = H * W
+    per_slot = HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16)
+    alg_bytes = per_slot * S
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    total_games = E * world
+    value = total_games * a.steps / t
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * t / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (masked uniform random policy, Philox seed 0x5EEDC0DE)",
+        "config": {
+            "workload": f"c3/c4: {a.map} self-play, {E} games/GPU ({2 * E} player slots), masks+obs every step",
+            "envs_per_gpu": E,
+            "utt": "VERSION_ORIGINAL, CANCEL_BOTH",
+            "max_steps": 2000,
+            "burnin_steps": a.burnin,
+            "parallelism": f"dp{world} (independent env shards)" + (", RCCL int16 obs all-gather" if gather_buf is not None else ""),
+        },
+        "step_kernel_ms": kern_ms,
+        "mean_units": mean_units,
+        "decoded_rows_per_slot": rows,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": a.pmc_traffic,
+            "kernel": "k_env<MODE_STEP>",
+            "alg_bytes_per_launch": alg_bytes,
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin)
+    if rank == 0:
+        print(json.dumps(out))
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

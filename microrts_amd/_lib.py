@@ -55,6 +55,13 @@ def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise ImportError(f"libmrts.so not found at {path}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                           " (no CPU fallback exists)")
+    # A process may hold only ONE HIP/HSA runtime.  PyTorch-ROCm bundles its own libamdhip64.so;
+    # importing torch first makes libmrts.so bind to that same runtime (its DT_NEEDED soname is
+    # already satisfied), which is also what lets torch tensors be passed as device pointers.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     P, I32, U32, U64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
     L.mrts_create.argtypes = [ctypes.POINTER(MrtsConfig), ctypes.POINTER(P)]

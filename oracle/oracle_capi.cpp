@@ -6,6 +6,8 @@
 // used by bench.py, behind a small C API consumed by ctypes from tests/.
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <sstream>
@@ -554,7 +556,11 @@ int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int 
 // ------------------------------------------------ CPU baseline: VecClient + random policy,
 // `threads` std::threads each stepping a disjoint shard of games (cores = threads).
 // Returns env-steps executed; *seconds = wall time of the timed region.
-double oref_bench(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int with_masks) {
+double oref_bench(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin) {
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    std::chrono::steady_clock::time_point t0;
     std::vector<void*> hs((size_t)threads);
     std::vector<int> per((size_t)threads);
     for (int t = 0; t < threads; t++) {
@@ -571,16 +577,23 @@ double oref_bench(const char* map_path, int n_games, int steps, int threads, uin
         std::vector<int32_t> acts((size_t)S * H * W * 7), obs((size_t)S * C * H * W);
         std::vector<double> rew((size_t)S);
         std::vector<uint8_t> done((size_t)S);
-        for (int k = 0; k < steps; k++) {
+        for (int k = -burnin; k < steps; k++) {
+            if (k == 0) {  // end of the untimed burn-in: rendezvous, then the timed region starts
+                std::unique_lock<std::mutex> lk(mu);
+                if (++arrived == threads) {
+                    t0 = std::chrono::steady_clock::now();
+                    cv.notify_all();
+                } else {
+                    cv.wait(lk, [&] { return arrived == threads; });
+                }
+            }
             oref_get_masks(h, 0, masks.data());
             for (int s = 0; s < S; s++)
-                oref_policy(masks.data() + (size_t)s * H * W * K, H * W, K, 7, seed, (uint32_t)(t * 100000 + s / 2), (uint32_t)k,
+                oref_policy(masks.data() + (size_t)s * H * W * K, H * W, K, 7, seed, (uint32_t)(t * 100000 + s / 2), (uint32_t)(k + burnin),
                             (uint32_t)(s & 1), acts.data() + (size_t)s * H * W * 7);
             oref_step(h, acts.data(), nullptr, obs.data(), rew.data(), done.data());
         }
-        (void)with_masks;
     };
-    auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> th;
     for (int t = 0; t < threads; t++) th.emplace_back(worker, t);
     for (auto& x : th) x.join();

@@ -1,0 +1,66 @@
+"""Summarise a tools/gpu_profile.sh run into profiles/<tag>_summary.md (+ copies of the raw stats).
+
+The rocprofv3 --stats table covers every launch of the profiled command, including the untimed
+burn-in (early-episode, fewer units, faster); the summary also reports the average over the last
+`--window` launches = bench.py's timed window, which is what bench.py's live HIP-event number
+measures.  PMC values (FETCH_SIZE / WRITE_SIZE, KB) are per launch, window averages; FETCH_SIZE is
+also shown x2 (MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE under-reports wide streaming reads by 2x;
+our reads are narrow, so the true value lies between the two).
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics
+
+
+def window(rows, name, n):
+    rs = sorted((r for r in rows if r["Kernel_Name"].startswith(name)), key=lambda r: int(r["Start_Timestamp"]))
+    return rs[-n:]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("tag")
+    ap.add_argument("--window", type=int, default=100)
+    a = ap.parse_args()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dst = os.path.join(root, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    bench = json.load(open(os.path.join(a.src, "bench.json")))
+    trace = list(csv.DictReader(open(os.path.join(a.src, "stats", "run_kernel_trace.csv"))))
+    lines = [f"# Profile {a.tag}", "", "bench.py line (default flags):", "", "```json", json.dumps(bench, indent=1), "```", ""]
+    lines += ["## rocprofv3 --kernel-trace --stats (all launches of `bench.py --steps 100 --warmup 10 --burnin 1000`)", "",
+              "```", open(os.path.join(a.src, "stats", "run_kernel_stats.csv")).read().strip(), "```", ""]
+    lines += [f"## Timed window (last {a.window} launches per kernel, from the kernel trace)", "",
+              "| kernel | launches | avg us | min us | max us |", "|---|---|---|---|---|"]
+    for k in ("k_env", "k_policy"):
+        w = window(trace, k, a.window)
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in w]
+        lines.append(f"| {k} | {len(d)} | {statistics.mean(d):.2f} | {min(d):.2f} | {max(d):.2f} |")
+    lines += ["", "## PMC (separate passes; KB per launch, timed-window average)", "",
+              "| kernel | FETCH_SIZE KB | FETCH_SIZE x2 KB | WRITE_SIZE KB |", "|---|---|---|---|"]
+    pmc = {}
+    for c, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
+        p = os.path.join(a.src, sub, "run_counter_collection.csv")
+        if os.path.exists(p):
+            rows = list(csv.DictReader(open(p)))
+            for k in ("k_env", "k_policy"):
+                w = window(rows, k, a.window)
+                pmc[(k, c)] = statistics.mean(float(r["Counter_Value"]) for r in w) if w else float("nan")
+    for k in ("k_env", "k_policy"):
+        f, wr = pmc.get((k, "FETCH_SIZE"), float("nan")), pmc.get((k, "WRITE_SIZE"), float("nan"))
+        lines.append(f"| {k} | {f:.0f} | {2 * f:.0f} | {wr:.0f} |")
+    if ("k_env", "WRITE_SIZE") in pmc:
+        t = (pmc[("k_env", "FETCH_SIZE")] + pmc[("k_env", "WRITE_SIZE")]) * 1024
+        lines += ["", f"k_env HBM traffic per launch (FETCH + WRITE, uncorrected): {t / 1e6:.1f} MB; "
+                      f"algorithmic bytes per launch (SURVEY §8d): {bench['roofline']['alg_bytes_per_launch'] / 1e6:.1f} MB"]
+    open(os.path.join(dst, f"{a.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    shutil.copy(os.path.join(a.src, "stats", "run_kernel_stats.csv"), os.path.join(dst, f"{a.tag}_kernel_stats.csv"))
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
