@@ -19,8 +19,8 @@
 using namespace mrts;
 
 namespace mrts {
-size_t ldsBytes(int HW, int W, int CAP);
-hipError_t launchEnv(int mode, const KParams& P, hipStream_t stream);
+size_t ldsBytes(int HW, int W, int CAP, int po);
+hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream);
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream);
 hipError_t prepareLds(size_t bytes);
 }  // namespace mrts
@@ -267,24 +267,26 @@ struct mrts_env {
     uint8_t* h_done = nullptr;
     std::vector<int32_t> h_stateScratch;
 
-    KParams params() const {
-        KParams P;
-        std::memset(&P, 0, sizeof(P));
-        P.utt = utt;
-        P.H = H;
-        P.W = W;
-        P.HW = HW;
-        P.CAP = CAP;
-        P.n_games = nGames;
-        P.n_sp_games = nSpGames;
-        P.max_steps = maxSteps;
-        P.C = C;
-        P.state = d_state;
-        P.tmpl = d_tmpl;
-        P.tmpl_off = d_tmplOff;
-        P.bot_kind = d_botKind;
-        return P;
+    KStatic hstatic;
+    KStatic* d_static = nullptr;
+    void buildStatic() {
+        std::memset(&hstatic, 0, sizeof(hstatic));
+        hstatic.utt = utt;
+        hstatic.H = H;
+        hstatic.W = W;
+        hstatic.HW = HW;
+        hstatic.CAP = CAP;
+        hstatic.n_games = nGames;
+        hstatic.n_sp_games = nSpGames;
+        hstatic.max_steps = maxSteps;
+        hstatic.C = C;
+        hstatic.partial_obs = partialObs;
+        hstatic.state = d_state;
+        hstatic.tmpl = d_tmpl;
+        hstatic.tmpl_off = d_tmplOff;
+        hstatic.bot_kind = d_botKind;
     }
+    hipError_t launch(int mode, const KDyn& D, hipStream_t s) const { return launchEnv(mode, hstatic, d_static, D, s); }
     int gameOfSlot(int slot, int* player) const {
         if (slot < 2 * nSpGames) {
             *player = slot & 1;
@@ -328,7 +330,6 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         if (cfg->n_bot_envs < 0) throw Fail{-EINVAL, "n_bot_envs < 0"};
         const int nSlots = cfg->n_selfplay_slots + cfg->n_bot_envs;
         if (nSlots <= 0) throw Fail{-EINVAL, "no environments"};
-        if (cfg->partial_obs) throw Fail{-ENOTSUP, "partial observability is not implemented yet on the GPU path"};
         if (!cfg->map_paths) throw Fail{-EINVAL, "map_paths is null"};
         env = new mrts_env();
         env->device = cfg->device;
@@ -372,7 +373,7 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         if (env->CAP > 0xFFF0) throw Fail{-EINVAL, "map too large"};
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, cfg->device));
-        const size_t lds = ldsBytes(env->HW, env->W, env->CAP);
+        const size_t lds = ldsBytes(env->HW, env->W, env->CAP, env->partialObs);
         if (lds > 160 * 1024) throw Fail{-EINVAL, "map too large for LDS"};
         if (lds > 64 * 1024) HIPCHK(prepareLds(lds));
         // templates blob
@@ -433,9 +434,15 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         HIPCHK(hipHostMalloc(&env->h_reward, S * 8, hipHostMallocDefault));
         HIPCHK(hipHostMalloc(&env->h_done, S, hipHostMallocDefault));
         HIPCHK(hipMemset(env->d_players, 0, S * 4));
+        // static kernel parameters → device buffer
+        env->buildStatic();
+        HIPCHK(hipMalloc(&env->d_static, sizeof(KStatic)));
+        HIPCHK(hipMemcpy(env->d_static, &env->hstatic, sizeof(KStatic), hipMemcpyHostToDevice));
         // initial state = reset (the Java constructor loads the maps)
-        KParams P = env->params();
-        HIPCHK(launchEnv(1, P, env->stream));
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.players = env->d_players;
+        HIPCHK(env->launch(1, D, env->stream));
         HIPCHK(hipStreamSynchronize(env->stream));
         *out = env;
         return 0;
@@ -464,14 +471,15 @@ int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, doub
                    uint8_t* d_masks, int32_t mask_player, void* stream) {
     try {
         HIPCHK(hipSetDevice(env->device));
-        KParams P = env->params();
-        P.players = d_players;
-        P.obs = d_obs;
-        P.reward = d_reward;
-        P.done = d_done;
-        P.masks = d_masks;
-        P.mask_player = mask_player;
-        HIPCHK(launchEnv(1, P, pickStream(env, stream)));
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.players = d_players;
+        D.obs = d_obs;
+        D.reward = d_reward;
+        D.done = d_done;
+        D.masks = d_masks;
+        D.mask_player = mask_player;
+        HIPCHK(env->launch(1, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -483,15 +491,16 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
     try {
         if (!d_actions) throw Fail{-EINVAL, "actions is null"};
         HIPCHK(hipSetDevice(env->device));
-        KParams P = env->params();
-        P.actions = d_actions;
-        P.players = d_players;
-        P.obs = d_obs;
-        P.reward = d_reward;
-        P.done = d_done;
-        P.masks = d_masks;
-        P.mask_player = mask_player;
-        HIPCHK(launchEnv(0, P, pickStream(env, stream)));
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.actions = d_actions;
+        D.players = d_players;
+        D.obs = d_obs;
+        D.reward = d_reward;
+        D.done = d_done;
+        D.masks = d_masks;
+        D.mask_player = mask_player;
+        HIPCHK(env->launch(0, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -502,10 +511,12 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
     try {
         if (!d_out) throw Fail{-EINVAL, "out is null"};
         HIPCHK(hipSetDevice(env->device));
-        KParams P = env->params();
-        P.masks = d_out;
-        P.mask_player = player;
-        HIPCHK(launchEnv(2, P, pickStream(env, stream)));
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.masks = d_out;
+        D.mask_player = player;
+        D.players = env->d_players;
+        HIPCHK(env->launch(2, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -674,6 +685,7 @@ void mrts_destroy(mrts_env* env) {
     if (!env) return;
     (void)hipSetDevice(env->device);
     if (env->stream) (void)hipStreamSynchronize(env->stream);
+    (void)hipFree(env->d_static);
     (void)hipFree(env->d_state);
     (void)hipFree(env->d_tmpl);
     (void)hipFree(env->d_tmplOff);

@@ -46,29 +46,36 @@ constexpr int stateWords(int cap) { return H_WORDS + N_ARRAYS * cap; }  // const
 // unit core word
 constexpr uint32_t UC_DEAD = 1u << 31;
 // assignment word
-constexpr uint32_t UA_PRESENT = 1u << 24, UA_READY = 1u << 25, UA_PA = 1u << 26;
+constexpr uint32_t UA_PRESENT = 1u << 24, UA_READY = 1u << 25, UA_PA = 1u << 26, UA_DEC = 1u << 27, UA_BAD = 1u << 28;
 constexpr int ACT_INVALID = 7;  // action type / direction outside the Java ranges
 
 // ---- map templates (one per distinct map), int32 words --------------------------------------------
 // [0] H [1] W [2] res0 [3] res1 [4] nu [5..5+nu) uc [..+nu) hp [..+nu) res [..+ceil(HW/4)) terrain (u8 x4)
 enum { T_H = 0, T_W = 1, T_RES0 = 2, T_RES1 = 3, T_NU = 4, T_UNITS = 5 };
 
-struct KParams {
+// Static per-handle parameters live in a device buffer (uploaded once at mrts_create): the kernels
+// read them through a pointer, so the unit-type tables can be indexed per lane without the
+// compiler copying a by-value kernel argument into scratch memory.
+struct KStatic {
     DevUtt utt;
     int32_t H, W, HW, CAP;
     int32_t n_games, n_sp_games;   // games [0, n_sp_games) are self-play, the rest agent-vs-bot
     int32_t max_steps, C;
-    int32_t mask_player;           // player whose masks bot-env slots receive
+    int32_t partial_obs;           // PartiallyObservableGameState views (8 planes)
     int32_t* state;                // [n_games][stateWords(CAP)]
     const int32_t* tmpl;           // template blob
     const int32_t* tmpl_off;       // [n_games] word offset of each game's template
     const int32_t* bot_kind;       // [n_games]
+};
+// Per-call buffers (kernel arguments by value)
+struct KDyn {
     const int32_t* actions;        // [n_slots][HW][7]
     const int32_t* players;        // [n_slots] or null
     int32_t* obs;                  // [n_slots][C][HW] or null
     double* reward;                // [n_slots] or null
     uint8_t* done;                 // [n_slots] or null
     uint8_t* masks;                // [n_slots][HW][K] or null
+    int32_t mask_player;           // player whose masks bot-env slots receive
 };
 
 struct PolicyParams {

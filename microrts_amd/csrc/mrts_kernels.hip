@@ -7,9 +7,9 @@
 // semantics are order-dependent (rows in cell order, fillWithNones in list order, conflict scans
 // and cycle() execution in LinkedHashMap insertion order), so every ORDERED decision runs
 // wave-uniformly (all lanes agree, scalar branches), while every order-free sub-problem
-// (candidate search, row decode, legality, conflict flags, ready flags, death compaction,
-// observation planes, legal-action masks) runs lane-parallel with ballots/reductions.
-// No MFMA: integer/indexing work (see DESIGN.md).
+// (row fetch + decode, legality, conflict flags, ready ranking, death compaction, visibility,
+// observation planes, legal-action masks) runs lane-parallel with ballots and DPP reductions.
+// No MFMA: integer/indexing work (DESIGN.md §Kernels).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,6 +22,7 @@ using namespace mrts;
 namespace {
 
 constexpr uint16_t EMPTY = 0xFFFF, WALL = 0xFFFE;
+constexpr int INF = 0x7FFFFFFF;
 enum { T_NONE = 0, T_MOVE = 1, T_HARVEST = 2, T_RETURN = 3, T_PRODUCE = 4, T_ATTACK = 5 };
 enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2 };
 enum : uint32_t {
@@ -51,16 +52,29 @@ DEV int clampdir(int d) { return (d >= 0 && d <= 3) ? d : ACT_INVALID; }
 
 DEV int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
 DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-DEV int wave_min(int v) {
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return uni(v);
-}
-DEV int wave_sum(int v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return uni(v);
-}
+DEV uint32_t uniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 DEV uint64_t ballot(bool p) { return __ballot(p); }
+DEV int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
 DEV void wsync() { __syncthreads(); }  // one wave per workgroup: s_barrier is nearly free
+
+// Whole-wave reductions with DPP (GFX9 row_bcast forms): quad swaps, half-row and row mirrors
+// reduce each 16-lane row; row_bcast:15/31 chain the rows; lane 63 holds the result.
+template <bool MIN>
+DEV int wave_reduce(int v) {
+    const int id = MIN ? INF : 0;
+    auto op = [](int a, int b) { return MIN ? min(a, b) : a + b; };
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xF, 0xF, false));  // row_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+DEV int wave_min(int v) { return wave_reduce<true>(v); }
+DEV int wave_sum(int v) { return wave_reduce<false>(v); }
 
 // java.util.Random (48-bit LCG, JDK 8) — GameState.r / UnitAction.r / Sampler.generator, per game
 struct JRand {
@@ -79,37 +93,55 @@ struct JRand {
         return val;
     }
 };
+DEV uint64_t rng_of(int lo, int hi) { return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32); }
+
+// Snapshot byte per unit for PartiallyObservableGameState views (rts/PartiallyObservableGameState.java:90-109):
+// bit p = unit is in player p's snapshot list; bits 2-4 / 5-7 = (snapshot UAA action type + 1), 0 = none.
+DEV int snap_in(uint32_t b, int p) { return (b >> p) & 1; }
+DEV int snap_act(uint32_t b, int p) { return (int)((b >> (2 + 3 * p)) & 7); }
 
 struct Game {
-    const KParams& P;
+    const KStatic& P;
+    const KDyn D;
     const DevUtt& U;
     int g, H, W, HW, CAP;
-    uint32_t* uc;   // unit core: x | y<<8 | type<<16 | (player+1)<<20 | dead<<31
-    uint32_t* ua;   // assignment: type | utype<<4 | tx<<8 | ty<<16 | PRESENT/READY/PA flags
-    int32_t* at;    // assignment issue time (UnitActionAssignment.time)
-    int32_t* as;    // assignment insertion sequence number
+    bool po;
+    uint32_t* uc;    // unit core: x | y<<8 | type<<16 | (player+1)<<20 | dead<<31
+    uint32_t* ua;    // assignment: type | utype<<4 | tx<<8 | ty<<16 | PRESENT/READY/PA/DEC/BAD
+    int32_t* at;     // assignment issue time (UnitActionAssignment.time)
+    int32_t* as;     // assignment insertion sequence number (LinkedHashMap order)
+    uint32_t* bits;  // running ResourceUsage positions, indices [-W, HW+W)
+    uint32_t* scell; // PO: last snapshot unit per cell (slot+1, 0 = none)
+    int32_t* rseq;   // ready-list scratch (64)
     int16_t* hp;
     int16_t* res;
-    int16_t* par;   // UnitAction.parameter (direction / NONE duration)
-    uint16_t* cell; // cell -> slot, EMPTY or WALL
-    uint32_t* bits; // running ResourceUsage positions, indices [-W, HW+W)
+    int16_t* par;    // UnitAction.parameter (direction / NONE duration)
+    uint16_t* cell;  // cell -> slot, EMPTY or WALL
+    uint16_t* rslot; // ready-list scratch (64)
+    uint8_t* snap;   // PO snapshot bits
     // wave-uniform scalars (only ever modified in uniform control flow)
     int time, nu, pres0, pres1, seq, steps, ccnt, deaths;
+    int snapLimit0, snapLimit1;  // seq counter when player 0 / 1's snapshot was taken
     uint32_t err;
     JRand rngCancel, rngDamage, rngSampler;
 
-    DEV Game(const KParams& p, uint8_t* smem)
-        : P(p), U(p.utt), g((int)blockIdx.x), H(p.H), W(p.W), HW(p.HW), CAP(p.CAP) {
+    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem)
+        : P(p), D(d), U(p.utt), g((int)blockIdx.x), H(p.H), W(p.W), HW(p.HW), CAP(p.CAP), po(p.partial_obs != 0) {
         uint8_t* q = smem;
         uc = (uint32_t*)q; q += 4 * CAP;
         ua = (uint32_t*)q; q += 4 * CAP;
         at = (int32_t*)q; q += 4 * CAP;
         as = (int32_t*)q; q += 4 * CAP;
         bits = (uint32_t*)q; q += 4 * ((HW + 2 * W + 31) / 32);
+        rseq = (int32_t*)q; q += 4 * 64;
+        scell = (uint32_t*)q; q += po ? 4 * HW : 0;
         hp = (int16_t*)q; q += 2 * CAP;
         res = (int16_t*)q; q += 2 * CAP;
         par = (int16_t*)q; q += 2 * CAP;
-        cell = (uint16_t*)q;
+        cell = (uint16_t*)q; q += 2 * HW;
+        rslot = (uint16_t*)q; q += 2 * 64;
+        snap = (uint8_t*)q;
+        snapLimit0 = snapLimit1 = 0;
     }
     DEV int pres(int p) const { return p == 0 ? pres0 : pres1; }
     DEV void addPres(int p, int v) {
@@ -133,12 +165,12 @@ struct Game {
         return 0;
     }
     DEV int etaSlot(int s) const {
-        uint32_t a = ua[s];
+        const uint32_t a = ua[s];
         return eta(ua_type(a), par[s], ua_ut(a), utyp(uc[s]));
     }
 
     // ------------------------------------------------------------------ state load / store
-    DEV void initCells() {  // terrain walls from the map template, units on top
+    DEV void initCells() {  // terrain walls from the map template
         const int32_t* t = tmpl();
         const int nu_t = t[T_NU];
         const uint8_t* terr = (const uint8_t*)(t + T_UNITS + 3 * nu_t);
@@ -147,14 +179,13 @@ struct Game {
     }
     DEV void placeUnits() {
         for (int i = lane_id(); i < nu; i += 64) {
-            uint32_t c = uc[i];
+            const uint32_t c = uc[i];
             if (!(c & UC_DEAD)) cell[uy(c) * W + ux(c)] = (uint16_t)i;
         }
         wsync();
     }
-    DEV void load() {
-        const int32_t* s = st();
-        int hv = lane_id() < H_WORDS ? s[lane_id()] : 0;
+    DEV void loadHeader(const int32_t* s) {
+        const int hv = lane_id() < H_WORDS ? s[lane_id()] : 0;
         time = rl(hv, H_TIME);
         nu = rl(hv, H_NU);
         pres0 = rl(hv, H_RES0);
@@ -163,10 +194,14 @@ struct Game {
         steps = rl(hv, H_STEPS);
         err = (uint32_t)rl(hv, H_ERR);
         ccnt = rl(hv, H_CANCEL_CNT);
-        rngCancel.s = (uint64_t)(uint32_t)rl(hv, H_RNG_CANCEL) | ((uint64_t)(uint32_t)rl(hv, H_RNG_CANCEL + 1) << 32);
-        rngDamage.s = (uint64_t)(uint32_t)rl(hv, H_RNG_DAMAGE) | ((uint64_t)(uint32_t)rl(hv, H_RNG_DAMAGE + 1) << 32);
-        rngSampler.s = (uint64_t)(uint32_t)rl(hv, H_RNG_SAMPLER) | ((uint64_t)(uint32_t)rl(hv, H_RNG_SAMPLER + 1) << 32);
+        rngCancel.s = rng_of(rl(hv, H_RNG_CANCEL), rl(hv, H_RNG_CANCEL + 1));
+        rngDamage.s = rng_of(rl(hv, H_RNG_DAMAGE), rl(hv, H_RNG_DAMAGE + 1));
+        rngSampler.s = rng_of(rl(hv, H_RNG_SAMPLER), rl(hv, H_RNG_SAMPLER + 1));
         deaths = 0;
+    }
+    DEV void load() {
+        const int32_t* s = st();
+        loadHeader(s);
         const int32_t* arr = s + H_WORDS;
         for (int i = lane_id(); i < nu; i += 64) {
             uc[i] = (uint32_t)arr[A_UC * CAP + i];
@@ -182,7 +217,7 @@ struct Game {
     }
     DEV void store() {
         int32_t* s = st();
-        int l = lane_id();
+        const int l = lane_id();
         int hv = 0;
         switch (l) {
             case H_TIME: hv = time; break;
@@ -239,27 +274,69 @@ struct Game {
         placeUnits();
     }
 
-    // ------------------------------------------------------------------ decode (fromVectorAction)
-    // Base reservations of every current assignment (PlayerAction.java:497-505, the merge at
-    // ResourceUsage.java:92-97); returns their per-player resource sums.
-    DEV void baseReservations(int& r0, int& r1) {
+    // ------------------------------------------------------------------ row fetch + decode
+    // UnitAction.fromVectorAction (rts/UnitAction.java:675-709) for every idle unit of the external
+    // player(s), lane-parallel, in ONE round of global loads: a pure function of (row, unit).  The
+    // decoded action is parked in the unit's empty assignment fields with UA_DEC.
+    DEV void predecode(const int32_t* rows0, const int32_t* rows1, int only) {
+        const int R = U.maxAttackRadius, ctr = R / 2;
+        bool bad_any = false;
+        for (int o = lane_id(); o < nu; o += 64) {
+            const uint32_t cu = uc[o];
+            const int pl = uplay(cu);
+            if (pl < 0 || (ua[o] & UA_PRESENT) || (only >= 0 && pl != only)) continue;
+            const int x = ux(cu), y = uy(cu), c = y * W + x;
+            const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)c * 7;
+            const int a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], a4 = r[4], a5 = r[5], a6 = r[6];
+            int t = (a0 >= 0 && a0 <= 5) ? a0 : ACT_INVALID, pr = -1, ut = 0, tx = 0, ty = 0;
+            bool bad = false;
+            switch (t) {
+                case T_MOVE: pr = clampdir(a1); break;
+                case T_HARVEST: pr = clampdir(a2); break;
+                case T_RETURN: pr = clampdir(a3); break;
+                case T_PRODUCE:
+                    pr = clampdir(a4);
+                    if (a5 < 0 || a5 >= U.ntypes) bad = true;  // utt.getUnitType(int) throws (:697)
+                    else ut = a5;
+                    break;
+                case T_ATTACK: {
+                    const int ax = x + (a6 % R - ctr), ay = y + (a6 / R - ctr);
+                    if (inb(ax, ay)) {
+                        tx = ax;
+                        ty = ay;
+                    } else {
+                        tx = ty = 255;  // off-map target: never legal
+                    }
+                } break;
+            }
+            bad_any |= bad;
+            ua[o] = pack_ua(t, ut, tx, ty) | UA_DEC | (bad ? UA_BAD : 0u);
+            par[o] = (int16_t)pr;
+        }
+        if (ballot(bad_any)) err |= E_PRODUCE_TYPE;
+        wsync();
+    }
+
+    // Base reservations of every current assignment the deciding view holds (PlayerAction.java:497-505,
+    // merged as ResourceUsage.java:92-97); in a PO view only snapshot units' assignments count.
+    DEV void baseReservations(int p, int& r0, int& r1) {
         const int NB = (HW + 2 * W + 31) / 32;
         for (int i = lane_id(); i < NB; i += 64) bits[i] = 0;
         wsync();
         int s0 = 0, s1 = 0;
         for (int o = lane_id(); o < nu; o += 64) {
-            uint32_t a = ua[o];
-            if (a & UA_PRESENT) {
-                int t = ua_type(a);
-                if (t == T_MOVE || t == T_PRODUCE) {
-                    uint32_t c = uc[o];
-                    int d = par[o];
-                    int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
-                    atomicOr(&bits[pos >> 5], 1u << (pos & 31));
-                    if (t == T_PRODUCE) {
-                        if (uplay(c) == 0) s0 += U.cost[ua_ut(a)];
-                        else s1 += U.cost[ua_ut(a)];
-                    }
+            const uint32_t a = ua[o];
+            if (!(a & UA_PRESENT)) continue;
+            if (po && !snap_in(snap[o], p)) continue;
+            const int t = ua_type(a);
+            if (t == T_MOVE || t == T_PRODUCE) {
+                const uint32_t c = uc[o];
+                const int d = par[o];
+                const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
+                atomicOr(&bits[pos >> 5], 1u << (pos & 31));
+                if (t == T_PRODUCE) {
+                    if (uplay(c) == 0) s0 += U.cost[ua_ut(a)];
+                    else s1 += U.cost[ua_ut(a)];
                 }
             }
         }
@@ -268,63 +345,35 @@ struct Game {
         wsync();
     }
 
-    // PlayerAction.fromVectorAction (rts/PlayerAction.java:495-528) + UnitAction.fromVectorAction
-    // (rts/UnitAction.java:675-709): rows in ascending cell order; a row is decoded iff the unit at
-    // its cell is owned by p and has no assignment; accepted iff ua.ru.consistentWith(running ru)
-    // (rts/ResourceUsage.java:31-50).  Accepted actions are parked in the unit's (empty) assignment
-    // fields with the UA_PA flag.
-    DEV void decode(int p, const int32_t* rows) {
+    // PlayerAction.fromVectorAction (rts/PlayerAction.java:495-528): decoded rows in ascending cell
+    // order; accepted iff ua.ru.consistentWith(running ru) (rts/ResourceUsage.java:31-50).  Only the
+    // acceptance chain is serial; accepted units get UA_PA.
+    DEV void decode(int p) {
         int run0, run1;
-        baseReservations(run0, run1);
-        const int R = U.maxAttackRadius, ctr = R / 2;
+        baseReservations(p, run0, run1);
         for (int c0 = 0; c0 < HW; c0 += 64) {
             const int c = c0 + lane_id();
             const int s = c < HW ? cell[c] : EMPTY;
-            const uint32_t cu = s < CAP ? uc[s] : 0u;
-            const bool cand = s < CAP && uplay(cu) == p && !(ua[s] & UA_PRESENT);
+            uint32_t a = 0;
+            bool cand = false;
+            if (s < CAP) {
+                a = ua[s];
+                cand = uplay(uc[s]) == p && (a & UA_DEC) && !(a & (UA_PRESENT | UA_BAD));
+            }
             uint64_t m = ballot(cand);
             if (m == 0) continue;
-            int t = 0, pr = -1, ut = 0, tx = 0, ty = 0, tpos = 0, cost = 0;
-            bool usesPos = false, bad = false;
-            if (cand) {
-                const int32_t* r = rows + (size_t)c * 7;
-                const int a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], a4 = r[4], a5 = r[5], a6 = r[6];
-                const int x = ux(cu), y = uy(cu);
-                t = (a0 >= 0 && a0 <= 5) ? a0 : ACT_INVALID;
-                switch (t) {
-                    case T_MOVE: pr = clampdir(a1); break;
-                    case T_HARVEST: pr = clampdir(a2); break;
-                    case T_RETURN: pr = clampdir(a3); break;
-                    case T_PRODUCE:
-                        pr = clampdir(a4);
-                        if (a5 < 0 || a5 >= U.ntypes) bad = true;  // utt.getUnitType(int) throws
-                        else ut = a5;
-                        break;
-                    case T_ATTACK: {
-                        const int ax = x + (a6 % R - ctr), ay = y + (a6 / R - ctr);
-                        if (inb(ax, ay)) {
-                            tx = ax;
-                            ty = ay;
-                        } else {
-                            tx = ty = 255;  // off-map target: never legal
-                        }
-                    } break;
-                }
-                usesPos = (t == T_MOVE || t == T_PRODUCE);
-                tpos = c + dyo(pr) * W + dxo(pr);  // ResourceUsage position (UnitAction.java:254-291)
-                cost = (t == T_PRODUCE && !bad) ? U.cost[ut] : 0;
-            }
-            if (ballot(bad)) err |= E_PRODUCE_TYPE;
+            const int t = ua_type(a), pr = par[s < CAP ? s : 0];
+            const bool usesPos = cand && (t == T_MOVE || t == T_PRODUCE);
+            const int tpos = c + dyo(pr) * W + dxo(pr) + W;  // ResourceUsage position (UnitAction.java:254-291)
+            const int cost = (cand && t == T_PRODUCE) ? U.cost[ua_ut(a)] : 0;
             uint64_t acc = 0;
             while (m) {
                 const int k = __builtin_ctzll(m);
                 m &= m - 1;
-                if (rl(bad, k)) continue;
                 const bool up = rl(usesPos, k);
-                const int tp = rl(tpos, k), cst = rl(cost, k);
+                const int bi = rl(tpos, k), cst = rl(cost, k);
                 bool ok = true;
-                const int bi = tp + W;
-                if (up) ok = !((bits[bi >> 5] >> (bi & 31)) & 1u);
+                if (up) ok = !((uniu(bits[bi >> 5]) >> (bi & 31)) & 1u);
                 if (run0 != 0) {
                     const int sum = (p == 0 ? cst : 0) + run0;
                     if (sum > 0 && sum > pres0) ok = false;
@@ -340,10 +389,7 @@ struct Game {
                     acc |= 1ull << k;
                 }
             }
-            if ((acc >> lane_id()) & 1ull) {
-                ua[s] = pack_ua(t, ut, tx, ty) | UA_PA;
-                par[s] = (int16_t)pr;
-            }
+            if ((acc >> lane_id()) & 1ull) ua[s] = a | UA_PA;
             wsync();
         }
     }
@@ -420,42 +466,50 @@ struct Game {
         }
     }
 
+    // Does present assignment o conflict with a new MOVE/PRODUCE (target ntgt, producer player pl,
+    // cost ncost) — !old.ru.consistentWith(new ru) (GameState.java:264, ResourceUsage.java:31-50)
+    DEV bool conflicts(int o, int ntgt, bool nProduce, int ncost, int pl) const {
+        const uint32_t a = ua[o];
+        if (!(a & UA_PRESENT)) return false;
+        const int ot = ua_type(a);
+        if (ot != T_MOVE && ot != T_PRODUCE) return false;
+        const uint32_t oc = uc[o];
+        const int od = par[o];
+        if (((uy(oc) + dyo(od)) * W + ux(oc) + dxo(od)) == ntgt) return true;
+        if (nProduce) {
+            const int ores = (ot == T_PRODUCE && uplay(oc) == pl) ? U.cost[ua_ut(a)] : 0;
+            const int sum = ores + ncost;
+            if (sum > 0 && sum > pres(pl)) return true;
+        }
+        return false;
+    }
+
     // GameState.issue for one pair (rts/GameState.java:252-326), wave-uniform arguments.
     DEV void issueOne(int s, int t, int prm, int tx, int ty, int ut) {
         if (t == T_MOVE || t == T_PRODUCE) {
-            const uint32_t cu = uc[s];
+            const uint32_t cu = uniu(uc[s]);
             const int pl = uplay(cu), typ = utyp(cu);
             const int ntgt = (uy(cu) + dyo(prm)) * W + ux(cu) + dxo(prm);
             const bool nProduce = (t == T_PRODUCE);
             const int ncost = nProduce ? U.cost[ut] : 0;
+            bool any = false;
+            for (int o0 = 0; o0 < nu; o0 += 64) {
+                const int o = o0 + lane_id();
+                any |= ballot(o < nu && conflicts(o, ntgt, nProduce, ncost, pl)) != 0;
+            }
             int lastSeq = -1;
-            while (true) {
-                // next conflicting assignment in insertion order (consistentWith against the
-                // ORIGINAL ru of the new action; the old action as it is now)
-                int best = 0x7FFFFFFF;
-                for (int o = lane_id(); o < nu; o += 64) {
-                    const uint32_t a = ua[o];
-                    if (!(a & UA_PRESENT) || as[o] <= lastSeq) continue;
-                    const int ot = ua_type(a);
-                    if (ot != T_MOVE && ot != T_PRODUCE) continue;
-                    const uint32_t oc = uc[o];
-                    const int od = par[o];
-                    bool conf = ((uy(oc) + dyo(od)) * W + ux(oc) + dxo(od)) == ntgt;
-                    if (nProduce) {
-                        const int ores = (ot == T_PRODUCE && uplay(oc) == pl) ? U.cost[ua_ut(a)] : 0;
-                        const int sum = ores + ncost;
-                        if (sum > 0 && sum > pres(pl)) conf = true;
-                    }
-                    if (conf) best = min(best, as[o]);
-                }
+            while (any) {  // rare: resolve the conflicting assignments in insertion order
+                int best = INF;
+                for (int o = lane_id(); o < nu; o += 64)
+                    if (as[o] > lastSeq && conflicts(o, ntgt, nProduce, ncost, pl)) best = min(best, as[o]);
                 best = wave_min(best);
-                if (best == 0x7FFFFFFF) break;
-                int os = -1;
+                if (best == INF) break;
+                int os = INF;
                 for (int o = lane_id(); o < nu; o += 64)
                     if ((ua[o] & UA_PRESENT) && as[o] == best) os = o;
-                os = wave_min(os < 0 ? 0x7FFFFFFF : os);
+                os = wave_min(os);
                 lastSeq = best;
-                if (at[os] == time) {  // same-cycle conflict: policy (GameState.java:266-297)
+                if (uni(at[os]) == time) {  // same-cycle conflict: policy (GameState.java:266-297)
                     bool cold = false, cnew = false;
                     if (U.crs == 2) {
                         if (rngCancel.nextInt(2) == 0) cnew = true;
@@ -467,12 +521,21 @@ struct Game {
                     } else {
                         cold = cnew = true;
                     }
-                    const int d1 = etaSlot(os);
+                    const int d1 = uni(etaSlot(os));
                     const int d2 = eta(t, prm, ut, typ);
                     const int md = min(d1, d2);
-                    if (cold && lane_id() == 0) {
-                        ua[os] = pack_ua(T_NONE, 0, 0, 0) | UA_PRESENT;
-                        par[os] = (int16_t)md;
+                    if (cold) {
+                        if (lane_id() == 0) {
+                            ua[os] = pack_ua(T_NONE, 0, 0, 0) | UA_PRESENT;
+                            par[os] = (int16_t)md;
+                            if (po) {  // the mutated UAA object is shared with the PO snapshots holding it
+                                uint32_t b = snap[os];
+                                for (int q = 0; q < 2; q++)
+                                    if (snap_in(b, q) && snap_act(b, q) && as[os] < (q == 0 ? snapLimit0 : snapLimit1))
+                                        b = (b & ~(7u << (2 + 3 * q))) | ((uint32_t)(T_NONE + 1) << (2 + 3 * q));
+                                snap[os] = (uint8_t)b;
+                            }
+                        }
                     }
                     if (cnew) {
                         t = T_NONE;
@@ -540,30 +603,78 @@ struct Game {
         }
     }
 
+    // ------------------------------------------------------------------ PO snapshot
+    // new PartiallyObservableGameState(gs, p) (rts/PartiallyObservableGameState.java:90-109):
+    // the list keeps p's units and every other unit whose cell p observes (:116-126); the
+    // assignment map is the live one at this moment (UAA objects shared).
+    DEV void snapshot(int p) {
+        // observer units: positions + sight, gathered per 64-slot chunk and broadcast by readlane
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            uint32_t cu = 0;
+            bool live = false;
+            if (o < nu) {
+                cu = uc[o];
+                live = !(cu & UC_DEAD);
+            }
+            bool vis = live && uplay(cu) == p;
+            const int x = ux(cu), y = uy(cu);
+            for (int q0 = 0; q0 < nu; q0 += 64) {
+                const int q = q0 + lane_id();
+                uint32_t qc = q < nu ? uc[q] : UC_DEAD;
+                uint64_t m = ballot(!(qc & UC_DEAD) && uplay(qc) == p);
+                while (m) {
+                    const int k = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t oc = (uint32_t)rl((int)qc, k);
+                    const int sr = U.sight[utyp(oc)];
+                    const int dx = ux(oc) - x, dy = uy(oc) - y;
+                    vis |= dx * dx + dy * dy <= sr * sr;
+                }
+            }
+            if (o < nu) {
+                uint32_t b = snap[o] & ~(1u << p) & ~(7u << (2 + 3 * p));
+                if (live && vis) {
+                    b |= 1u << p;
+                    const uint32_t a = ua[o];
+                    if (a & UA_PRESENT) b |= (uint32_t)(ua_type(a) + 1) << (2 + 3 * p);
+                }
+                snap[o] = (uint8_t)b;
+            }
+        }
+        if (p == 0) snapLimit0 = seq;
+        else snapLimit1 = seq;
+        wsync();
+    }
+    DEV void clearSnap() {
+        for (int o = lane_id(); o < CAP; o += 64) snap[o] = 0;
+        wsync();
+    }
+
     // ------------------------------------------------------------------ cycle
     DEV void kill(int k) {  // GameState.removeUnit (rts/GameState.java:79-82)
         if (lane_id() == 0) {
             const uint32_t c = uc[k];
             uc[k] = c | UC_DEAD;
             cell[uy(c) * W + ux(c)] = EMPTY;
-            ua[k] &= ~UA_PRESENT;  // stays READY if it is in this cycle's snapshot
+            ua[k] &= ~UA_PRESENT;
         }
         deaths++;
         wsync();
     }
     // UnitAction.execute (rts/UnitAction.java:338-465) — also for units killed earlier in the loop
     DEV void execute(int s) {
-        const uint32_t cu = uc[s];
+        const uint32_t cu = uniu(uc[s]);
         const bool dead = cu & UC_DEAD;
         const int x = ux(cu), y = uy(cu), typ = utyp(cu), pl = uplay(cu);
-        const uint32_t a = ua[s];
+        const uint32_t a = uniu(ua[s]);
         const int t = ua_type(a);
-        const int prm = par[s];
+        const int prm = uni(par[s]);
         switch (t) {
             case T_MOVE: {
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
                 if (!dead) {
-                    if (cell[ny * W + nx] != EMPTY) err |= E_COLLISION;
+                    if (uni(cell[ny * W + nx]) != EMPTY) err |= E_COLLISION;
                     if (lane_id() == 0) {
                         cell[y * W + x] = EMPTY;
                         cell[ny * W + nx] = (uint16_t)s;
@@ -573,11 +684,11 @@ struct Game {
                 wsync();
             } break;
             case T_ATTACK: {
-                const int n = cell[ua_ty(a) * W + ua_tx(a)];
+                const int n = uni(cell[ua_ty(a) * W + ua_tx(a)]);
                 if (n < CAP) {
                     int dmg = U.minD[typ];
                     if (U.minD[typ] != U.maxD[typ]) dmg = U.minD[typ] + rngDamage.nextInt(1 + (U.maxD[typ] - U.minD[typ]));
-                    const int nhp = hp[n] - dmg;
+                    const int nhp = uni(hp[n]) - dmg;
                     if (lane_id() == 0) hp[n] = (int16_t)nhp;
                     wsync();
                     if (nhp <= 0) kill(n);
@@ -586,9 +697,9 @@ struct Game {
             case T_HARVEST: {
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
                 if (inb(nx, ny)) {
-                    const int n = cell[ny * W + nx];
-                    if (n < CAP && (U.flags[utyp(uc[n])] & F_RESOURCE) && (U.flags[typ] & F_HARVEST) && res[s] == 0) {
-                        const int nr = res[n] - U.harvestAmt[typ];
+                    const int n = uni(cell[ny * W + nx]);
+                    if (n < CAP && (U.flags[utyp(uniu(uc[n]))] & F_RESOURCE) && (U.flags[typ] & F_HARVEST) && uni(res[s]) == 0) {
+                        const int nr = uni(res[n]) - U.harvestAmt[typ];
                         if (lane_id() == 0) {
                             res[n] = (int16_t)nr;
                             res[s] = (int16_t)U.harvestAmt[typ];
@@ -601,9 +712,9 @@ struct Game {
             case T_RETURN: {
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
                 if (inb(nx, ny)) {
-                    const int n = cell[ny * W + nx];
-                    const int carried = res[s];
-                    if (n < CAP && (U.flags[utyp(uc[n])] & F_STOCKPILE) && carried > 0) {
+                    const int n = uni(cell[ny * W + nx]);
+                    const int carried = uni(res[s]);
+                    if (n < CAP && (U.flags[utyp(uniu(uc[n]))] & F_STOCKPILE) && carried > 0) {
                         addPres(pl, carried);
                         if (lane_id() == 0) res[s] = 0;
                         wsync();
@@ -614,7 +725,7 @@ struct Game {
                 const int ut = ua_ut(a);
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
                 if (pres(pl) - U.cost[ut] >= 0) {
-                    if (cell[ny * W + nx] != EMPTY) {
+                    if (uni(cell[ny * W + nx]) != EMPTY) {
                         err |= E_ADDUNIT;  // PhysicalGameState.addUnit throws (:190-195)
                     } else if (nu >= CAP) {
                         err |= E_CAPACITY;
@@ -626,6 +737,7 @@ struct Game {
                             ua[nu] = 0;
                             par[nu] = -1;
                             cell[ny * W + nx] = (uint16_t)nu;
+                            if (po) snap[nu] = 0;  // produced this step: in no snapshot
                         }
                         nu++;
                         addPres(pl, -U.cost[ut]);
@@ -638,42 +750,73 @@ struct Game {
             default: break;
         }
     }
-    // GameState.cycle (rts/GameState.java:553-571); returns gameover()
+    // GameState.cycle (rts/GameState.java:553-571): time++, snapshot the ready assignments
+    // (ETA + issue time <= time) in insertion order, then remove + execute each in that order.
     DEV void cycle() {
         time++;
-        for (int o = lane_id(); o < nu; o += 64) {
-            const uint32_t a = ua[o];
-            if ((a & UA_PRESENT) && etaSlot(o) + at[o] <= time) ua[o] = a | UA_READY;
+        // gather the ready list into LDS (slot order), count R
+        int R = 0;
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            bool ready = false;
+            if (o < nu) {
+                const uint32_t a = ua[o];
+                ready = (a & UA_PRESENT) && etaSlot(o) + at[o] <= time;
+            }
+            const uint64_t m = ballot(ready);
+            const int idx = R + lanes_below(m);
+            if (ready && idx < 64) {
+                rslot[idx] = (uint16_t)o;
+                rseq[idx] = as[o];
+            }
+            if (ready) ua[o] |= UA_READY;
+            R += __popcll(m);
         }
         wsync();
-        while (true) {
-            int best = 0x7FFFFFFF;
-            for (int o = lane_id(); o < nu; o += 64)
-                if (ua[o] & UA_READY) best = min(best, as[o]);
-            best = wave_min(best);
-            if (best == 0x7FFFFFFF) break;
-            int os = 0x7FFFFFFF;
-            for (int o = lane_id(); o < nu; o += 64)
-                if ((ua[o] & UA_READY) && as[o] == best) os = o;
-            os = wave_min(os);
-            if (lane_id() == 0) ua[os] &= ~(UA_READY | UA_PRESENT);
+        if (R == 0) return;
+        if (R <= 64) {
+            // rank by insertion sequence: lane k holds ready item k
+            const int k = lane_id();
+            const int myseq = k < R ? rseq[k] : INF;
+            const int myslot = k < R ? rslot[k] : 0;
+            int rank = 0;
+            for (int j = 0; j < R; j++) rank += rl(myseq, j) < myseq;
             wsync();
-            execute(os);
+            if (k < R) rslot[rank] = (uint16_t)myslot;
+            wsync();
+            for (int r = 0; r < R; r++) {
+                const int os = uni(rslot[r]);
+                if (lane_id() == 0) ua[os] &= ~(UA_READY | UA_PRESENT);
+                wsync();
+                execute(os);
+            }
+        } else {  // > 64 ready assignments: repeated minimum search
+            while (true) {
+                int best = INF;
+                for (int o = lane_id(); o < nu; o += 64)
+                    if (ua[o] & UA_READY) best = min(best, as[o]);
+                best = wave_min(best);
+                if (best == INF) break;
+                int os = INF;
+                for (int o = lane_id(); o < nu; o += 64)
+                    if ((ua[o] & UA_READY) && as[o] == best) os = o;
+                os = wave_min(os);
+                if (lane_id() == 0) ua[os] &= ~(UA_READY | UA_PRESENT);
+                wsync();
+                execute(os);
+            }
         }
     }
     // PhysicalGameState.gameover/winner (rts/PhysicalGameState.java:334-387)
     DEV void outcome(bool& gameover, int& winner) {
         int c0 = 0, c1 = 0;
-        for (int o = lane_id(); o < nu; o += 64) {
-            const uint32_t c = uc[o];
-            if (!(c & UC_DEAD)) {
-                const int p = uplay(c);
-                c0 += (p == 0);
-                c1 += (p == 1);
-            }
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            const uint32_t c = o < nu ? uc[o] : UC_DEAD;
+            const bool live = !(c & UC_DEAD);
+            c0 += __popcll(ballot(live && uplay(c) == 0));
+            c1 += __popcll(ballot(live && uplay(c) == 1));
         }
-        c0 = wave_sum(c0);
-        c1 = wave_sum(c1);
         gameover = (c0 + c1 == 0) || ((c0 > 0) != (c1 > 0));
         winner = (c0 > 0 && c1 == 0) ? 0 : ((c1 > 0 && c0 == 0) ? 1 : -1);
     }
@@ -684,7 +827,7 @@ struct Game {
             const int o = o0 + lane_id();
             const bool alive = o < nu && !(uc[o] & UC_DEAD);
             const uint64_t m = ballot(alive);
-            const int idx = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            const int idx = base + lanes_below(m);
             uint32_t c = 0, a = 0;
             int32_t t0 = 0, t1 = 0;
             int16_t h = 0, r = 0, pr = 0;
@@ -718,28 +861,119 @@ struct Game {
     }
 
     // ------------------------------------------------------------------ observation
-    // GameState.getVectorObservation (rts/GameState.java:922-968): 6 planes [C][H][W] int32
-    DEV void writeObs(int slot, int player) {
-        int32_t* o = P.obs + (size_t)slot * P.C * HW;
+    // GameState.getVectorObservation (rts/GameState.java:922-968): 6 planes [C][H][W] int32.
+    // Lane = 4 consecutive cells -> one dwordx4 store per plane.
+    DEV void obsCell(int c, int player, int v[6]) const {
+        const int s = cell[c];
+        v[0] = v[1] = v[2] = v[3] = v[4] = 0;
+        v[5] = (s == WALL) ? 1 : 0;
+        if (s < CAP) {
+            const uint32_t cu = uc[s];
+            const uint32_t a = ua[s];
+            const int pl = uplay(cu);
+            v[0] = hp[s];
+            v[1] = res[s];
+            v[2] = pl >= 0 ? ((pl + player) % 2) + 1 : 0;
+            v[3] = utyp(cu) + 1;
+            v[4] = (a & UA_PRESENT) ? ua_type(a) : 0;
+        }
+    }
+    DEV void writeObsFull(int slot0, int nslots, int player0) {
+        int32_t* o0 = D.obs + (size_t)slot0 * P.C * HW;
+        if ((HW & 3) == 0) {
+            for (int c4 = 4 * lane_id(); c4 < HW; c4 += 256) {
+                int v[4][6];
+#pragma unroll
+                for (int j = 0; j < 4; j++) obsCell(c4 + j, player0, v[j]);
+#pragma unroll
+                for (int pl = 0; pl < 6; pl++)
+                    *(int4*)(o0 + (size_t)pl * HW + c4) = make_int4(v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
+                if (nslots == 2) {  // the other player's view differs only in the owner plane
+                    int32_t* o1 = o0 + (size_t)P.C * HW;
+#pragma unroll
+                    for (int pl = 0; pl < 6; pl++) {
+                        int4 w = make_int4(v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
+                        if (pl == 2) {
+                            w.x = w.x ? 3 - w.x : 0;
+                            w.y = w.y ? 3 - w.y : 0;
+                            w.z = w.z ? 3 - w.z : 0;
+                            w.w = w.w ? 3 - w.w : 0;
+                        }
+                        *(int4*)(o1 + (size_t)pl * HW + c4) = w;
+                    }
+                }
+            }
+        } else {
+            for (int i = 0; i < nslots; i++) {
+                int32_t* o = o0 + (size_t)i * P.C * HW;
+                for (int c = lane_id(); c < HW; c += 64) {
+                    int v[6];
+                    obsCell(c, player0 + i, v);
+#pragma unroll
+                    for (int pl = 0; pl < 6; pl++) o[(size_t)pl * HW + c] = v[pl];
+                }
+            }
+        }
+    }
+    // PartiallyObservableGameState.getVectorObservation (rts/PartiallyObservableGameState.java:137-209):
+    // the snapshot's units (live fields, possibly dead) in list order, last writer per cell; the
+    // snapshot's assignments; walls; own / enemy sight disks of the snapshot units (:211-234).
+    DEV void writeObsPO(int slot, int p) {
+        for (int c = lane_id(); c < HW; c += 64) scell[c] = 0;
+        wsync();
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            if (o < nu && snap_in(snap[o], p)) {
+                const uint32_t cu = uc[o];
+                atomicMax(&scell[uy(cu) * W + ux(cu)], (uint32_t)(o + 1));
+            }
+        }
+        wsync();
+        int32_t* out = D.obs + (size_t)slot * P.C * HW;
         for (int c = lane_id(); c < HW; c += 64) {
-            const int s = cell[c];
+            const int s = (int)scell[c] - 1;
             int v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
-            if (s < CAP) {
+            if (s >= 0) {
                 const uint32_t cu = uc[s];
-                const uint32_t a = ua[s];
                 const int pl = uplay(cu);
                 v0 = hp[s];
                 v1 = res[s];
-                v2 = pl >= 0 ? ((pl + player) % 2) + 1 : 0;
+                v2 = pl >= 0 ? ((pl + p) % 2) + 1 : 0;
                 v3 = utyp(cu) + 1;
-                v4 = (a & UA_PRESENT) ? ua_type(a) : 0;
+                const int sa = snap_act(snap[s], p);
+                v4 = sa ? sa - 1 : 0;
             }
-            o[c] = v0;
-            o[HW + c] = v1;
-            o[2 * HW + c] = v2;
-            o[3 * HW + c] = v3;
-            o[4 * HW + c] = v4;
-            o[5 * HW + c] = (s == WALL) ? 1 : 0;
+            out[c] = v0;
+            out[HW + c] = v1;
+            out[2 * HW + c] = v2;
+            out[3 * HW + c] = v3;
+            out[4 * HW + c] = v4;
+            out[5 * HW + c] = cell[c] == WALL ? 1 : 0;
+        }
+        // visibility: lane = cell, uniform loop over the snapshot's owned units
+        for (int c0 = 0; c0 < HW; c0 += 64) {
+            const int c = c0 + lane_id();
+            const int cx = c % W, cy = c / W;
+            int mine = 0, theirs = 0;
+            for (int o0 = 0; o0 < nu; o0 += 64) {
+                const int o = o0 + lane_id();
+                const uint32_t oc = o < nu ? uc[o] : 0u;
+                uint64_t m = ballot(o < nu && snap_in(snap[o], p) && uplay(oc) >= 0);
+                while (m) {
+                    const int k = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t u = (uint32_t)rl((int)oc, k);
+                    const int sr = U.sight[utyp(u)];
+                    const int dx = cx - ux(u), dy = cy - uy(u);
+                    const bool in = abs(dx) <= sr && abs(dy) <= sr && dx * dx + dy * dy <= sr * sr;
+                    if (uplay(u) == p) mine |= in;
+                    else theirs |= in;
+                }
+            }
+            if (c < HW) {
+                out[6 * HW + c] = mine;
+                out[7 * HW + c] = theirs;
+            }
         }
     }
 
@@ -747,87 +981,79 @@ struct Game {
     // JNIGridnetClient.getMasks (tests/JNIGridnetClient.java:210-223) + UnitAction.getValidActionArray
     // (rts/UnitAction.java:711-751) over Unit.getUnitActions(gs, 10) (rts/units/Unit.java:382-522).
     DEV void unitMask(int s, uint32_t& w0, uint32_t& w1, uint32_t& w2) const {
-        w0 = w1 = w2 = 0;
+        uint64_t lo = 0;
+        uint32_t hi = 0;
         auto setb = [&](int k) {
-            if (k < 32) w0 |= 1u << k;
-            else if (k < 64) w1 |= 1u << (k - 32);
-            else w2 |= 1u << (k - 64);
+            if (k < 64) lo |= 1ull << k;
+            else hi |= 1u << (k - 64);
         };
         const uint32_t cu = uc[s];
         const int x = ux(cu), y = uy(cu), typ = utyp(cu), pl = uplay(cu);
         const uint32_t fl = U.flags[typ];
         const int nt = U.ntypes, R = U.maxAttackRadius, ctr = R / 2;
         const int atkBase = 1 + 6 + 16 + nt;
-        int nc[4];
-        bool nin[4];
-        for (int d = 0; d < 4; d++) {
-            const int nx = x + dxo(d), ny = y + dyo(d);
-            nin[d] = inb(nx, ny);
-            nc[d] = nin[d] ? cell[ny * W + nx] : WALL;
-        }
         setb(0);
         setb(1 + T_NONE);
-        if (fl & F_ATTACK) {
-            const int r = U.range[typ];
-            if (r == 1) {
-                for (int d = 0; d < 4; d++) {
-                    if (nc[d] < CAP) {
-                        const int op = uplay(uc[nc[d]]);
-                        if (op >= 0 && op != pl) {
-                            setb(1 + T_ATTACK);
-                            setb(atkBase + (ctr + dyo(d)) * R + (ctr + dxo(d)));
-                        }
-                    }
-                }
-            } else {
-                for (int dy = -r; dy <= r; dy++)
-                    for (int dx = -r; dx <= r; dx++) {
-                        if (dx * dx + dy * dy > r * r || !inb(x + dx, y + dy)) continue;
-                        const int n = cell[(y + dy) * W + x + dx];
-                        if (n < CAP) {
-                            const int op = uplay(uc[n]);
-                            if (op >= 0 && op != pl) {
-                                setb(1 + T_ATTACK);
-                                setb(atkBase + (ctr + dy) * R + (ctr + dx));
-                            }
-                        }
-                    }
-            }
-        }
-        if (fl & F_HARVEST) {
-            const int carried = res[s];
-            for (int d = 0; d < 4; d++) {
-                if (nc[d] >= CAP) continue;
-                const uint32_t oc = uc[nc[d]];
+        const bool canProduce = false;
+        (void)canProduce;
+        bool afford[MAX_PRODUCES];
+#pragma unroll
+        for (int i = 0; i < MAX_PRODUCES; i++) afford[i] = i < U.nprod[typ] && pres(pl) >= U.cost[U.prod[typ][i]];
+        const int carried = res[s];
+        const int r = U.range[typ];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int nx = x + dxo(d), ny = y + dyo(d);
+            const int n = inb(nx, ny) ? cell[ny * W + nx] : WALL;
+            if (n < CAP) {
+                const uint32_t oc = uc[n];
+                const int op = uplay(oc);
                 const uint32_t ofl = U.flags[utyp(oc)];
-                if (carried == 0 && (ofl & F_RESOURCE)) {
-                    setb(1 + T_HARVEST);
-                    setb(1 + 6 + 4 + d);
+                if ((fl & F_ATTACK) && r == 1 && op >= 0 && op != pl) {
+                    setb(1 + T_ATTACK);
+                    setb(atkBase + (ctr + dyo(d)) * R + (ctr + dxo(d)));
                 }
-                if (carried > 0 && (ofl & F_STOCKPILE) && uplay(oc) == pl) {
-                    setb(1 + T_RETURN);
-                    setb(1 + 6 + 8 + d);
+                if (fl & F_HARVEST) {
+                    if (carried == 0 && (ofl & F_RESOURCE)) {
+                        setb(1 + T_HARVEST);
+                        setb(1 + 6 + 4 + d);
+                    }
+                    if (carried > 0 && (ofl & F_STOCKPILE) && op == pl) {
+                        setb(1 + T_RETURN);
+                        setb(1 + 6 + 8 + d);
+                    }
                 }
-            }
-        }
-        for (int i = 0; i < U.nprod[typ]; i++) {
-            const int ut = U.prod[typ][i];
-            if (pres(pl) >= U.cost[ut]) {
-                for (int d = 0; d < 4; d++)
-                    if (nc[d] == EMPTY) {
+            } else if (n == EMPTY) {
+#pragma unroll
+                for (int i = 0; i < MAX_PRODUCES; i++)
+                    if (afford[i]) {
                         setb(1 + T_PRODUCE);
                         setb(1 + 6 + 12 + d);
-                        setb(1 + 6 + 16 + ut);
+                        setb(1 + 6 + 16 + U.prod[typ][i]);
                     }
-            }
-        }
-        if (fl & F_MOVE) {
-            for (int d = 0; d < 4; d++)
-                if (nc[d] == EMPTY) {
+                if (fl & F_MOVE) {
                     setb(1 + T_MOVE);
                     setb(1 + 6 + d);
                 }
+            }
         }
+        if ((fl & F_ATTACK) && r > 1) {
+            for (int dy = -r; dy <= r; dy++)
+                for (int dx = -r; dx <= r; dx++) {
+                    if (dx * dx + dy * dy > r * r || !inb(x + dx, y + dy)) continue;
+                    const int n = cell[(y + dy) * W + x + dx];
+                    if (n < CAP) {
+                        const int op = uplay(uc[n]);
+                        if (op >= 0 && op != pl) {
+                            setb(1 + T_ATTACK);
+                            setb(atkBase + (ctr + dy) * R + (ctr + dx));
+                        }
+                    }
+                }
+        }
+        w0 = (uint32_t)lo;
+        w1 = (uint32_t)(lo >> 32);
+        w2 = hi;
     }
     // Park each idle unit's 79-bit mask in its unused assignment words (at/as/ua low bits).
     DEV void stashMasks(int p) {
@@ -861,7 +1087,7 @@ struct Game {
     static DEV uint32_t expand4(uint32_t b) { return ((b & 0xFu) * 0x00204081u) & 0x01010101u; }
     DEV void writeMasks(int slot, int p) {
         const int K = U.K;
-        uint8_t* out = P.masks + (size_t)slot * HW * K;
+        uint8_t* out = D.masks + (size_t)slot * HW * K;
         const int total = HW * K;
         if ((total & 15) == 0) {
             for (int j = lane_id(); j < total / 16; j += 64) {
@@ -897,45 +1123,52 @@ struct Game {
 };
 
 template <int MODE>
-__global__ __launch_bounds__(64) void k_env(KParams P) {
+__global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
-    Game G(P, smem);
+    const KStatic& P = *PS;
+    Game G(P, D, smem);
     const bool selfplay = G.g < P.n_sp_games;
     const int slot0 = selfplay ? 2 * G.g : 2 * P.n_sp_games + (G.g - P.n_sp_games);
     const int nslots = selfplay ? 2 : 1;
+    const int agent = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
+    bool freshObs = true;  // observation comes from the current (post-step or fresh) state
 
     if (MODE == MODE_RESET) {
-        const int32_t* s = G.st();
-        int hv = lane_id() < H_WORDS ? s[lane_id()] : 0;
+        G.loadHeader(G.st());
         G.err = 0;
-        G.ccnt = rl(hv, H_CANCEL_CNT);
-        G.rngCancel.s = (uint64_t)(uint32_t)rl(hv, H_RNG_CANCEL) | ((uint64_t)(uint32_t)rl(hv, H_RNG_CANCEL + 1) << 32);
-        G.rngDamage.s = (uint64_t)(uint32_t)rl(hv, H_RNG_DAMAGE) | ((uint64_t)(uint32_t)rl(hv, H_RNG_DAMAGE + 1) << 32);
-        G.rngSampler.s = (uint64_t)(uint32_t)rl(hv, H_RNG_SAMPLER) | ((uint64_t)(uint32_t)rl(hv, H_RNG_SAMPLER + 1) << 32);
         G.initCells();
         G.resetFromTemplate();
         if (lane_id() < nslots) {
-            if (P.reward) P.reward[slot0 + lane_id()] = 0.0;
-            if (P.done) P.done[slot0 + lane_id()] = 0;
+            if (D.reward) D.reward[slot0 + lane_id()] = 0.0;
+            if (D.done) D.done[slot0 + lane_id()] = 0;
         }
     } else {
         G.load();
     }
+    if (G.po) G.clearSnap();
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
         if (selfplay) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
+            G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1);
             for (int p = 0; p < 2; p++) {
-                G.decode(p, P.actions + (size_t)(slot0 + p) * rowStride);
+                if (G.po) G.snapshot(p);
+                G.decode(p);
                 G.issuePlayer(p, 1);
             }
         } else {
-            // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203), PassiveAI opponent
-            const int player = P.players ? uni(P.players[slot0]) : 0;
-            G.decode(player, P.actions + (size_t)slot0 * rowStride);
-            G.issuePlayer(player, 1);
-            G.issuePlayer(1 - player, 10);  // PassiveAI.getAction = fillWithNones(gs, p, 10)
+            // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203), PassiveAI opponent:
+            // both views are taken and both actions computed before either issueSafe
+            const int32_t* rows = D.actions + (size_t)slot0 * rowStride;
+            G.predecode(rows, rows, agent);
+            if (G.po) {
+                G.snapshot(agent);
+                G.snapshot(1 - agent);
+            }
+            G.decode(agent);
+            G.issuePlayer(agent, 1);
+            G.issuePlayer(1 - agent, 10);  // PassiveAI.getAction = fillWithNones(gs, p, 10)
         }
         G.cycle();
         bool gameover;
@@ -947,25 +1180,35 @@ __global__ __launch_bounds__(64) void k_env(KParams P) {
         const bool reset = gameover || G.steps >= P.max_steps;
         if (lane_id() < nslots) {
             const int slot = slot0 + lane_id();
-            const int maxp = selfplay ? lane_id() : (P.players ? P.players[slot] : 0);
-            if (P.reward) P.reward[slot] = gameover ? (winner == maxp ? 1.0 : -1.0) : 0.0;
-            if (P.done) P.done[slot] = (gameover || reset) ? 1 : 0;
+            const int maxp = selfplay ? lane_id() : agent;
+            if (D.reward) D.reward[slot] = gameover ? (winner == maxp ? 1.0 : -1.0) : 0.0;
+            if (D.done) D.done[slot] = (gameover || reset) ? 1 : 0;
         }
-        if (reset) G.resetFromTemplate();
-        else if (G.deaths) G.compact();
+        if (reset) {
+            G.resetFromTemplate();
+            if (G.po) G.clearSnap();
+        } else {
+            freshObs = false;
+        }
     }
 
-    if (MODE != MODE_MASKS && P.obs) {
-        for (int i = 0; i < nslots; i++) {
-            const int player = selfplay ? i : (P.players ? P.players[slot0] : 0);
-            G.writeObs(slot0 + i, player);
+    if (MODE != MODE_MASKS && D.obs) {
+        if (G.po) {
+            for (int i = 0; i < nslots; i++) {
+                const int p = selfplay ? i : agent;
+                if (freshObs) G.snapshot(p);  // PO view of the reset state
+                G.writeObsPO(slot0 + i, p);
+            }
+        } else {
+            G.writeObsFull(slot0, nslots, selfplay ? 0 : agent);
         }
     }
-    if (P.masks) {
+    if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
+    if (D.masks) {
         wsync();
-        for (int i = 0; i < nslots; i++) G.stashMasks(selfplay ? i : P.mask_player);
+        for (int i = 0; i < nslots; i++) G.stashMasks(selfplay ? i : D.mask_player);
         wsync();
-        for (int i = 0; i < nslots; i++) G.writeMasks(slot0 + i, selfplay ? i : P.mask_player);
+        for (int i = 0; i < nslots; i++) G.writeMasks(slot0 + i, selfplay ? i : D.mask_player);
     }
     if (MODE != MODE_MASKS) {
         wsync();
@@ -997,47 +1240,76 @@ DEV int pickBit(uint32_t r, uint64_t bitsv, int n) {
     while (k--) bitsv &= bitsv - 1;
     return __builtin_ctzll(bitsv);
 }
+// one cell's action from its mask record (bytes m[0..K)), Philox counter (slot id, step, cell, 0)
+DEV void sampleCell(const PolicyParams& Q, const uint8_t* m, int slot, int c, int32_t a[7]) {
+    for (int k = 0; k < 7; k++) a[k] = 0;
+    if (!m[0]) return;
+    uint64_t lo = 0, hi = 0;  // mask slots 1..K-1 -> bit i-1
+    for (int i = 1; i < Q.K; i++) {
+        const uint64_t b = m[i] ? 1ull : 0ull;
+        if (i - 1 < 64) lo |= b << (i - 1);
+        else hi |= b << (i - 1 - 64);
+    }
+    uint32_t ctr[4] = {Q.slot_id_base + (uint32_t)slot, Q.step, (uint32_t)c, 0u};
+    philox(ctr, (uint32_t)Q.seed, (uint32_t)(Q.seed >> 32));
+    auto field = [&](int off, int n) -> uint64_t {  // mask slots [off, off+n) (off >= 1)
+        const int b = off - 1;
+        uint64_t v;
+        if (b >= 64) v = hi >> (b - 64);
+        else v = (lo >> b) | (b ? (hi << (64 - b)) : 0ull);
+        return n >= 64 ? v : (v & ((1ull << n) - 1));
+    };
+    const int t = pickBit(ctr[0], field(1, 6), 6);
+    if (t < 0) return;
+    a[0] = t;
+    switch (t) {
+        case 1: a[1] = pickBit(ctr[1], field(7, 4), 4); break;
+        case 2: a[2] = pickBit(ctr[1], field(11, 4), 4); break;
+        case 3: a[3] = pickBit(ctr[1], field(15, 4), 4); break;
+        case 4:
+            a[4] = pickBit(ctr[1], field(19, 4), 4);
+            a[5] = pickBit(ctr[2], field(23, Q.ntypes), Q.ntypes);
+            break;
+        case 5: {
+            const int off = 23 + Q.ntypes, n = Q.K - off;
+            a[6] = pickBit(ctr[1], field(off, n), n);
+        } break;
+    }
+}
+
+// Tiled form: one wave = 64 cells of one slot.  The 64 mask records (64*K bytes, 16-B aligned when
+// HW*K and 64*K are multiples of 16) stream into LDS with dwordx4 loads, the 64 action rows (1792 B)
+// stream out with dwordx4 stores.
+__global__ __launch_bounds__(64) void k_policy_tiled(PolicyParams Q) {
+    __shared__ __align__(16) uint8_t sm[64 * 96];
+    __shared__ __align__(16) int32_t sa[64 * 7];
+    const int lane = (int)threadIdx.x, slot = (int)blockIdx.y;
+    const int c0 = (int)blockIdx.x * 64;
+    const int ncell = min(64, Q.HW - c0);
+    const uint8_t* src = Q.masks + ((size_t)slot * Q.HW + c0) * Q.K;
+    const int nbytes = ncell * Q.K, n16 = nbytes >> 4;
+    for (int i = lane; i < n16; i += 64) ((uint4*)sm)[i] = ((const uint4*)src)[i];
+    for (int i = 16 * n16 + lane; i < nbytes; i += 64) sm[i] = src[i];
+    __syncthreads();
+    int32_t a[7];
+    if (lane < ncell) sampleCell(Q, sm + lane * Q.K, slot, c0 + lane, a);
+    else
+        for (int k = 0; k < 7; k++) a[k] = 0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) sa[lane * 7 + k] = a[k];
+    __syncthreads();
+    int32_t* dst = Q.actions + ((size_t)slot * Q.HW + c0) * 7;
+    const int nw = ncell * 7, nw4 = nw >> 2;
+    for (int i = lane; i < nw4; i += 64) ((int4*)dst)[i] = ((const int4*)sa)[i];
+    for (int i = 4 * nw4 + lane; i < nw; i += 64) dst[i] = sa[i];
+}
 
 __global__ __launch_bounds__(64) void k_policy(PolicyParams Q) {
     const int c = (int)(blockIdx.x * 64 + threadIdx.x);
     const int slot = (int)blockIdx.y;
     if (c >= Q.HW) return;
-    const uint8_t* m = Q.masks + ((size_t)slot * Q.HW + c) * Q.K;
-    int32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
-    if (m[0]) {
-        uint64_t lo = 0, hi = 0;  // mask bits 1..K-1 → bit i-1
-        for (int i = 1; i < Q.K; i++) {
-            const uint64_t b = m[i] ? 1ull : 0ull;
-            if (i - 1 < 64) lo |= b << (i - 1);
-            else hi |= b << (i - 1 - 64);
-        }
-        uint32_t ctr[4] = {Q.slot_id_base + (uint32_t)slot, Q.step, (uint32_t)c, 0u};
-        philox(ctr, (uint32_t)Q.seed, (uint32_t)(Q.seed >> 32));
-        auto field = [&](int off, int n) -> uint64_t {  // mask slots [off, off+n) (off >= 1)
-            const int b = off - 1;
-            uint64_t v;
-            if (b >= 64) v = hi >> (b - 64);
-            else v = (lo >> b) | (b ? (hi << (64 - b)) : 0ull);
-            return n >= 64 ? v : (v & ((1ull << n) - 1));
-        };
-        const int t = pickBit(ctr[0], field(1, 6), 6);
-        if (t >= 0) {
-            a[0] = t;
-            switch (t) {
-                case 1: a[1] = pickBit(ctr[1], field(7, 4), 4); break;
-                case 2: a[2] = pickBit(ctr[1], field(11, 4), 4); break;
-                case 3: a[3] = pickBit(ctr[1], field(15, 4), 4); break;
-                case 4:
-                    a[4] = pickBit(ctr[1], field(19, 4), 4);
-                    a[5] = pickBit(ctr[2], field(23, Q.ntypes), Q.ntypes);
-                    break;
-                case 5: {
-                    const int off = 23 + Q.ntypes, n = Q.K - off;
-                    a[6] = pickBit(ctr[1], field(off, n), n);
-                } break;
-            }
-        }
-    }
+    int32_t a[7];
+    sampleCell(Q, Q.masks + ((size_t)slot * Q.HW + c) * Q.K, slot, c, a);
     int32_t* out = Q.actions + ((size_t)slot * Q.HW + c) * 7;
 #pragma unroll
     for (int k = 0; k < 7; k++) out[k] = a[k];
@@ -1046,16 +1318,17 @@ __global__ __launch_bounds__(64) void k_policy(PolicyParams Q) {
 }  // namespace
 
 namespace mrts {
-size_t ldsBytes(int HW, int W, int CAP) {
-    return (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 6 * (size_t)CAP + 2 * (size_t)HW;
+size_t ldsBytes(int HW, int W, int CAP, int po) {
+    return (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + (po ? 4 * (size_t)HW : 0) +
+           6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
 }
-hipError_t launchEnv(int mode, const KParams& P, hipStream_t stream) {
-    const size_t lds = ldsBytes(P.HW, P.W, P.CAP);
-    dim3 grid((unsigned)P.n_games), block(64);
+hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
+    const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);
+    dim3 grid((unsigned)hs.n_games), block(64);
     switch (mode) {
-        case MODE_STEP: hipLaunchKernelGGL(k_env<MODE_STEP>, grid, block, lds, stream, P); break;
-        case MODE_RESET: hipLaunchKernelGGL(k_env<MODE_RESET>, grid, block, lds, stream, P); break;
-        default: hipLaunchKernelGGL(k_env<MODE_MASKS>, grid, block, lds, stream, P); break;
+        case MODE_STEP: hipLaunchKernelGGL(k_env<MODE_STEP>, grid, block, lds, stream, ds, D); break;
+        case MODE_RESET: hipLaunchKernelGGL(k_env<MODE_RESET>, grid, block, lds, stream, ds, D); break;
+        default: hipLaunchKernelGGL(k_env<MODE_MASKS>, grid, block, lds, stream, ds, D); break;
     }
     return hipGetLastError();
 }
@@ -1067,7 +1340,10 @@ hipError_t prepareLds(size_t bytes) {
 }
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream) {
     dim3 grid((unsigned)((Q.HW + 63) / 64), (unsigned)Q.n_slots), block(64);
-    hipLaunchKernelGGL(k_policy, grid, block, 0, stream, Q);
+    if (((size_t)Q.HW * Q.K) % 16 == 0 && (64 * Q.K) % 16 == 0 && Q.HW % 4 == 0 && Q.K <= 96)
+        hipLaunchKernelGGL(k_policy_tiled, grid, block, 0, stream, Q);
+    else
+        hipLaunchKernelGGL(k_policy, grid, block, 0, stream, Q);
     return hipGetLastError();
 }
 }  // namespace mrts

@@ -37,12 +37,13 @@ def _compare_step(env, ref, step, dump_every, tag=""):
 
 
 def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, policy="masked", dump_every=10, seed=3,
-             players=None):
+             players=None, partial_obs=False):
     torch = _torch()
     from microrts_amd import DeviceVecEnv, UnitTypeTable
 
-    env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=UnitTypeTable(utt, crs), seed=seed)
-    ref = oracle_py.OracleVecClient(n_sp, n_bot, max_steps, maps, utt_version=utt, crs=crs, seed=seed)
+    env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=UnitTypeTable(utt, crs), seed=seed, partial_obs=partial_obs)
+    ref = oracle_py.OracleVecClient(n_sp, n_bot, max_steps, maps, utt_version=utt, crs=crs, seed=seed,
+                                    partial_obs=partial_obs)
     S = ref.S
     if players is not None:
         env.players.copy_(torch.as_tensor(players, dtype=torch.int32))
@@ -113,6 +114,18 @@ def test_bot_envs_passive():
 
 def test_selfplay_plus_bots():
     _rollout(["maps/8x8/basesWorkers8x8.xml"] * 6, 4, n_bot=2, steps=200, players=[0, 0, 0, 0, 1, 0])
+
+
+@pytest.mark.parametrize("mp,policy", [("maps/BWDistantResources32x32.xml", "masked"), ("maps/8x8/basesWorkers8x8.xml", "uniform"),
+                                       ("maps/16x16/basesWorkers16x16.xml", "uniform")])
+def test_partial_observability(mp, policy):
+    """BASELINE config c5 semantics: PartiallyObservableGameState views (8 planes)."""
+    _rollout([mp] * 16, 16, steps=200, policy=policy, partial_obs=True)
+
+
+def test_partial_observability_bots_and_resets():
+    _rollout(["maps/8x8/basesWorkers8x8.xml"] * 6, 2, n_bot=4, steps=200, max_steps=45, players=[0, 0, 1, 0, 1, 1],
+             partial_obs=True, policy="uniform")
 
 
 def test_host_api_matches_oracle():
