@@ -85,7 +85,7 @@ def main():
     env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, a.map)] * (2 * E), device=local, seed=SEED,
                        slot_id_base=rank * 2 * E)
     S, H, W, C, K = env.dims
-    stream = env.stream
+    stream = torch.cuda.current_stream(env.device)
     gather_buf = None
     if a.gather_obs and world > 1:
         gather_buf = torch.empty((world,) + tuple(env.obs.shape), dtype=torch.int16, device=env.device)
@@ -98,8 +98,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if gather_buf is not None:
-            with torch.cuda.stream(stream):
-                dist.all_gather_into_tensor(gather_buf.view(-1), env.obs.to(torch.int16).view(-1))
+            dist.all_gather_into_tensor(gather_buf.view(-1), env.obs.to(torch.int16).view(-1))
 
     env.reset()
     for k in range(a.burnin + a.warmup):

@@ -76,7 +76,8 @@ int mrts_step(mrts_env* env, const int32_t* actions, const int32_t* players, mrt
 int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out /* [n_slots][H][W][K] */);          /* getMasks :307-316 */
 
 /* Device-pointer API: same semantics, caller-owned HBM buffers, stream-ordered on `stream`
- * (a hipStream_t; NULL = the handle's own stream), no host synchronisation. d_players may be NULL
+ * (a hipStream_t; NULL = HIP's default stream, as everywhere in HIP; mrts_stream() gives the handle's
+ * own stream), no host synchronisation. d_players may be NULL
  * (all zeros).  d_masks may be NULL; when given, the masks getMasks(mask_player) would return after
  * this call are written too (fused, saves a launch). */
 int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,

@@ -304,7 +304,7 @@ int fail(const Fail& f) {
     return f.code;
 }
 
-hipStream_t pickStream(mrts_env* env, void* s) { return s ? (hipStream_t)s : env->stream; }
+hipStream_t pickStream(mrts_env*, void* s) { return (hipStream_t)s; }  // NULL = HIP's default stream, like every HIP API
 
 void checkFlagsAfter(mrts_env* env) {  // Java exceptions → error codes
     std::vector<uint32_t> fl((size_t)env->nSlots);

@@ -1240,16 +1240,10 @@ DEV int pickBit(uint32_t r, uint64_t bitsv, int n) {
     while (k--) bitsv &= bitsv - 1;
     return __builtin_ctzll(bitsv);
 }
-// one cell's action from its mask record (bytes m[0..K)), Philox counter (slot id, step, cell, 0)
-DEV void sampleCell(const PolicyParams& Q, const uint8_t* m, int slot, int c, int32_t a[7]) {
+// one cell's action from its mask bits (lo/hi: mask slots 1..K-1 -> bit i-1), Philox counter
+// (slot id, step, cell, 0)
+DEV void sampleBits(const PolicyParams& Q, uint64_t lo, uint64_t hi, int slot, int c, int32_t a[7]) {
     for (int k = 0; k < 7; k++) a[k] = 0;
-    if (!m[0]) return;
-    uint64_t lo = 0, hi = 0;  // mask slots 1..K-1 -> bit i-1
-    for (int i = 1; i < Q.K; i++) {
-        const uint64_t b = m[i] ? 1ull : 0ull;
-        if (i - 1 < 64) lo |= b << (i - 1);
-        else hi |= b << (i - 1 - 64);
-    }
     uint32_t ctr[4] = {Q.slot_id_base + (uint32_t)slot, Q.step, (uint32_t)c, 0u};
     philox(ctr, (uint32_t)Q.seed, (uint32_t)(Q.seed >> 32));
     auto field = [&](int off, int n) -> uint64_t {  // mask slots [off, off+n) (off >= 1)
@@ -1276,25 +1270,68 @@ DEV void sampleCell(const PolicyParams& Q, const uint8_t* m, int slot, int c, in
         } break;
     }
 }
+DEV void sampleCell(const PolicyParams& Q, const uint8_t* m, int slot, int c, int32_t a[7]) {
+    for (int k = 0; k < 7; k++) a[k] = 0;
+    if (!m[0]) return;
+    uint64_t lo = 0, hi = 0;
+    for (int i = 1; i < Q.K; i++) {
+        const uint64_t b = m[i] ? 1ull : 0ull;
+        if (i - 1 < 64) lo |= b << (i - 1);
+        else hi |= b << (i - 1 - 64);
+    }
+    sampleBits(Q, lo, hi, slot, c, a);
+}
+// 16 mask bytes (0 / non-zero) -> 16 bits, byte k -> bit k
+DEV uint32_t nz4(uint32_t w) {
+    uint32_t t = w | (w >> 4);
+    t |= t >> 2;
+    t |= t >> 1;
+    return ((t & 0x01010101u) * 0x01020408u) >> 24;
+}
+DEV uint32_t pack16(uint4 v) { return nz4(v.x) | (nz4(v.y) << 4) | (nz4(v.z) << 8) | (nz4(v.w) << 12); }
 
 // Tiled form: one wave = 64 cells of one slot.  The 64 mask records (64*K bytes, 16-B aligned when
-// HW*K and 64*K are multiples of 16) stream into LDS with dwordx4 loads, the 64 action rows (1792 B)
-// stream out with dwordx4 stores.
+// HW*K and 64*K are multiples of 16) stream in with dwordx4 loads and are packed to bits in
+// registers on arrival (LDS holds 1 bit per mask byte); the 64 action rows (1792 B) stream out of
+// LDS with dwordx4 stores.
 __global__ __launch_bounds__(64) void k_policy_tiled(PolicyParams Q) {
-    __shared__ __align__(16) uint8_t sm[64 * 96];
+    __shared__ uint16_t tb[64 * 96 / 16 + 8];
     __shared__ __align__(16) int32_t sa[64 * 7];
     const int lane = (int)threadIdx.x, slot = (int)blockIdx.y;
     const int c0 = (int)blockIdx.x * 64;
     const int ncell = min(64, Q.HW - c0);
     const uint8_t* src = Q.masks + ((size_t)slot * Q.HW + c0) * Q.K;
     const int nbytes = ncell * Q.K, n16 = nbytes >> 4;
-    for (int i = lane; i < n16; i += 64) ((uint4*)sm)[i] = ((const uint4*)src)[i];
-    for (int i = 16 * n16 + lane; i < nbytes; i += 64) sm[i] = src[i];
+    for (int i = lane; i < n16; i += 64) tb[i] = (uint16_t)pack16(((const uint4*)src)[i]);
+    if (lane == 0 && (nbytes & 15)) {
+        uint32_t b = 0;
+        for (int i = 16 * n16; i < nbytes; i++) b |= (src[i] ? 1u : 0u) << (i - 16 * n16);
+        tb[n16] = (uint16_t)b;
+    }
     __syncthreads();
-    int32_t a[7];
-    if (lane < ncell) sampleCell(Q, sm + lane * Q.K, slot, c0 + lane, a);
-    else
-        for (int k = 0; k < 7; k++) a[k] = 0;
+    int32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (lane < ncell) {
+        const int b0 = lane * Q.K;
+        if ((tb[b0 >> 4] >> (b0 & 15)) & 1) {
+            // bits b0+1 .. b0+K-1 -> lo/hi
+            const int s = b0 + 1, w0 = s >> 4, sh = s & 15;
+            uint64_t x0 = 0, x1 = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) x0 |= (uint64_t)tb[w0 + j] << (16 * j);
+#pragma unroll
+            for (int j = 0; j < 3; j++) x1 |= (uint64_t)tb[w0 + 4 + j] << (16 * j);
+            uint64_t lo = sh ? ((x0 >> sh) | (x1 << (64 - sh))) : x0;
+            uint64_t hi = x1 >> sh;
+            const int nb = Q.K - 1;  // valid bits
+            if (nb < 64) {
+                lo &= (1ull << nb) - 1;
+                hi = 0;
+            } else if (nb < 128) {
+                hi &= (1ull << (nb - 64)) - 1;
+            }
+            sampleBits(Q, lo, hi, slot, c0 + lane, a);
+        }
+    }
 #pragma unroll
     for (int k = 0; k < 7; k++) sa[lane * 7 + k] = a[k];
     __syncthreads();

@@ -5,7 +5,7 @@
   / ``getMasks`` / ``close``, host numpy arrays that are library-owned views reused by the next
   call (like the Java ``Response`` buffers, GameState.java:923-925).
 * ``DeviceVecEnv`` is the zero-copy rollout form: every buffer is a torch tensor in HBM and all
-  calls are stream-ordered on the handle's HIP stream (no host sync).
+  calls are ordered on torch's current HIP stream (no host sync).
 
 There is no CPU fallback: constructing either class without a GPU or without libmrts.so raises.
 """
@@ -178,7 +178,9 @@ class JNIGridnetVecClient:
 
 
 class DeviceVecEnv:
-    """Zero-copy rollout backend: torch HBM tensors, stream-ordered on the handle's HIP stream."""
+    """Zero-copy rollout backend: torch HBM tensors; every call is ordered on torch's CURRENT HIP
+    stream of the env's device (or an explicit `stream=`), so ordinary torch ops on the tensors need
+    no extra synchronisation."""
 
     def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
                  device=0, seed=0, slot_id_base=0, with_masks=True):
@@ -186,6 +188,7 @@ class DeviceVecEnv:
 
         if not torch.cuda.is_available():
             raise RuntimeError("DeviceVecEnv needs an MI355X (torch.cuda is unavailable); there is no CPU fallback")
+        self.torch = torch
         utt = utt or UnitTypeTable()
         paths = [_resolve("", p) for p in map_paths]
         self._h = _Handle(num_selfplay_slots, num_bot_envs, max_steps, paths, ai2s, utt, partial_obs, device, seed,
@@ -193,7 +196,6 @@ class DeviceVecEnv:
         h = self._h
         dev = torch.device("cuda", device)
         self.device = dev
-        self.stream = torch.cuda.ExternalStream(h.L.mrts_stream(h.h), device=dev)
         S, H, W, C, K = h.S, h.H, h.W, h.C, h.K
         self.obs = torch.zeros((S, C, H, W), dtype=torch.int32, device=dev)
         self.reward = torch.zeros((S,), dtype=torch.float64, device=dev)
@@ -208,37 +210,43 @@ class DeviceVecEnv:
     def _p(t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
-    def reset(self):
+    def _s(self, stream):
+        s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def reset(self, stream=None):
         h = self._h
         _lib.check(h.L.mrts_reset_dev(h.h, self._p(self.players), self._p(self.obs), self._p(self.reward),
-                                      self._p(self.done), self._p(self.masks), self.mask_player, None))
+                                      self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
 
-    def step(self, actions=None):
+    def step(self, actions=None, stream=None):
         h = self._h
         a = self.actions if actions is None else actions
         _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self.reward),
-                                     self._p(self.done), self._p(self.masks), self.mask_player, None))
+                                     self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
 
-    def get_masks(self, out=None):
+    def get_masks(self, out=None, stream=None):
         h = self._h
         out = self.masks if out is None else out
-        _lib.check(h.L.mrts_get_masks_dev(h.h, self.mask_player, self._p(out), None))
+        _lib.check(h.L.mrts_get_masks_dev(h.h, self.mask_player, self._p(out), self._s(stream)))
         return out
 
-    def random_policy(self, seed, step, masks=None, out=None):
+    def random_policy(self, seed, step, masks=None, out=None, stream=None):
         h = self._h
         m = self.masks if masks is None else masks
         out = self.actions if out is None else out
-        _lib.check(h.L.mrts_policy_dev(h.h, self._p(m), seed, step, self._p(out), None))
+        _lib.check(h.L.mrts_policy_dev(h.h, self._p(m), seed, step, self._p(out), self._s(stream)))
         return out
 
     def synchronize(self):
-        self.stream.synchronize()
+        self.torch.cuda.current_stream(self.device).synchronize()
 
     def dump_state(self, slot):
+        self.synchronize()
         return self._h.dump(slot)
 
     def error_flags(self):
+        self.synchronize()
         return self._h.error_flags()
 
     @property
@@ -247,4 +255,5 @@ class DeviceVecEnv:
         return h.S, h.H, h.W, h.C, h.K
 
     def close(self):
+        self.synchronize()
         self._h.close()

@@ -10,7 +10,7 @@ res = []
 for k in range(2100):
     env.random_policy(0x5EEDC0DE, k)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record(env.stream); env.step(); e.record(env.stream)
+    s.record(); env.step(); e.record()
     if k % 100 == 0:
         env.synchronize()
         u = np.mean([env.dump_state(i)[4] for i in range(0, 64, 2)])
