@@ -80,10 +80,12 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from microrts_amd import DeviceVecEnv
+    from microrts_amd import dist as mdist
 
     E = a.envs
-    env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, a.map)] * (2 * E), device=local, seed=SEED,
-                       slot_id_base=rank * 2 * E)
+    sh = mdist.shard(rank, E)
+    env = DeviceVecEnv(sh["n_slots"], 0, 2000, [os.path.join(ROOT, a.map)] * sh["n_slots"], device=local, seed=SEED,
+                       slot_id_base=sh["slot_id_base"])
     S, H, W, C, K = env.dims
     stream = torch.cuda.current_stream(env.device)
     gather_buf = None
@@ -98,7 +100,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if gather_buf is not None:
-            dist.all_gather_into_tensor(gather_buf.view(-1), env.obs.to(torch.int16).view(-1))
+            mdist.gather_observations(env.obs, gather_buf)
 
     env.reset()
     for k in range(a.burnin + a.warmup):
@@ -124,10 +126,7 @@ def main():
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([t], dtype=torch.float64, device=env.device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
+    t = mdist.max_over_ranks(t, env.device)
     step_ms = [s.elapsed_time(e) for s, e in evs]
     kern_ms = float(np.mean(step_ms))
     flags = env.error_flags()

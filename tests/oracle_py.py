@@ -61,13 +61,13 @@ class OracleVecClient:
     """Mirror of tests.JNIGridnetVecClient (src/tests/JNIGridnetVecClient.java) on the CPU oracle."""
 
     def __init__(self, n_selfplay_slots, n_bot_envs, max_steps, map_paths, partial_obs=False, utt_version=1, crs=1,
-                 bot_kinds=None, seed=0):
+                 bot_kinds=None, seed=0, slot_id_base=0):
         L = load()
         self.L = L
         paths = (ctypes.c_char_p * len(map_paths))(*[os.path.join(ROOT, p).encode() for p in map_paths])
         bk = np.asarray(bot_kinds if bot_kinds is not None else [0] * n_bot_envs, dtype=np.int32)
         self.h = L.oref_create(n_selfplay_slots, n_bot_envs, _ptr(bk) if n_bot_envs else None, max_steps, int(partial_obs),
-                               utt_version, crs, ctypes.cast(paths, ctypes.c_void_p), seed)
+                               utt_version, crs, ctypes.cast(paths, ctypes.c_void_p), seed + slot_id_base)
         if not self.h:
             raise RuntimeError(L.oref_last_error().decode())
         d = [ctypes.c_int32() for _ in range(5)]
