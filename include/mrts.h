@@ -52,6 +52,9 @@ typedef struct {
     int32_t utt_version;        /* new UnitTypeTable(version, crs): 1 ORIGINAL, 2 FINETUNED, 3 NON_DETERMINISTIC */
     int32_t conflict_policy;    /* 1 CANCEL_BOTH, 2 CANCEL_RANDOM, 3 CANCEL_ALTERNATING (UnitTypeTable.java:46-57) */
     const int32_t* bot_kinds;   /* a_ai2s (:107): per bot env, MRTS_BOT_* ; NULL = all passive */
+    const int32_t* ai1_kinds;   /* non-NULL selects the bot-only client (:157-177, JNIBotClient): per env the
+                                   MRTS_BOT_* of a_ai1s (bot_kinds = a_ai2s); n_selfplay_slots must be 0;
+                                   observations and masks are not produced (Java returns null) */
     const char* const* map_paths; /* a_mapPaths (:106): one per slot */
     int32_t device;             /* HIP device ordinal */
     uint64_t seed;              /* seeds the per-game java.util.Random streams */

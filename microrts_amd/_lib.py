@@ -29,6 +29,7 @@ class MrtsConfig(ctypes.Structure):
         ("utt_version", ctypes.c_int32),
         ("conflict_policy", ctypes.c_int32),
         ("bot_kinds", ctypes.POINTER(ctypes.c_int32)),
+        ("ai1_kinds", ctypes.POINTER(ctypes.c_int32)),
         ("map_paths", ctypes.POINTER(ctypes.c_char_p)),
         ("device", ctypes.c_int32),
         ("seed", ctypes.c_uint64),

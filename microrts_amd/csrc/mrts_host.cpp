@@ -254,7 +254,8 @@ struct mrts_env {
     int32_t* d_state = nullptr;
     int32_t* d_tmpl = nullptr;
     int32_t* d_tmplOff = nullptr;
-    int32_t* d_botKind = nullptr;
+    int32_t* d_gameKind = nullptr;
+    std::vector<int32_t> gameKindHost;
     // library-owned buffers for the host-pointer API
     int32_t* d_actions = nullptr;
     int32_t* d_players = nullptr;
@@ -284,7 +285,7 @@ struct mrts_env {
         hstatic.state = d_state;
         hstatic.tmpl = d_tmpl;
         hstatic.tmpl_off = d_tmplOff;
-        hstatic.bot_kind = d_botKind;
+        hstatic.game_kind = d_gameKind;
     }
     hipError_t launch(int mode, const KDyn& D, hipStream_t s) const { return launchEnv(mode, hstatic, d_static, D, s); }
     int gameOfSlot(int slot, int* player) const {
@@ -344,9 +345,13 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         env->nSpGames = cfg->n_selfplay_slots / 2;
         env->nGames = env->nSpGames + cfg->n_bot_envs;
         env->slotIdBase = (uint32_t)cfg->slot_id_base;
+        if (cfg->ai1_kinds && cfg->n_selfplay_slots) throw Fail{-EINVAL, "the bot-only client has no self-play slots"};
+        env->gameKindHost.assign((size_t)env->nGames, 0);  // self-play = 0
         for (int j = 0; j < cfg->n_bot_envs; j++) {
-            const int k = cfg->bot_kinds ? cfg->bot_kinds[j] : MRTS_BOT_PASSIVE;
-            if (k != MRTS_BOT_PASSIVE) throw Fail{-ENOTSUP, "only PassiveAI opponents are implemented on the GPU path"};
+            const int k2 = cfg->bot_kinds ? cfg->bot_kinds[j] : MRTS_BOT_PASSIVE;
+            const int k1 = cfg->ai1_kinds ? cfg->ai1_kinds[j] : MRTS_BOT_PASSIVE;
+            if (k1 < 0 || k1 > 1 || k2 < 0 || k2 > 1) throw Fail{-ENOTSUP, "only PassiveAI / RandomBiasedAI are native"};
+            env->gameKindHost[(size_t)(env->nSpGames + j)] = (cfg->ai1_kinds ? 2 : 1) | (k1 << 4) | (k2 << 8);
         }
         // maps: one template per distinct path
         std::map<std::string, int> tmplIndex;
@@ -401,11 +406,10 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         HIPCHK(hipMalloc(&env->d_state, sw * env->nGames * 4));
         HIPCHK(hipMalloc(&env->d_tmpl, blob.size() * 4));
         HIPCHK(hipMalloc(&env->d_tmplOff, (size_t)env->nGames * 4));
-        HIPCHK(hipMalloc(&env->d_botKind, (size_t)env->nGames * 4));
+        HIPCHK(hipMalloc(&env->d_gameKind, (size_t)env->nGames * 4));
         HIPCHK(hipMemcpy(env->d_tmpl, blob.data(), blob.size() * 4, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(env->d_tmplOff, env->tmplOffHost.data(), (size_t)env->nGames * 4, hipMemcpyHostToDevice));
-        std::vector<int32_t> bk((size_t)env->nGames, 0);
-        HIPCHK(hipMemcpy(env->d_botKind, bk.data(), bk.size() * 4, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(env->d_gameKind, env->gameKindHost.data(), (size_t)env->nGames * 4, hipMemcpyHostToDevice));
         // headers: java.util.Random seeds per game (same derivation as the CPU oracle)
         std::vector<int32_t> hdr(sw * env->nGames, 0);
         auto scramble = [](uint64_t s) { return (s ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1); };
@@ -689,7 +693,7 @@ void mrts_destroy(mrts_env* env) {
     (void)hipFree(env->d_state);
     (void)hipFree(env->d_tmpl);
     (void)hipFree(env->d_tmplOff);
-    (void)hipFree(env->d_botKind);
+    (void)hipFree(env->d_gameKind);
     (void)hipFree(env->d_actions);
     (void)hipFree(env->d_players);
     (void)hipFree(env->d_obs);

@@ -65,7 +65,7 @@ struct KStatic {
     int32_t* state;                // [n_games][stateWords(CAP)]
     const int32_t* tmpl;           // template blob
     const int32_t* tmpl_off;       // [n_games] word offset of each game's template
-    const int32_t* bot_kind;       // [n_games]
+    const int32_t* game_kind;      // [n_games]: type | ai1 << 4 | ai2 << 8 (see mrts_kernels.hip)
 };
 // Per-call buffers (kernel arguments by value)
 struct KDyn {

@@ -25,6 +25,8 @@ constexpr uint16_t EMPTY = 0xFFFF, WALL = 0xFFFE;
 constexpr int INF = 0x7FFFFFFF;
 enum { T_NONE = 0, T_MOVE = 1, T_HARVEST = 2, T_RETURN = 3, T_PRODUCE = 4, T_ATTACK = 5 };
 enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2 };
+enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2 };  // game_kind & 15
+enum { GK_PASSIVE = 0, GK_RANDOM_BIASED = 1 };                    // AI kinds (bits 4-7 ai1, 8-11 ai2)
 enum : uint32_t {
     E_CAPACITY = 1u << 0, E_ADDUNIT = 1u << 1, E_PRODUCE_TYPE = 1u << 2, E_OLDER = 1u << 3,
     E_NEG_RES = 1u << 4, E_COLLISION = 1u << 5
@@ -92,6 +94,7 @@ struct JRand {
         } while ((int)((uint32_t)bits - (uint32_t)val + (uint32_t)(bound - 1)) < 0);
         return val;
     }
+    DEV double nextDouble() { return (double)(((int64_t)next(26) << 27) + next(27)) * (1.0 / 9007199254740992.0); }
 };
 DEV uint64_t rng_of(int lo, int hi) { return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32); }
 
@@ -561,30 +564,42 @@ struct Game {
         wsync();
     }
 
-    // GameState.issueSafe(pa) (rts/GameState.java:338-408) for pa = [accepted rows in cell order]
-    // + PlayerAction.fillWithNones(gs, p, fillDur) (rts/PlayerAction.java:328-346) in list order.
-    DEV void issuePlayer(int p, int fillDur) {
-        for (int c0 = 0; c0 < HW; c0 += 64) {
-            const int c = c0 + lane_id();
-            const int s = c < HW ? cell[c] : EMPTY;
-            const bool isPA = s < CAP && uplay(uc[s]) == p && (ua[s] & UA_PA);
-            uint64_t m = ballot(isPA);
-            if (m == 0) continue;
-            int t = 0, prm = 0, tx = 0, ty = 0, ut = 0;
-            if (isPA) {
-                const uint32_t a = ua[s];
-                t = ua_type(a);
-                prm = par[s];
-                tx = ua_tx(a);
-                ty = ua_ty(a);
-                ut = ua_ut(a);
-                legality(s, t, prm, tx, ty, ut);
+    // GameState.issueSafe(pa) (rts/GameState.java:338-408).  Agent pa = [accepted rows in cell order]
+    // + PlayerAction.fillWithNones(gs, p, fillDur) (rts/PlayerAction.java:328-346) in list order;
+    // AI pa (RandomBiasedAI / PassiveAI) = its units in list order (listOrder).
+    DEV void issuePA(int s, bool isPA, uint64_t m) {
+        int t = 0, prm = 0, tx = 0, ty = 0, ut = 0;
+        if (isPA) {
+            const uint32_t a = ua[s];
+            t = ua_type(a);
+            prm = par[s];
+            tx = ua_tx(a);
+            ty = ua_ty(a);
+            ut = ua_ut(a);
+            legality(s, t, prm, tx, ty, ut);
+        }
+        wsync();
+        while (m) {
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            issueOne(rl(s, k), rl(t, k), rl(prm, k), rl(tx, k), rl(ty, k), rl(ut, k));
+        }
+    }
+    DEV void issuePlayer(int p, int fillDur, bool listOrder) {
+        if (!listOrder) {
+            for (int c0 = 0; c0 < HW; c0 += 64) {
+                const int c = c0 + lane_id();
+                const int s = c < HW ? cell[c] : EMPTY;
+                const bool isPA = s < CAP && uplay(uc[s]) == p && (ua[s] & UA_PA);
+                const uint64_t m = ballot(isPA);
+                if (m) issuePA(s, isPA, m);
             }
-            wsync();
-            while (m) {
-                const int k = __builtin_ctzll(m);
-                m &= m - 1;
-                issueOne(rl(s, k), rl(t, k), rl(prm, k), rl(tx, k), rl(ty, k), rl(ut, k));
+        } else {
+            for (int o0 = 0; o0 < nu; o0 += 64) {
+                const int o = o0 + lane_id();
+                const bool isPA = o < nu && !(uc[o] & UC_DEAD) && uplay(uc[o]) == p && (ua[o] & UA_PA);
+                const uint64_t m = ballot(isPA);
+                if (m) issuePA(o, isPA, m);
             }
         }
         for (int o0 = 0; o0 < nu; o0 += 64) {
@@ -601,6 +616,188 @@ struct Game {
                 issueOne(o0 + k, T_NONE, fillDur, 0, 0, 0);
             }
         }
+    }
+
+    // ------------------------------------------------------------------ RandomBiasedAI
+    // RandomBiasedAI.getAction (ai/RandomBiasedAI.java:51-107): for every idle unit of b in list
+    // order, getUnitActions(gs) (rts/units/Unit.java:382-522) weighted 5 (attack/harvest/return) or 1,
+    // Sampler.weighted (util/Sampler.java:116-135) with the game's java.util.Random, then accepted iff
+    // consistent with the running reservations, else that list's NONE(10).  The chosen actions are
+    // parked with UA_PA and issued later in list order.  getUnitActions of an owned unit is the same
+    // in every view (neighbours and range-3 targets are always inside its own sight radius), the
+    // base reservations are the view's (PO: b's snapshot).
+    DEV void randomBiased(int b) {
+        bool anyIdle = false;
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            anyIdle |= ballot(o < nu && !(uc[o] & UC_DEAD) && uplay(uc[o]) == b && !(ua[o] & UA_PRESENT)) != 0;
+        }
+        if (!anyIdle) return;  // canExecuteAnyAction (rts/GameState.java:416-423): empty pa, no draws
+        int run0, run1;
+        baseReservations(b, run0, run1);
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            uint64_t m = ballot(o < nu && !(uc[o] & UC_DEAD) && uplay(uc[o]) == b && !(ua[o] & UA_PRESENT));
+            while (m) {
+                const int k = __builtin_ctzll(m);
+                m &= m - 1;
+                pickRandomBiased(o0 + k, b, run0, run1);
+            }
+        }
+    }
+    DEV void pickRandomBiased(int s, int b, int& run0, int& run1) {
+        const uint32_t cu = uniu(uc[s]);
+        const int x = ux(cu), y = uy(cu), typ = utyp(cu);
+        const uint32_t fl = U.flags[typ];
+        const int carried = uni(res[s]);
+        int nb[4];
+        uint32_t atkDirs = 0, harvDirs = 0, retDirs = 0, freeDirs = 0;
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int nx = x + dxo(d), ny = y + dyo(d);
+            nb[d] = inb(nx, ny) ? uni(cell[ny * W + nx]) : WALL;
+            if (nb[d] < CAP) {
+                const uint32_t oc = uniu(uc[nb[d]]);
+                const int op = uplay(oc);
+                const uint32_t ofl = U.flags[utyp(oc)];
+                if (op >= 0 && op != b) atkDirs |= 1u << d;
+                if (ofl & F_RESOURCE) harvDirs |= 1u << d;
+                if ((ofl & F_STOCKPILE) && op == b) retDirs |= 1u << d;
+            } else if (nb[d] == EMPTY) {
+                freeDirs |= 1u << d;
+            }
+        }
+        const int r = U.range[typ];
+        int nAtk = 0;
+        if (fl & F_ATTACK) {
+            if (r == 1) {
+                nAtk = __popc(atkDirs);
+            } else {
+                for (int q0 = 0; q0 < nu; q0 += 64) {
+                    const int q = q0 + lane_id();
+                    bool in = false;
+                    if (q < nu) {
+                        const uint32_t qc = uc[q];
+                        const int op = uplay(qc), dx = ux(qc) - x, dy = uy(qc) - y;
+                        in = !(qc & UC_DEAD) && op >= 0 && op != b && dx * dx + dy * dy <= r * r;
+                    }
+                    nAtk += __popcll(ballot(in));
+                }
+            }
+        }
+        const int nHarv = (fl & F_HARVEST) && carried == 0 ? __popc(harvDirs) : 0;
+        const int nRet = (fl & F_HARVEST) && carried > 0 ? __popc(retDirs) : 0;
+        int nProd = 0;
+        for (int i = 0; i < U.nprod[typ]; i++)
+            if (pres(b) >= U.cost[U.prod[typ][i]]) nProd += __popc(freeDirs);
+        const int nMove = (fl & F_MOVE) ? __popc(freeDirs) : 0;
+        const int n5 = nAtk + nHarv + nRet, n1 = nProd + nMove + 1;
+        double total = 0.0;
+        for (int i = 0; i < n5; i++) total += 5.0;
+        for (int i = 0; i < n1; i++) total += 1.0;
+        const double tmp = rngSampler.nextDouble() * total;
+        int idx = -1;
+        double accum = 0.0;
+        for (int i = 0; i < n5 + n1; i++) {
+            accum += i < n5 ? 5.0 : 1.0;
+            if (accum >= tmp) {
+                idx = i;
+                break;
+            }
+        }
+        auto nth = [](uint32_t m, int n) {  // n-th set bit (0-based)
+            for (int i = 0; i < n; i++) m &= m - 1;
+            return __builtin_ctz(m);
+        };
+        int t = T_NONE, prm = 10, ut = 0, tx = 0, ty = 0;
+        if (idx < nAtk) {
+            t = T_ATTACK;
+            prm = -1;
+            if (r == 1) {
+                const int d = nth(atkDirs, idx);
+                tx = x + dxo(d);
+                ty = y + dyo(d);
+            } else {  // idx-th enemy in list order inside the disk
+                int seen = 0;
+                for (int q0 = 0; q0 < nu; q0 += 64) {
+                    const int q = q0 + lane_id();
+                    uint32_t qc = 0;
+                    bool in = false;
+                    if (q < nu) {
+                        qc = uc[q];
+                        const int op = uplay(qc), dx = ux(qc) - x, dy = uy(qc) - y;
+                        in = !(qc & UC_DEAD) && op >= 0 && op != b && dx * dx + dy * dy <= r * r;
+                    }
+                    const uint64_t mm = ballot(in);
+                    const int cnt = __popcll(mm);
+                    if (idx - seen < cnt) {
+                        uint64_t z = mm;
+                        for (int i = 0; i < idx - seen; i++) z &= z - 1;
+                        const uint32_t tc = (uint32_t)rl((int)qc, __builtin_ctzll(z));
+                        tx = ux(tc);
+                        ty = uy(tc);
+                        break;
+                    }
+                    seen += cnt;
+                }
+            }
+        } else if (idx < nAtk + nHarv) {
+            t = T_HARVEST;
+            prm = nth(harvDirs, idx - nAtk);
+        } else if (idx < n5) {
+            t = T_RETURN;
+            prm = nth(retDirs, idx - nAtk - nHarv);
+        } else {
+            int j = idx - n5;
+            if (j < nProd) {
+                for (int i = 0; i < U.nprod[typ]; i++) {
+                    const int u2 = U.prod[typ][i];
+                    if (pres(b) < U.cost[u2]) continue;
+                    const int n = __popc(freeDirs);
+                    if (j < n) {
+                        t = T_PRODUCE;
+                        ut = u2;
+                        prm = nth(freeDirs, j);
+                        break;
+                    }
+                    j -= n;
+                }
+            } else if (j < nProd + nMove) {
+                t = T_MOVE;
+                prm = nth(freeDirs, j - nProd);
+            }
+        }
+        // ua.resourceUsage(u, pgs).consistentWith(pa.r, gs) (RandomBiasedAI.java:91)
+        bool ok = true;
+        int bi = 0, cst = 0;
+        const bool up = (t == T_MOVE || t == T_PRODUCE);
+        if (up) {
+            bi = (y + dyo(prm)) * W + x + dxo(prm) + W;
+            ok = !((uniu(bits[bi >> 5]) >> (bi & 31)) & 1u);
+        }
+        if (t == T_PRODUCE) cst = U.cost[ut];
+        if (run0 != 0) {
+            const int sum = (b == 0 ? cst : 0) + run0;
+            if (sum > 0 && sum > pres0) ok = false;
+        }
+        if (run1 != 0) {
+            const int sum = (b == 1 ? cst : 0) + run1;
+            if (sum > 0 && sum > pres1) ok = false;
+        }
+        if (ok) {
+            if (up && lane_id() == 0) bits[bi >> 5] |= 1u << (bi & 31);
+            if (b == 0) run0 += cst;
+            else run1 += cst;
+        } else {
+            t = T_NONE;
+            prm = 10;
+            ut = tx = ty = 0;
+        }
+        if (lane_id() == 0) {
+            ua[s] = pack_ua(t, ut, tx, ty) | UA_PA;
+            par[s] = (int16_t)prm;
+        }
+        wsync();
     }
 
     // ------------------------------------------------------------------ PO snapshot
@@ -1122,15 +1319,24 @@ struct Game {
     }
 };
 
+// PassiveAI.getAction = fillWithNones(gs, p, 10) (ai/PassiveAI.java:41-45): nothing to park, the
+// list-order fill in issuePlayer does it; RandomBiasedAI parks its actions.
+DEV void aiGetAction(Game& G, int kind, int p) {
+    if (kind == GK_RANDOM_BIASED) G.randomBiased(p);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
     Game G(P, D, smem);
-    const bool selfplay = G.g < P.n_sp_games;
+    const int kind = P.game_kind[G.g];
+    const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
+    const bool selfplay = gtype == GT_SELFPLAY;
     const int slot0 = selfplay ? 2 * G.g : 2 * P.n_sp_games + (G.g - P.n_sp_games);
     const int nslots = selfplay ? 2 : 1;
-    const int agent = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
+    // agent-vs-bot: the agent's side; bot-vs-bot: the side ai1 plays (JNIBotClient.gameStep(player))
+    const int side = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
     bool freshObs = true;  // observation comes from the current (post-step or fresh) state
 
     if (MODE == MODE_RESET) {
@@ -1149,38 +1355,45 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
-        if (selfplay) {
+        if (gtype == GT_SELFPLAY) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
             G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1);
             for (int p = 0; p < 2; p++) {
                 if (G.po) G.snapshot(p);
                 G.decode(p);
-                G.issuePlayer(p, 1);
+                G.issuePlayer(p, 1, false);
             }
-        } else {
-            // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203), PassiveAI opponent:
-            // both views are taken and both actions computed before either issueSafe
+        } else if (gtype == GT_AGENT_VS_BOT) {
+            // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203): both views are taken and
+            // both actions computed before either issueSafe
             const int32_t* rows = D.actions + (size_t)slot0 * rowStride;
-            G.predecode(rows, rows, agent);
+            G.predecode(rows, rows, side);
             if (G.po) {
-                G.snapshot(agent);
-                G.snapshot(1 - agent);
+                G.snapshot(side);
+                G.snapshot(1 - side);
             }
-            G.decode(agent);
-            G.issuePlayer(agent, 1);
-            G.issuePlayer(1 - agent, 10);  // PassiveAI.getAction = fillWithNones(gs, p, 10)
+            G.decode(side);
+            aiGetAction(G, ai2, 1 - side);
+            G.issuePlayer(side, 1, false);
+            G.issuePlayer(1 - side, 10, true);
+        } else {
+            // JNIBotClient.gameStep (tests/JNIBotClient.java:108-135): both AIs on the full state
+            aiGetAction(G, ai1, side);
+            aiGetAction(G, ai2, 1 - side);
+            G.issuePlayer(side, 10, true);
+            G.issuePlayer(1 - side, 10, true);
         }
         G.cycle();
         bool gameover;
         int winner;
         G.outcome(gameover, winner);
         // WinLossRewardFunction (ai/reward/WinLossRewardFunction.java:16-24) + VecClient auto-reset
-        // keeping the terminal reward/done (tests/JNIGridnetVecClient.java:241-287)
+        // keeping the terminal reward/done (tests/JNIGridnetVecClient.java:214-287)
         G.steps++;
         const bool reset = gameover || G.steps >= P.max_steps;
         if (lane_id() < nslots) {
             const int slot = slot0 + lane_id();
-            const int maxp = selfplay ? lane_id() : agent;
+            const int maxp = selfplay ? lane_id() : side;
             if (D.reward) D.reward[slot] = gameover ? (winner == maxp ? 1.0 : -1.0) : 0.0;
             if (D.done) D.done[slot] = (gameover || reset) ? 1 : 0;
         }
@@ -1192,19 +1405,20 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         }
     }
 
-    if (MODE != MODE_MASKS && D.obs) {
+    const bool external = gtype != GT_BOT_VS_BOT;  // bot-only clients return no observation / masks
+    if (MODE != MODE_MASKS && D.obs && external) {
         if (G.po) {
             for (int i = 0; i < nslots; i++) {
-                const int p = selfplay ? i : agent;
+                const int p = selfplay ? i : side;
                 if (freshObs) G.snapshot(p);  // PO view of the reset state
                 G.writeObsPO(slot0 + i, p);
             }
         } else {
-            G.writeObsFull(slot0, nslots, selfplay ? 0 : agent);
+            G.writeObsFull(slot0, nslots, side);
         }
     }
     if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
-    if (D.masks) {
+    if (D.masks && external) {
         wsync();
         for (int i = 0; i < nslots; i++) G.stashMasks(selfplay ? i : D.mask_player);
         wsync();

@@ -62,16 +62,24 @@ def _check_rfs(rfs):
         raise NotImplementedError("only [WinLossRewardFunction] is implemented on the GPU path")
 
 
+def _kinds(ais, n):
+    kinds = [_bot_kind(a) for a in (ais or [])][:n]
+    kinds += [_lib.MRTS_BOT_PASSIVE] * (n - len(kinds))
+    return (ctypes.c_int32 * max(1, n))(*(kinds or [0]))
+
+
 class _Handle:
-    def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base):
+    def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base,
+                 ai1s=None):
         L = _lib.load()
         self.L = L
         self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
-        kinds = [_bot_kind(a) for a in (ai2s or [])][:n_bot]
-        kinds += [_lib.MRTS_BOT_PASSIVE] * (n_bot - len(kinds))
-        self._kinds = (ctypes.c_int32 * max(1, n_bot))(*(kinds or [0]))
+        self._kinds = _kinds(ai2s, n_bot)
+        self._ai1 = _kinds(ai1s, n_bot) if ai1s is not None else None
+        P32 = ctypes.POINTER(ctypes.c_int32)
         cfg = _lib.MrtsConfig(n_selfplay, n_bot, max_steps, int(bool(partial_obs)), utt.version, utt.crs,
-                              ctypes.cast(self._kinds, ctypes.POINTER(ctypes.c_int32)),
+                              ctypes.cast(self._kinds, P32),
+                              ctypes.cast(self._ai1, P32) if self._ai1 is not None else None,
                               ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base)
         h = ctypes.c_void_p()
         _lib.check(L.mrts_create(ctypes.byref(cfg), ctypes.byref(h)))
@@ -113,12 +121,13 @@ class JNIGridnetVecClient:
     """tests.JNIGridnetVecClient (src/tests/JNIGridnetVecClient.java:106-142) on MI355X."""
 
     def __init__(self, a_num_selfplayenvs, a_num_envs, a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai2s=None,
-                 a_utt=None, partial_obs=False, device=0, seed=0, slot_id_base=0):
+                 a_utt=None, partial_obs=False, device=0, seed=0, slot_id_base=0, _ai1s=None):
         _check_rfs(a_rfs)
         utt = a_utt or UnitTypeTable()
         paths = [_resolve(a_micrortsPath, p) for p in a_mapPaths]
         self._h = _Handle(a_num_selfplayenvs, a_num_envs, a_max_steps, paths, a_ai2s, utt, partial_obs, device, seed,
-                          slot_id_base)
+                          slot_id_base, ai1s=_ai1s)
+        self.botOnly = _ai1s is not None
         self.maxSteps = a_max_steps
         self.utt = utt
         self.partialObs = partial_obs
@@ -127,9 +136,17 @@ class JNIGridnetVecClient:
         self.num_slots, self.height, self.width, self.num_planes, self.mask_slots = h.S, h.H, h.W, h.C, h.K
         self._resp = _lib.MrtsResponses()
 
+    @classmethod
+    def bots(cls, a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai1s, a_ai2s, a_utt=None, partial_obs=False, device=0,
+             seed=0, slot_id_base=0):
+        """The bot-only constructor JNIGridnetVecClient(maxSteps, rfs, path, mapPaths, ai1s, ai2s, utt, po)
+        (src/tests/JNIGridnetVecClient.java:157-177): JNIBotClients, reward/done only."""
+        return cls(0, len(a_ai2s), a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai2s, a_utt, partial_obs, device, seed,
+                   slot_id_base, _ai1s=list(a_ai1s))
+
     def _responses(self):
         h, r = self._h, self._resp
-        obs = np.ctypeslib.as_array(r.obs, shape=(h.S, h.C, h.H, h.W))
+        obs = None if getattr(self, "botOnly", False) else np.ctypeslib.as_array(r.obs, shape=(h.S, h.C, h.H, h.W))
         rew = np.ctypeslib.as_array(r.reward, shape=(h.S, 1))
         done = np.ctypeslib.as_array(r.done, shape=(h.S, 1)).view(np.bool_)
         return Responses(obs, rew, done)
@@ -143,6 +160,8 @@ class JNIGridnetVecClient:
 
     def gameStep(self, action, players=None):
         """gameStep(int[][][] action, int[] players) (:213-297); action = [slots][H*W][7]."""
+        if action is None:  # bot-only clients take no actions (JNIGridnetVecClient.java:214-216)
+            action = np.zeros((self._h.S, self._h.H * self._h.W, 7), np.int32)
         a = np.ascontiguousarray(action, np.int32).reshape(self._h.S, self._h.H * self._h.W, 7)
         p = None if players is None else np.ascontiguousarray(players, np.int32)
         _lib.check(self._h.L.mrts_step(self._h.h, a.ctypes.data_as(ctypes.c_void_p),
@@ -183,7 +202,7 @@ class DeviceVecEnv:
     no extra synchronisation."""
 
     def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
-                 device=0, seed=0, slot_id_base=0, with_masks=True):
+                 device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None):
         import torch
 
         if not torch.cuda.is_available():
@@ -192,7 +211,7 @@ class DeviceVecEnv:
         utt = utt or UnitTypeTable()
         paths = [_resolve("", p) for p in map_paths]
         self._h = _Handle(num_selfplay_slots, num_bot_envs, max_steps, paths, ai2s, utt, partial_obs, device, seed,
-                          slot_id_base)
+                          slot_id_base, ai1s=ai1s)
         h = self._h
         dev = torch.device("cuda", device)
         self.device = dev

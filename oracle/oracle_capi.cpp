@@ -400,6 +400,12 @@ struct BotVec {
     MapTemplate map;
     GSP gs;
     JavaRandom gen;  // util/Sampler.java:17 — one JVM-global generator shared by both AIs
+    JavaRandom cancelGen, damageGen;
+    void newGame() {
+        gs = std::make_shared<GameState>(instantiate(map, world->utt), &world->utt);
+        gs->cancelRandom = &cancelGen;
+        gs->damageRandom = &damageGen;
+    }
     std::unique_ptr<AI> ai1, ai2;
     int envSteps = 0, maxSteps = 2000;
 };
@@ -412,11 +418,13 @@ void* oref_botclient_create(const char* map_path, int ai1, int ai2, int max_step
         b->world->H = b->map.height;
         b->world->W = b->map.width;
         b->gen.setSeed(seed);
+        b->cancelGen.setSeed((int64_t)((uint64_t)seed ^ 0x9E3779B97F4A7C15ULL));
+        b->damageGen.setSeed((int64_t)((uint64_t)seed ^ 0xC2B2AE3D27D4EB4FULL));
         b->maxSteps = max_steps;
         auto mk = [&](int k) -> AI* { return k == BOT_PASSIVE ? (AI*)new PassiveAI() : (AI*)new RandomBiasedAI(&b->gen); };
         b->ai1.reset(mk(ai1));
         b->ai2.reset(mk(ai2));
-        b->gs = std::make_shared<GameState>(instantiate(b->map, b->world->utt), &b->world->utt);
+        b->newGame();
         return b;
     } catch (std::exception& e) {
         g_err = e.what();
@@ -436,7 +444,7 @@ int oref_botclient_step(void* h, int player, double* reward, uint8_t* done) {
         winLoss(*b->gs, player, *reward, *done);
         b->envSteps++;
         if (*done || b->envSteps >= b->maxSteps) {
-            b->gs = std::make_shared<GameState>(instantiate(b->map, b->world->utt), &b->world->utt);
+            b->newGame();
             *done = 1;
             b->envSteps = 0;
         }

@@ -123,3 +123,31 @@ def policy(mask, seed, env_id, step, player, n_types=7):
     out = np.zeros((H * W, 7), np.int32)
     L.oref_policy(_ptr(m), H * W, K, n_types, seed, env_id, step, player, _ptr(out))
     return out
+
+
+class OracleBotClient:
+    """tests.JNIBotClient (src/tests/JNIBotClient.java) + the bot-only VecClient auto-reset, one game."""
+
+    def __init__(self, map_path, ai1, ai2, max_steps=2000, utt_version=1, crs=1, seed=0):
+        L = load()
+        self.L = L
+        self.h = L.oref_botclient_create(os.path.join(ROOT, map_path).encode(), ai1, ai2, max_steps, utt_version, crs, seed)
+        if not self.h:
+            raise RuntimeError(L.oref_last_error().decode())
+
+    def step(self, player=0):
+        r = ctypes.c_double()
+        d = ctypes.c_uint8()
+        if self.L.oref_botclient_step(self.h, player, ctypes.byref(r), ctypes.byref(d)) != 0:
+            raise RuntimeError(self.L.oref_last_error().decode())
+        return r.value, d.value
+
+    def dump(self):
+        buf = np.zeros(1 << 16, np.int32)
+        n = self.L.oref_botclient_dump(self.h, _ptr(buf), buf.size)
+        return buf[:n].copy()
+
+    def close(self):
+        if self.h:
+            self.L.oref_botclient_destroy(self.h)
+            self.h = None

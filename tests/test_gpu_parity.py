@@ -37,13 +37,15 @@ def _compare_step(env, ref, step, dump_every, tag=""):
 
 
 def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, policy="masked", dump_every=10, seed=3,
-             players=None, partial_obs=False):
+             players=None, partial_obs=False, bots=None):
     torch = _torch()
     from microrts_amd import DeviceVecEnv, UnitTypeTable
 
-    env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=UnitTypeTable(utt, crs), seed=seed, partial_obs=partial_obs)
+    env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=UnitTypeTable(utt, crs), seed=seed, partial_obs=partial_obs,
+                       ai2s=bots)
+    kinds = [1 if b == "RandomBiasedAI" else 0 for b in bots] if bots else None
     ref = oracle_py.OracleVecClient(n_sp, n_bot, max_steps, maps, utt_version=utt, crs=crs, seed=seed,
-                                    partial_obs=partial_obs)
+                                    partial_obs=partial_obs, bot_kinds=kinds)
     S = ref.S
     if players is not None:
         env.players.copy_(torch.as_tensor(players, dtype=torch.int32))
@@ -126,6 +128,41 @@ def test_partial_observability(mp, policy):
 def test_partial_observability_bots_and_resets():
     _rollout(["maps/8x8/basesWorkers8x8.xml"] * 6, 2, n_bot=4, steps=200, max_steps=45, players=[0, 0, 1, 0, 1, 1],
              partial_obs=True, policy="uniform")
+
+
+@pytest.mark.parametrize("po", [False, True])
+def test_agent_vs_random_biased(po):
+    """JNIGridnetClient with a RandomBiasedAI opponent (a2 + a17): java.util.Random sampling on the GPU."""
+    players = [0, 1, 0, 1, 0, 1, 1, 0]
+    _rollout(["maps/8x8/basesWorkers8x8.xml"] * 8, 0, n_bot=8, steps=300, players=players, partial_obs=po,
+             bots=["RandomBiasedAI"] * 8, policy="masked")
+
+
+@pytest.mark.parametrize("mp", ["maps/4x4/base4x4.xml", "maps/16x16/basesWorkers16x16.xml"])
+def test_bot_only_client(mp):
+    """Config c1 (JNIBotClient: RandomBiasedAI vs RandomBiasedAI / PassiveAI) on the GPU vs the oracle."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n = 8
+    ai1 = ["RandomBiasedAI"] * 6 + ["PassiveAI", "RandomBiasedAI"]
+    ai2 = ["RandomBiasedAI"] * 6 + ["RandomBiasedAI", "PassiveAI"]
+    players = [0, 1] * 4
+    env = DeviceVecEnv(0, n, 300, [mp] * n, ai1s=ai1, ai2s=ai2, seed=9)
+    env.players.copy_(torch.as_tensor(players, dtype=torch.int32))
+    kind = {"PassiveAI": 0, "RandomBiasedAI": 1}
+    refs = [oracle_py.OracleBotClient(mp, kind[a], kind[b], max_steps=300, seed=9 + j) for j, (a, b) in enumerate(zip(ai1, ai2))]
+    env.reset()
+    for step in range(700):
+        env.step()
+        env.synchronize()
+        rw, dn = env.reward.cpu().numpy(), env.done.cpu().numpy()
+        for j, r in enumerate(refs):
+            er, ed = r.step(players[j])
+            assert rw[j] == er and dn[j] == ed, f"env {j} step {step}"
+            if step % 25 == 0:
+                assert np.array_equal(env.dump_state(j), r.dump()), f"state env {j} step {step}"
+    env.close()
 
 
 def test_host_api_matches_oracle():
