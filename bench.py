@@ -39,6 +39,9 @@ def parse():
                     help="untimed steps from reset before warmup: the timed window sees mid-episode unit counts")
     ap.add_argument("--envs", type=int, default=4096, help="self-play games per GPU")
     ap.add_argument("--map", default=MAP)
+    ap.add_argument("--mask-mode", choices=["delta", "full"], default="delta",
+                    help="delta: the persistent mask tensor is updated in place (only changed rows written); "
+                         "full: every mask byte is rewritten each step")
     ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of observations each step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -85,7 +88,8 @@ def main():
     E = a.envs
     sh = mdist.shard(rank, E)
     env = DeviceVecEnv(sh["n_slots"], 0, 2000, [os.path.join(ROOT, a.map)] * sh["n_slots"], device=local, seed=SEED,
-                       slot_id_base=sh["slot_id_base"])
+                       slot_id_base=sh["slot_id_base"], mask_delta=a.mask_mode == "delta",
+                       source_bits=a.mask_mode == "delta")
     S, H, W, C, K = env.dims
     stream = torch.cuda.current_stream(env.device)
     gather_buf = None
@@ -159,6 +163,7 @@ def main():
             "utt": "VERSION_ORIGINAL, CANCEL_BOTH",
             "max_steps": 2000,
             "burnin_steps": a.burnin,
+            "mask_mode": a.mask_mode,
             "parallelism": f"dp{world} (independent env shards)" + (", RCCL int16 obs all-gather" if gather_buf is not None else ""),
         },
         "step_kernel_ms": kern_ms,

@@ -59,6 +59,10 @@ typedef struct {
     int32_t device;             /* HIP device ordinal */
     uint64_t seed;              /* seeds the per-game java.util.Random streams */
     int32_t slot_id_base;       /* global id of this handle's slot 0 (multi-GPU: disjoint RNG streams) */
+    int32_t mask_delta;         /* 1: when a *_dev call gets the same mask buffer (and mask_player) as this
+                                   handle's previous mask write, only rows that changed are rewritten; the
+                                   buffer must not be modified by the caller in between (the Java client
+                                   owns and reuses its mask array the same way, JNIGridnetClient.java:211) */
 } mrts_config;
 
 typedef struct {               /* ai/jni/Responses.java:12-30 (one reward function: WinLoss) */
@@ -92,8 +96,13 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
 /* Synthetic masked-uniform random policy (bench / rollouts): per own idle cell a uniform action
  * type among the mask's set type bits, then a uniform parameter among that type's set bits
  * (Philox4x32-10, key = seed, counter = (slot_id_base + slot, step, cell, 0)).  d_masks as written
- * by the calls above; d_actions = [n_slots][H*W][7]. */
-int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, uint64_t seed, uint32_t step, int32_t* d_actions, void* stream);
+ * by the calls above (d_source: their source bits, or NULL); d_actions = [n_slots][H*W][7]. */
+int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_source, uint64_t seed, uint32_t step,
+                    int32_t* d_actions, void* stream);
+/* Optional compact output of every mask write: mask slot 0 ("own unit without an action here") as
+ * bits, uint32 [n_slots][ceil(H*W/32)] (sticky; NULL disables).  mrts_policy_dev uses it, when
+ * given, to read only the candidate cells' mask rows. */
+int mrts_set_source_output(mrts_env* env, uint32_t* d_source);
 
 /* Canonical state dump of the game behind `slot` (same format as the CPU oracle's dumpState):
  * [time, 2, res0, res1, n_units, (type, player, x, y, hp, resources)*, n_assignments,

@@ -15,7 +15,7 @@ ERR_BITS = {
 # every symbol include/mrts.h declares
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_reset_dev", "mrts_step_dev",
-    "mrts_get_masks_dev", "mrts_policy_dev", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_get_masks_dev", "mrts_policy_dev", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
 ]
 
@@ -34,6 +34,7 @@ class MrtsConfig(ctypes.Structure):
         ("device", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("slot_id_base", ctypes.c_int32),
+        ("mask_delta", ctypes.c_int32),
     ]
 
 
@@ -74,7 +75,8 @@ def load(path=LIB_PATH):
     L.mrts_reset_dev.argtypes = [P, P, P, P, P, P, I32, P]
     L.mrts_step_dev.argtypes = [P, P, P, P, P, P, P, I32, P]
     L.mrts_get_masks_dev.argtypes = [P, I32, P, P]
-    L.mrts_policy_dev.argtypes = [P, P, U64, U32, P, P]
+    L.mrts_policy_dev.argtypes = [P, P, P, U64, U32, P, P]
+    L.mrts_set_source_output.argtypes = [P, P]
     L.mrts_get_state.argtypes = [P, I32, P, I32]
     L.mrts_error_flags.argtypes = [P, P]
     L.mrts_env_steps.argtypes = [P, P]

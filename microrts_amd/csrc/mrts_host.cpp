@@ -21,6 +21,9 @@ using namespace mrts;
 namespace mrts {
 size_t ldsBytes(int HW, int W, int CAP, int po);
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream);
+#ifdef MRTS_PHASE_TIMING
+hipError_t phaseTimes(unsigned long long* out, int reset);
+#endif
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream);
 hipError_t prepareLds(size_t bytes);
 }  // namespace mrts
@@ -270,6 +273,19 @@ struct mrts_env {
 
     KStatic hstatic;
     KStatic* d_static = nullptr;
+    // delta mask writes: which buffer / player the last mask write went to
+    int maskDelta = 0;
+    const uint8_t* lastMaskPtr = nullptr;
+    int lastMaskPlayer = -1;
+    uint32_t* d_source = nullptr;
+    void prepMasks(KDyn& D) {
+        D.source = D.masks ? d_source : nullptr;
+        D.mask_delta = (maskDelta && D.masks && D.masks == lastMaskPtr && D.mask_player == lastMaskPlayer) ? 1 : 0;
+        if (D.masks) {
+            lastMaskPtr = D.masks;
+            lastMaskPlayer = D.mask_player;
+        }
+    }
     void buildStatic() {
         std::memset(&hstatic, 0, sizeof(hstatic));
         hstatic.utt = utt;
@@ -345,6 +361,7 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         env->nSpGames = cfg->n_selfplay_slots / 2;
         env->nGames = env->nSpGames + cfg->n_bot_envs;
         env->slotIdBase = (uint32_t)cfg->slot_id_base;
+        env->maskDelta = cfg->mask_delta;
         if (cfg->ai1_kinds && cfg->n_selfplay_slots) throw Fail{-EINVAL, "the bot-only client has no self-play slots"};
         env->gameKindHost.assign((size_t)env->nGames, 0);  // self-play = 0
         for (int j = 0; j < cfg->n_bot_envs; j++) {
@@ -392,17 +409,17 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
             blob.push_back(m.res[0]);
             blob.push_back(m.res[1]);
             blob.push_back(nu);
+            std::vector<int32_t> terr((size_t)(env->HW + 3) / 4, 0);
+            std::memcpy(terr.data(), m.terrain.data(), (size_t)env->HW);
+            blob.insert(blob.end(), terr.begin(), terr.end());
             for (auto& u : m.units)
                 blob.push_back((int32_t)((uint32_t)u.x | ((uint32_t)u.y << 8) | ((uint32_t)u.type << 16) | ((uint32_t)(u.player + 1) << 20)));
             for (auto& u : m.units) blob.push_back(u.hp);
             for (auto& u : m.units) blob.push_back(u.res);
-            std::vector<int32_t> terr((size_t)(env->HW + 3) / 4, 0);
-            std::memcpy(terr.data(), m.terrain.data(), (size_t)env->HW);
-            blob.insert(blob.end(), terr.begin(), terr.end());
         }
         env->tmplOffHost.resize((size_t)env->nGames);
         for (int g = 0; g < env->nGames; g++) env->tmplOffHost[(size_t)g] = off[(size_t)gameTmpl[(size_t)g]];
-        const size_t sw = (size_t)stateWords(env->CAP);
+        const size_t sw = (size_t)stateWords(env->CAP, env->HW);
         HIPCHK(hipMalloc(&env->d_state, sw * env->nGames * 4));
         HIPCHK(hipMalloc(&env->d_tmpl, blob.size() * 4));
         HIPCHK(hipMalloc(&env->d_tmplOff, (size_t)env->nGames * 4));
@@ -483,6 +500,7 @@ int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, doub
         D.done = d_done;
         D.masks = d_masks;
         D.mask_player = mask_player;
+        env->prepMasks(D);
         HIPCHK(env->launch(1, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
@@ -504,6 +522,7 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
         D.done = d_done;
         D.masks = d_masks;
         D.mask_player = mask_player;
+        env->prepMasks(D);
         HIPCHK(env->launch(0, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
@@ -520,6 +539,7 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
         D.masks = d_out;
         D.mask_player = player;
         D.players = env->d_players;
+        env->prepMasks(D);
         HIPCHK(env->launch(2, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
@@ -527,7 +547,14 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
     }
 }
 
-int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, uint64_t seed, uint32_t step, int32_t* d_actions, void* stream) {
+int mrts_set_source_output(mrts_env* env, uint32_t* d_source) {
+    if (!env) return -EINVAL;
+    env->d_source = d_source;
+    return 0;
+}
+
+int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_source, uint64_t seed, uint32_t step,
+                    int32_t* d_actions, void* stream) {
     try {
         HIPCHK(hipSetDevice(env->device));
         PolicyParams Q;
@@ -539,6 +566,7 @@ int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, uint64_t seed, uint32
         Q.step = step;
         Q.seed = seed;
         Q.masks = d_masks;
+        Q.source = d_source;
         Q.actions = d_actions;
         HIPCHK(launchPolicy(Q, pickStream(env, stream)));
         return 0;
@@ -611,7 +639,7 @@ int mrts_get_state(mrts_env* env, int32_t slot, int32_t* buf, int32_t cap) {
         if (slot < 0 || slot >= env->nSlots) throw Fail{-EINVAL, "slot out of range"};
         int pl;
         const int g = env->gameOfSlot(slot, &pl);
-        const size_t sw = (size_t)stateWords(env->CAP);
+        const size_t sw = (size_t)stateWords(env->CAP, env->HW);
         std::vector<int32_t> s(sw);
         HIPCHK(hipStreamSynchronize(env->stream));
         HIPCHK(hipMemcpy(s.data(), env->d_state + (size_t)g * sw, sw * 4, hipMemcpyDeviceToHost));
@@ -658,7 +686,7 @@ int mrts_get_state(mrts_env* env, int32_t slot, int32_t* buf, int32_t cap) {
 }
 
 static int readHeaderWord(mrts_env* env, int word, int32_t* out_per_slot) {
-    const size_t sw = (size_t)stateWords(env->CAP);
+    const size_t sw = (size_t)stateWords(env->CAP, env->HW);
     HIPCHK(hipStreamSynchronize(env->stream));
     std::vector<int32_t> w((size_t)env->nGames);
     HIPCHK(hipMemcpy2D(w.data(), 4, env->d_state + word, sw * 4, 4, (size_t)env->nGames, hipMemcpyDeviceToHost));
@@ -707,4 +735,8 @@ void mrts_destroy(mrts_env* env) {
     delete env;
 }
 
+#ifdef MRTS_PHASE_TIMING
+// diagnostic build only: per-phase cycle sums of k_env (tools/phase_timing.py)
+int mrts_phase_times(unsigned long long* out, int reset) { return mrts::phaseTimes(out, reset) == hipSuccess ? 0 : -EIO; }
+#endif
 }  // extern "C"

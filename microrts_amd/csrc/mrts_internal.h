@@ -41,7 +41,10 @@ enum {
 };
 // followed by 7 SoA arrays of CAP int32: UC, HP, RES, UA, PAR, AT, AS (see mrts_kernels.hip)
 enum { A_UC = 0, A_HP = 1, A_RES = 2, A_UA = 3, A_PAR = 4, A_AT = 5, A_AS = 6, N_ARRAYS = 7 };
-constexpr int stateWords(int cap) { return H_WORDS + N_ARRAYS * cap; }  // constexpr: host + device
+// followed by 2 x maskWords(HW): per player, the cells whose mask rows were non-zero in the mask buffer
+// written last (delta mask writes, mrts_config.mask_delta)
+constexpr int maskWords(int hw) { return (hw + 31) / 32; }
+constexpr int stateWords(int cap, int hw) { return H_WORDS + N_ARRAYS * cap + 2 * maskWords(hw); }  // host + device
 
 // unit core word
 constexpr uint32_t UC_DEAD = 1u << 31;
@@ -51,7 +54,9 @@ constexpr int ACT_INVALID = 7;  // action type / direction outside the Java rang
 
 // ---- map templates (one per distinct map), int32 words --------------------------------------------
 // [0] H [1] W [2] res0 [3] res1 [4] nu [5..5+nu) uc [..+nu) hp [..+nu) res [..+ceil(HW/4)) terrain (u8 x4)
-enum { T_H = 0, T_W = 1, T_RES0 = 2, T_RES1 = 3, T_NU = 4, T_UNITS = 5 };
+// map template: header, terrain bytes ((HW+3)/4 words, fixed offset so it loads with the state), units
+enum { T_H = 0, T_W = 1, T_RES0 = 2, T_RES1 = 3, T_NU = 4, T_TERR = 5 };
+constexpr int tmplUnits(int hw) { return T_TERR + (hw + 3) / 4; }  // host + device
 
 // Static per-handle parameters live in a device buffer (uploaded once at mrts_create): the kernels
 // read them through a pointer, so the unit-type tables can be indexed per lane without the
@@ -62,7 +67,7 @@ struct KStatic {
     int32_t n_games, n_sp_games;   // games [0, n_sp_games) are self-play, the rest agent-vs-bot
     int32_t max_steps, C;
     int32_t partial_obs;           // PartiallyObservableGameState views (8 planes)
-    int32_t* state;                // [n_games][stateWords(CAP)]
+    int32_t* state;                // [n_games][stateWords(CAP, HW)]
     const int32_t* tmpl;           // template blob
     const int32_t* tmpl_off;       // [n_games] word offset of each game's template
     const int32_t* game_kind;      // [n_games]: type | ai1 << 4 | ai2 << 8 (see mrts_kernels.hip)
@@ -75,7 +80,9 @@ struct KDyn {
     double* reward;                // [n_slots] or null
     uint8_t* done;                 // [n_slots] or null
     uint8_t* masks;                // [n_slots][HW][K] or null
+    uint32_t* source;              // [n_slots][maskWords(HW)] mask slot 0 as bits, or null
     int32_t mask_player;           // player whose masks bot-env slots receive
+    int32_t mask_delta;            // 1: `masks` holds the previous masks of this handle -> rewrite changed rows only
 };
 
 struct PolicyParams {
@@ -83,6 +90,7 @@ struct PolicyParams {
     uint32_t slot_id_base, step;
     uint64_t seed;
     const uint8_t* masks;
+    const uint32_t* source;        // optional [n_slots][maskWords(HW)]
     int32_t* actions;
 };
 

@@ -13,6 +13,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "mrts_internal.h"
 
 using namespace mrts;
@@ -25,6 +28,23 @@ constexpr uint16_t EMPTY = 0xFFFF, WALL = 0xFFFE;
 constexpr int INF = 0x7FFFFFFF;
 enum { T_NONE = 0, T_MOVE = 1, T_HARVEST = 2, T_RETURN = 3, T_PRODUCE = 4, T_ATTACK = 5 };
 enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2 };
+
+// Diagnostic build only (-DMRTS_PHASE_TIMING, tools/phase_timing.py): per-phase shader-clock cycles
+// summed over games; not compiled into libmrts.so.
+#ifdef MRTS_PHASE_TIMING
+constexpr int PH_GAMES = 1 << 16;
+__device__ unsigned long long g_phase[16 * PH_GAMES];  // [phase][game], no contention
+#define PHASE(i)                                                                          \
+    do {                                                                                  \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                 \
+        if (lane_id() == 0 && G.g < PH_GAMES) g_phase[(i) * PH_GAMES + G.g] += t_ - tph_; \
+        tph_ = t_;                                                                        \
+    } while (0)
+#else
+#define PHASE(i) \
+    do {         \
+    } while (0)
+#endif
 enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2 };  // game_kind & 15
 enum { GK_PASSIVE = 0, GK_RANDOM_BIASED = 1 };                    // AI kinds (bits 4-7 ai1, 8-11 ai2)
 enum : uint32_t {
@@ -116,6 +136,7 @@ struct Game {
     uint32_t* bits;  // running ResourceUsage positions, indices [-W, HW+W)
     uint32_t* scell; // PO: last snapshot unit per cell (slot+1, 0 = none)
     int32_t* rseq;   // ready-list scratch (64)
+    uint32_t* mprev; // previous mask row sets, [2][maskWords(HW)] (delta mask writes)
     int16_t* hp;
     int16_t* res;
     int16_t* par;    // UnitAction.parameter (direction / NONE duration)
@@ -137,6 +158,7 @@ struct Game {
         as = (int32_t*)q; q += 4 * CAP;
         bits = (uint32_t*)q; q += 4 * ((HW + 2 * W + 31) / 32);
         rseq = (int32_t*)q; q += 4 * 64;
+        mprev = (uint32_t*)q; q += 8 * maskWords(HW);
         scell = (uint32_t*)q; q += po ? 4 * HW : 0;
         hp = (int16_t*)q; q += 2 * CAP;
         res = (int16_t*)q; q += 2 * CAP;
@@ -153,7 +175,7 @@ struct Game {
     }
     DEV bool inb(int x, int y) const { return x >= 0 && x < W && y >= 0 && y < H; }
     DEV const int32_t* tmpl() const { return P.tmpl + P.tmpl_off[g]; }
-    DEV int32_t* st() const { return P.state + (size_t)g * stateWords(CAP); }
+    DEV int32_t* st() const { return P.state + (size_t)g * stateWords(CAP, HW); }
 
     // UnitAction.ETA (rts/UnitAction.java:307-329)
     DEV int eta(int t, int prm, int ut, int unitType) const {
@@ -173,11 +195,20 @@ struct Game {
     }
 
     // ------------------------------------------------------------------ state load / store
+    DEV void setTerrainWord(int w, uint32_t v) {  // 4 terrain bytes -> cells 4w..4w+3
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (4 * w + b < HW) cell[4 * w + b] = ((v >> (8 * b)) & 0xFFu) ? WALL : EMPTY;
+    }
     DEV void initCells() {  // terrain walls from the map template
-        const int32_t* t = tmpl();
-        const int nu_t = t[T_NU];
-        const uint8_t* terr = (const uint8_t*)(t + T_UNITS + 3 * nu_t);
-        for (int c = lane_id(); c < HW; c += 64) cell[c] = terr[c] ? WALL : EMPTY;
+        const int32_t* t = tmpl() + T_TERR;
+        for (int w = lane_id(); w < (HW + 3) / 4; w += 64) setTerrainWord(w, (uint32_t)t[w]);
+        wsync();
+    }
+    DEV uint32_t* prevG() const { return (uint32_t*)(st() + H_WORDS + N_ARRAYS * CAP); }
+    DEV void loadPrev() {  // previous mask row sets (delta mask writes), when not fetched by load()
+        const uint32_t* pg = prevG();
+        for (int i = lane_id(); i < 2 * maskWords(HW); i += 64) mprev[i] = pg[i];
         wsync();
     }
     DEV void placeUnits() {
@@ -187,8 +218,8 @@ struct Game {
         }
         wsync();
     }
-    DEV void loadHeader(const int32_t* s) {
-        const int hv = lane_id() < H_WORDS ? s[lane_id()] : 0;
+    DEV void loadHeader(const int32_t* s) { loadHeader(lane_id() < H_WORDS ? s[lane_id()] : 0); }
+    DEV void loadHeader(int hv) {  // hv = header word lane_id() (lanes < H_WORDS)
         time = rl(hv, H_TIME);
         nu = rl(hv, H_NU);
         pres0 = rl(hv, H_RES0);
@@ -202,11 +233,31 @@ struct Game {
         rngSampler.s = rng_of(rl(hv, H_RNG_SAMPLER), rl(hv, H_RNG_SAMPLER + 1));
         deaths = 0;
     }
-    DEV void load() {
+    // One global round trip: header, unit rows 0..63 (speculative — CAP >= 64), the terrain and the
+    // previous mask row sets are all in flight before the first wait.
+    DEV void load(bool wantPrev) {
         const int32_t* s = st();
-        loadHeader(s);
         const int32_t* arr = s + H_WORDS;
-        for (int i = lane_id(); i < nu; i += 64) {
+        const int32_t* terr = tmpl() + T_TERR;
+        const int l = lane_id();
+        const int TW = (HW + 3) / 4, PW = 2 * maskWords(HW);
+        const int hv = l < H_WORDS ? s[l] : 0;
+        int32_t r[N_ARRAYS];
+#pragma unroll
+        for (int a = 0; a < N_ARRAYS; a++) r[a] = arr[a * CAP + l];
+        const uint32_t tw = l < TW ? (uint32_t)terr[l] : 0u;
+        const uint32_t pv = (wantPrev && l < PW) ? (uint32_t)arr[N_ARRAYS * CAP + l] : 0u;
+        loadHeader(hv);
+        if (l < nu) {
+            uc[l] = (uint32_t)r[A_UC];
+            hp[l] = (int16_t)r[A_HP];
+            res[l] = (int16_t)r[A_RES];
+            ua[l] = (uint32_t)r[A_UA];
+            par[l] = (int16_t)r[A_PAR];
+            at[l] = r[A_AT];
+            as[l] = r[A_AS];
+        }
+        for (int i = l + 64; i < nu; i += 64) {
             uc[i] = (uint32_t)arr[A_UC * CAP + i];
             hp[i] = (int16_t)arr[A_HP * CAP + i];
             res[i] = (int16_t)arr[A_RES * CAP + i];
@@ -215,7 +266,13 @@ struct Game {
             at[i] = arr[A_AT * CAP + i];
             as[i] = arr[A_AS * CAP + i];
         }
-        initCells();
+        if (l < TW) setTerrainWord(l, tw);
+        for (int w = l + 64; w < TW; w += 64) setTerrainWord(w, (uint32_t)terr[w]);
+        if (wantPrev) {
+            if (l < PW) mprev[l] = pv;
+            for (int i = l + 64; i < PW; i += 64) mprev[i] = prevG()[i];
+        }
+        wsync();
         placeUnits();
     }
     DEV void store() {
@@ -261,10 +318,11 @@ struct Game {
         pres0 = t[T_RES0];
         pres1 = t[T_RES1];
         nu = nu_t;
+        const int32_t* tu = t + tmplUnits(HW);
         for (int i = lane_id(); i < nu_t; i += 64) {
-            uc[i] = (uint32_t)t[T_UNITS + i];
-            hp[i] = (int16_t)t[T_UNITS + nu_t + i];
-            res[i] = (int16_t)t[T_UNITS + 2 * nu_t + i];
+            uc[i] = (uint32_t)tu[i];
+            hp[i] = (int16_t)tu[nu_t + i];
+            res[i] = (int16_t)tu[2 * nu_t + i];
             ua[i] = 0;
             par[i] = -1;
             at[i] = 0;
@@ -1253,10 +1311,12 @@ struct Game {
         w2 = hi;
     }
     // Park each idle unit's 79-bit mask in its unused assignment words (at/as/ua low bits).
-    DEV void stashMasks(int p) {
+    // pset: bit p = park the masks of player p's idle units (both players in one pass for self-play)
+    DEV void stashMasks(int pset) {
         for (int o = lane_id(); o < nu; o += 64) {
             const uint32_t c = uc[o];
-            if ((c & UC_DEAD) || uplay(c) != p || (ua[o] & UA_PRESENT)) continue;
+            const int op = uplay(c);
+            if ((c & UC_DEAD) || op < 0 || !((pset >> op) & 1) || (ua[o] & UA_PRESENT)) continue;
             uint32_t w0, w1, w2;
             unitMask(o, w0, w1, w2);
             at[o] = (int32_t)w0;
@@ -1282,40 +1342,108 @@ struct Game {
         return (uint32_t)v & 0xFFFFu;
     }
     static DEV uint32_t expand4(uint32_t b) { return ((b & 0xFu) * 0x00204081u) & 0x01010101u; }
-    DEV void writeMasks(int slot, int p) {
+    // one 16-byte chunk j of the [HW][K] byte mask of player p, from the parked per-unit bits
+    DEV uint4 maskChunk(int j, int p) const {
         const int K = U.K;
-        uint8_t* out = D.masks + (size_t)slot * HW * K;
+        const int o0 = 16 * j;
+        const int cA = o0 / K, kA = o0 - cA * K;
+        uint64_t lo;
+        uint32_t hi;
+        cellMaskBits(cA, p, lo, hi);
+        uint32_t b = bits16(lo, hi, kA);
+        const int nA = K - kA;
+        if (nA < 16) {
+            b &= (1u << nA) - 1u;
+            cellMaskBits(cA + 1, p, lo, hi);
+            b |= (bits16(lo, hi, 0) << nA) & 0xFFFFu;
+        }
+        uint4 v;
+        v.x = expand4(b);
+        v.y = expand4(b >> 4);
+        v.z = expand4(b >> 8);
+        v.w = expand4(b >> 12);
+        return v;
+    }
+    DEV bool ownIdleAt(int c, int p) const {
+        const int s = c < HW ? cell[c] : EMPTY;
+        return s < CAP && uplay(uc[s]) == p && !(ua[s] & UA_PRESENT);
+    }
+    // The mask rows of the game's external slots (slot0 + i is player pl[i]'s view).  Full mode writes
+    // all H*W*K bytes per slot; delta mode (the buffer holds this handle's previous masks) rewrites
+    // only the 16-byte chunks overlapping a cell that has, or had at the previous write, an own idle
+    // unit — the buffer ends up identical.  The dirty cells of both slots are gathered into one list
+    // and their chunks are spread over the lanes, so a typical step is a single parallel pass.
+    DEV void writeMasks(int slot0, int nslots, int pl0, int pl1) {
+        const int K = U.K;
         const int total = HW * K;
-        if ((total & 15) == 0) {
-            for (int j = lane_id(); j < total / 16; j += 64) {
-                const int o0 = 16 * j;
-                const int cA = o0 / K, kA = o0 - cA * K;
-                uint64_t lo;
-                uint32_t hi;
-                cellMaskBits(cA, p, lo, hi);
-                uint32_t b = bits16(lo, hi, kA);
-                const int nA = K - kA;
-                if (nA < 16) {
-                    b &= (1u << nA) - 1u;
-                    cellMaskBits(cA + 1, p, lo, hi);
-                    b |= (bits16(lo, hi, 0) << nA) & 0xFFFFu;
+        const int MW = maskWords(HW);
+        const bool delta = D.mask_delta && (total & 15) == 0;
+        uint32_t* pg = prevG();
+        const int l = lane_id();
+        int nlist = 0;
+        for (int i = 0; i < nslots; i++) {
+            const int p = i ? pl1 : pl0;
+            const int slot = slot0 + i;
+            for (int c0 = 0; c0 < HW; c0 += 64) {
+                const uint64_t m = ballot(ownIdleAt(c0 + l, p));
+                const int w = c0 >> 5;
+                const uint32_t mine = l == 0 ? (uint32_t)m : (uint32_t)(m >> 32);
+                if (l < 2 && w + l < MW) {
+                    if (D.source) D.source[(size_t)slot * MW + w + l] = mine;
+                    pg[p * MW + w + l] = mine;
                 }
-                uint4 v;
-                v.x = expand4(b);
-                v.y = expand4(b >> 4);
-                v.z = expand4(b >> 8);
-                v.w = expand4(b >> 12);
-                *(uint4*)(out + o0) = v;
-            }
-        } else {
-            for (int o = lane_id(); o < total; o += 64) {
-                const int c = o / K, k = o - c * K;
-                uint64_t lo;
-                uint32_t hi;
-                cellMaskBits(c, p, lo, hi);
-                out[o] = (uint8_t)(k < 64 ? ((lo >> k) & 1u) : ((hi >> (k - 64)) & 1u));
+                if (delta) {
+                    const uint64_t old = (uint64_t)mprev[p * MW + w] | (w + 1 < MW ? (uint64_t)mprev[p * MW + w + 1] << 32 : 0ull);
+                    const uint64_t dirty = old | m;
+                    const int n = __popcll(dirty);
+                    if (n) {
+                        if (nlist + n > 64) {
+                            flushDirty(nlist, slot0, pl0, pl1);
+                            nlist = 0;
+                        }
+                        if ((dirty >> l) & 1ull) rslot[nlist + lanes_below(dirty)] = (uint16_t)((i << 15) | (c0 + l));
+                        nlist += n;
+                    }
+                }
             }
         }
+        if (delta) {
+            if (nlist) flushDirty(nlist, slot0, pl0, pl1);
+            return;
+        }
+        for (int i = 0; i < nslots; i++) {
+            const int p = i ? pl1 : pl0;
+            uint8_t* out = D.masks + (size_t)(slot0 + i) * total;
+            if ((total & 15) == 0) {
+                for (int j = l; j < total / 16; j += 64) *(uint4*)(out + 16 * j) = maskChunk(j, p);
+            } else {
+                for (int o = l; o < total; o += 64) {
+                    const int c = o / K, k = o - c * K;
+                    uint64_t lo;
+                    uint32_t hi;
+                    cellMaskBits(c, p, lo, hi);
+                    out[o] = (uint8_t)(k < 64 ? ((lo >> k) & 1u) : ((hi >> (k - 64)) & 1u));
+                }
+            }
+        }
+    }
+    // rewrite the chunks of the listed dirty cells (rslot[0..n): slot index << 15 | cell)
+    DEV void flushDirty(int n, int slot0, int pl0, int pl1) {
+        wsync();
+        const int K = U.K, total = HW * K;
+        const int NCH = (K + 14) / 16 + 1;  // chunks a K-byte record can touch
+        for (int base = 0; base < NCH * n; base += 64) {
+            const int item = base + lane_id();
+            if (item < NCH * n) {
+                const int k = item / NCH, t = item - k * NCH;
+                const uint32_t e = rslot[k];
+                const int i = (int)(e >> 15), c = (int)(e & 0x7FFFu);
+                const int j = ((c * K) >> 4) + t;
+                if (j <= ((c * K + K - 1) >> 4))
+                    *(uint4*)(D.masks + (size_t)(slot0 + i) * total + 16 * j) = maskChunk(j, i ? pl1 : pl0);
+            }
+        }
+        wsync();
     }
 };
 
@@ -1338,30 +1466,38 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     // agent-vs-bot: the agent's side; bot-vs-bot: the side ai1 plays (JNIBotClient.gameStep(player))
     const int side = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
     bool freshObs = true;  // observation comes from the current (post-step or fresh) state
+#ifdef MRTS_PHASE_TIMING
+    uint64_t tph_ = __builtin_amdgcn_s_memtime();
+#endif
 
     if (MODE == MODE_RESET) {
         G.loadHeader(G.st());
         G.err = 0;
         G.initCells();
         G.resetFromTemplate();
+        if (D.mask_delta && D.masks) G.loadPrev();
         if (lane_id() < nslots) {
             if (D.reward) D.reward[slot0 + lane_id()] = 0.0;
             if (D.done) D.done[slot0 + lane_id()] = 0;
         }
     } else {
-        G.load();
+        G.load(D.mask_delta && D.masks);
     }
     if (G.po) G.clearSnap();
+    PHASE(0);
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
         if (gtype == GT_SELFPLAY) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
             G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1);
+            PHASE(1);
             for (int p = 0; p < 2; p++) {
                 if (G.po) G.snapshot(p);
                 G.decode(p);
+                PHASE(2);
                 G.issuePlayer(p, 1, false);
+                PHASE(3);
             }
         } else if (gtype == GT_AGENT_VS_BOT) {
             // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203): both views are taken and
@@ -1384,6 +1520,7 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
             G.issuePlayer(1 - side, 10, true);
         }
         G.cycle();
+        PHASE(4);
         bool gameover;
         int winner;
         G.outcome(gameover, winner);
@@ -1403,6 +1540,7 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         } else {
             freshObs = false;
         }
+        PHASE(5);
     }
 
     const bool external = gtype != GT_BOT_VS_BOT;  // bot-only clients return no observation / masks
@@ -1417,17 +1555,23 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
             G.writeObsFull(slot0, nslots, side);
         }
     }
+    PHASE(6);
     if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
+    PHASE(7);
     if (D.masks && external) {
         wsync();
-        for (int i = 0; i < nslots; i++) G.stashMasks(selfplay ? i : D.mask_player);
+        G.stashMasks(selfplay ? 3 : (1 << D.mask_player));
         wsync();
-        for (int i = 0; i < nslots; i++) G.writeMasks(slot0 + i, selfplay ? i : D.mask_player);
+        PHASE(8);
+        if (selfplay) G.writeMasks(slot0, 2, 0, 1);
+        else G.writeMasks(slot0, 1, D.mask_player, D.mask_player);
+        PHASE(9);
     }
     if (MODE != MODE_MASKS) {
         wsync();
         G.store();
     }
+    PHASE(10);
 }
 
 // ---------------------------------------------------------------- random policy (bench / rollouts)
@@ -1555,6 +1699,63 @@ __global__ __launch_bounds__(64) void k_policy_tiled(PolicyParams Q) {
     for (int i = 4 * nw4 + lane; i < nw; i += 64) dst[i] = sa[i];
 }
 
+// Source-bit form: one wave = one slot.  Candidate cells come from the env's source bits; only their
+// mask records are read (the <= 6 aligned 16-B chunks covering each).  Rows are composed in LDS,
+// 256 cells (7 KB) at a time, and leave with coalesced dwordx4 stores.
+__global__ __launch_bounds__(64) void k_policy_src(PolicyParams Q) {
+    __shared__ __align__(16) int32_t sa[256 * 7];
+    const int lane = (int)threadIdx.x, slot = (int)blockIdx.x;
+    const int MW = (Q.HW + 31) / 32;
+    const uint32_t* src = Q.source + (size_t)slot * MW;
+    const uint8_t* mrec = Q.masks + (size_t)slot * Q.HW * Q.K;
+    int32_t* dst = Q.actions + (size_t)slot * Q.HW * 7;
+    for (int c0 = 0; c0 < Q.HW; c0 += 256) {
+        const int ncell = min(256, Q.HW - c0);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int c = c0 + 64 * j + lane;
+            int32_t row[7] = {0, 0, 0, 0, 0, 0, 0};
+            if (c < Q.HW && ((src[c >> 5] >> (c & 31)) & 1u)) {
+                // record bytes [b0, b0+K) -> record bits 0..K-1 in (r0, r1), from the covering
+                // aligned 16-B chunks; chunk q's byte 0 sits at record bit pos = 16q - b0
+                const int b0 = c * Q.K, j0 = b0 >> 4, j1 = (b0 + Q.K - 1) >> 4;
+                uint64_t r0 = 0, r1 = 0;
+                for (int q = j0; q <= j1; q++) {
+                    const uint64_t b16 = pack16(((const uint4*)mrec)[q]);
+                    const int pos = 16 * q - b0;
+                    if (pos < 0) {
+                        r0 |= b16 >> (-pos);
+                    } else if (pos < 64) {
+                        r0 |= b16 << pos;
+                        if (pos > 48) r1 |= b16 >> (64 - pos);
+                    } else {
+                        r1 |= b16 << (pos - 64);
+                    }
+                }
+                // record bits 1..K-1 -> lo/hi (bit i -> bit i-1)
+                uint64_t lo = (r0 >> 1) | (r1 << 63), hi = r1 >> 1;
+                const int nb = Q.K - 1;
+                if (nb < 64) {
+                    lo &= (1ull << nb) - 1;
+                    hi = 0;
+                } else {
+                    hi &= (1ull << (nb - 64)) - 1;
+                }
+                sampleBits(Q, lo, hi, slot, c, row);
+            }
+            const int r = 64 * j + lane;  // stride-7 words: conflict-free LDS writes
+#pragma unroll
+            for (int k = 0; k < 7; k++) sa[r * 7 + k] = row[k];
+        }
+        __syncthreads();
+        int32_t* d = dst + (size_t)c0 * 7;
+        const int nw = ncell * 7, nw4 = nw >> 2;
+        for (int i = lane; i < nw4; i += 64) ((int4*)d)[i] = ((const int4*)sa)[i];
+        for (int i = 4 * nw4 + lane; i < nw; i += 64) d[i] = sa[i];
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(64) void k_policy(PolicyParams Q) {
     const int c = (int)(blockIdx.x * 64 + threadIdx.x);
     const int slot = (int)blockIdx.y;
@@ -1569,8 +1770,31 @@ __global__ __launch_bounds__(64) void k_policy(PolicyParams Q) {
 }  // namespace
 
 namespace mrts {
+#ifdef MRTS_PHASE_TIMING
+// out[16]: per-phase sums over games (and the max over games in out[16..31] when given 32 slots)
+hipError_t phaseTimes(unsigned long long* out, int reset) {
+    std::vector<unsigned long long> h((size_t)16 * PH_GAMES);
+    hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_phase), h.size() * sizeof(h[0]));
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < 16; i++) {
+        unsigned long long sum = 0, mx = 0;
+        for (int g = 0; g < PH_GAMES; g++) {
+            sum += h[(size_t)i * PH_GAMES + g];
+            mx = h[(size_t)i * PH_GAMES + g] > mx ? h[(size_t)i * PH_GAMES + g] : mx;
+        }
+        out[i] = sum;
+        out[16 + i] = mx;
+    }
+    if (reset) {
+        std::fill(h.begin(), h.end(), 0ull);
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), h.data(), h.size() * sizeof(h[0]));
+    }
+    return e;
+}
+#endif
 size_t ldsBytes(int HW, int W, int CAP, int po) {
-    return (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + (po ? 4 * (size_t)HW : 0) +
+    return (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) +
+           (po ? 4 * (size_t)HW : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
 }
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
@@ -1591,7 +1815,9 @@ hipError_t prepareLds(size_t bytes) {
 }
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream) {
     dim3 grid((unsigned)((Q.HW + 63) / 64), (unsigned)Q.n_slots), block(64);
-    if (((size_t)Q.HW * Q.K) % 16 == 0 && (64 * Q.K) % 16 == 0 && Q.HW % 4 == 0 && Q.K <= 96)
+    if (Q.source && ((size_t)Q.HW * Q.K) % 16 == 0 && Q.HW % 4 == 0 && Q.K <= 96 && Q.K >= 65)
+        hipLaunchKernelGGL(k_policy_src, dim3((unsigned)Q.n_slots), block, 0, stream, Q);
+    else if (((size_t)Q.HW * Q.K) % 16 == 0 && (64 * Q.K) % 16 == 0 && Q.HW % 4 == 0 && Q.K <= 96)
         hipLaunchKernelGGL(k_policy_tiled, grid, block, 0, stream, Q);
     else
         hipLaunchKernelGGL(k_policy, grid, block, 0, stream, Q);

@@ -70,7 +70,7 @@ def _kinds(ais, n):
 
 class _Handle:
     def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base,
-                 ai1s=None):
+                 ai1s=None, mask_delta=False):
         L = _lib.load()
         self.L = L
         self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
@@ -80,7 +80,8 @@ class _Handle:
         cfg = _lib.MrtsConfig(n_selfplay, n_bot, max_steps, int(bool(partial_obs)), utt.version, utt.crs,
                               ctypes.cast(self._kinds, P32),
                               ctypes.cast(self._ai1, P32) if self._ai1 is not None else None,
-                              ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base)
+                              ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base,
+                              int(bool(mask_delta)))
         h = ctypes.c_void_p()
         _lib.check(L.mrts_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -202,7 +203,10 @@ class DeviceVecEnv:
     no extra synchronisation."""
 
     def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
-                 device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None):
+                 device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None, mask_delta=True, source_bits=True):
+        """mask_delta: `masks` is owned by this object and reused every call, so only changed rows are
+        rewritten (the tensor must not be written by the caller).  source_bits: also keep mask slot 0
+        as bits in `source` ([slots][ceil(H*W/32)] int32), which random_policy uses."""
         import torch
 
         if not torch.cuda.is_available():
@@ -211,7 +215,7 @@ class DeviceVecEnv:
         utt = utt or UnitTypeTable()
         paths = [_resolve("", p) for p in map_paths]
         self._h = _Handle(num_selfplay_slots, num_bot_envs, max_steps, paths, ai2s, utt, partial_obs, device, seed,
-                          slot_id_base, ai1s=ai1s)
+                          slot_id_base, ai1s=ai1s, mask_delta=mask_delta and with_masks)
         h = self._h
         dev = torch.device("cuda", device)
         self.device = dev
@@ -222,6 +226,9 @@ class DeviceVecEnv:
         self.masks = torch.zeros((S, H, W, K), dtype=torch.uint8, device=dev) if with_masks else None
         self.actions = torch.zeros((S, H * W, 7), dtype=torch.int32, device=dev)
         self.players = torch.zeros((S,), dtype=torch.int32, device=dev)
+        self.source = torch.zeros((S, (H * W + 31) // 32), dtype=torch.int32, device=dev) if (with_masks and source_bits) else None
+        if self.source is not None:
+            _lib.check(h.L.mrts_set_source_output(h.h, self._p(self.source)))
         self.mask_player = 0
         torch.cuda.synchronize(dev)
 
@@ -254,7 +261,8 @@ class DeviceVecEnv:
         h = self._h
         m = self.masks if masks is None else masks
         out = self.actions if out is None else out
-        _lib.check(h.L.mrts_policy_dev(h.h, self._p(m), seed, step, self._p(out), self._s(stream)))
+        src = self.source if masks is None else None
+        _lib.check(h.L.mrts_policy_dev(h.h, self._p(m), self._p(src), seed, step, self._p(out), self._s(stream)))
         return out
 
     def synchronize(self):

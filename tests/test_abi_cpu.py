@@ -33,6 +33,7 @@ def test_config_struct_layout():
     # mrts_config: 6 int32, pointer, pointer, int32, uint64, int32 (natural alignment)
     assert ctypes.sizeof(_lib.MrtsConfig) == 6 * 4 + 8 + 8 + 8 + 4 + 4 + 8 + 8
     assert _lib.MrtsConfig.seed.offset == 56
+    assert _lib.MrtsConfig.mask_delta.offset == 68
 
 
 def test_argument_validation():

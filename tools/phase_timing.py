@@ -1,0 +1,56 @@
+"""Diagnostic: where a k_env<MODE_STEP> game step spends its time (16x16, 4096 games).
+
+Loads the timing build (make -C microrts_amd/csrc timing -> libmrts_timing.so) whose k_env adds
+s_memtime stamps between phases; prints mean shader-clock cycles per game step per phase."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402,F401
+
+from microrts_amd import _lib  # noqa: E402
+
+L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_timing.so"))
+L.mrts_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_int]
+from microrts_amd import DeviceVecEnv  # noqa: E402
+
+NAMES = ["load", "predecode", "decode", "issue", "cycle", "outcome+reset", "obs", "compact", "stashMasks",
+         "writeMasks", "store"]
+E = int(os.environ.get("E", 4096))
+MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
+SEED = 0x5EEDC0DE
+
+
+def read(reset):
+    buf = (ctypes.c_ulonglong * 32)()
+    _lib.check(L.mrts_phase_times(buf, reset))
+    return list(buf)
+
+
+for delta in (True, False):
+    env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=1, mask_delta=delta, source_bits=delta)
+    env.reset()
+    for k in range(int(os.environ.get("BURNIN", 1000))):
+        env.random_policy(SEED, k)
+        env.step()
+    env.synchronize()
+    read(1)
+    n = 100
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ms = 0.0
+    for k in range(n):
+        env.random_policy(SEED, 5000 + k)
+        s.record()
+        env.step()
+        e.record()
+        e.synchronize()
+        ms += s.elapsed_time(e)
+    ph = read(1)
+    per = {NAMES[i]: round(ph[i] / (n * E)) for i in range(len(NAMES))}
+    print(json.dumps({"mask_delta": delta, "k_env_us": 1e3 * ms / n, "mean_cycles_per_game_step": per,
+                      "total_cycles": sum(per.values()),
+                      "max_game_cycles_over_100_steps": {NAMES[i]: ph[16 + i] for i in range(len(NAMES))}}), flush=True)
+    env.close()
