@@ -96,9 +96,14 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
 /* Synthetic masked-uniform random policy (bench / rollouts): per own idle cell a uniform action
  * type among the mask's set type bits, then a uniform parameter among that type's set bits
  * (Philox4x32-10, key = seed, counter = (slot_id_base + slot, step, cell, 0)).  d_masks as written
- * by the calls above (d_source: their source bits, or NULL); d_actions = [n_slots][H*W][7]. */
+ * by the calls above (d_source: their source bits, or NULL); d_actions = [n_slots][H*W][7].
+ * With mask_delta and d_source, a call into the same d_actions as the previous call rewrites only
+ * the rows whose candidate status changed or is set (the result is identical to a full write);
+ * call mrts_policy_invalidate() after writing d_actions yourself. */
 int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_source, uint64_t seed, uint32_t step,
                     int32_t* d_actions, void* stream);
+/* the next mrts_policy_dev call writes every row */
+int mrts_policy_invalidate(mrts_env* env);
 /* Optional compact output of every mask write: mask slot 0 ("own unit without an action here") as
  * bits, uint32 [n_slots][ceil(H*W/32)] (sticky; NULL disables).  mrts_policy_dev uses it, when
  * given, to read only the candidate cells' mask rows. */

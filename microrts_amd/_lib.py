@@ -15,7 +15,7 @@ ERR_BITS = {
 # every symbol include/mrts.h declares
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_reset_dev", "mrts_step_dev",
-    "mrts_get_masks_dev", "mrts_policy_dev", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_get_masks_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
 ]
 
@@ -76,6 +76,7 @@ def load(path=LIB_PATH):
     L.mrts_step_dev.argtypes = [P, P, P, P, P, P, P, I32, P]
     L.mrts_get_masks_dev.argtypes = [P, I32, P, P]
     L.mrts_policy_dev.argtypes = [P, P, P, U64, U32, P, P]
+    L.mrts_policy_invalidate.argtypes = [P]
     L.mrts_set_source_output.argtypes = [P, P]
     L.mrts_get_state.argtypes = [P, I32, P, I32]
     L.mrts_error_flags.argtypes = [P, P]

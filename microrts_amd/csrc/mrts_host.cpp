@@ -24,7 +24,7 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
 #ifdef MRTS_PHASE_TIMING
 hipError_t phaseTimes(unsigned long long* out, int reset);
 #endif
-hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream);
+hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream, bool* prevWritten);
 hipError_t prepareLds(size_t bytes);
 }  // namespace mrts
 
@@ -278,6 +278,11 @@ struct mrts_env {
     const uint8_t* lastMaskPtr = nullptr;
     int lastMaskPlayer = -1;
     uint32_t* d_source = nullptr;
+    // delta policy writes: candidate set of the last source-form policy write, and where it went
+    uint32_t* d_polPrev = nullptr;
+    const int32_t* lastPolicyActions = nullptr;
+    bool polValid = false;
+    int polParity = 0;
     void prepMasks(KDyn& D) {
         D.source = D.masks ? d_source : nullptr;
         D.mask_delta = (maskDelta && D.masks && D.masks == lastMaskPtr && D.mask_player == lastMaskPlayer) ? 1 : 0;
@@ -393,6 +398,7 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         // capacity: one live unit per cell, plus slack for the step's births over its deaths
         env->CAP = env->HW + std::max(64, env->HW / 4);
         if (env->CAP > 0xFFF0) throw Fail{-EINVAL, "map too large"};
+        if ((size_t)env->nSlots * env->HW >= (size_t)1 << 31) throw Fail{-EINVAL, "n_slots * H * W must be < 2^31"};
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, cfg->device));
         const size_t lds = ldsBytes(env->HW, env->W, env->CAP, env->partialObs);
@@ -547,6 +553,12 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
     }
 }
 
+int mrts_policy_invalidate(mrts_env* env) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    env->polValid = false;
+    return 0;
+}
+
 int mrts_set_source_output(mrts_env* env, uint32_t* d_source) {
     if (!env) return -EINVAL;
     env->d_source = d_source;
@@ -568,7 +580,21 @@ int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_sou
         Q.masks = d_masks;
         Q.source = d_source;
         Q.actions = d_actions;
-        HIPCHK(launchPolicy(Q, pickStream(env, stream)));
+        Q.prev = nullptr;
+        Q.prev_out = nullptr;
+        Q.delta = 0;
+        const size_t pw = (size_t)env->nSlots * maskWords(env->HW);
+        if (d_source && env->maskDelta) {  // double-buffered candidate sets: read one, write the other
+            if (!env->d_polPrev) HIPCHK(hipMalloc(&env->d_polPrev, 2 * pw * 4));
+            Q.prev = env->d_polPrev + pw * env->polParity;
+            Q.prev_out = env->d_polPrev + pw * (1 - env->polParity);
+            Q.delta = (env->polValid && d_actions == env->lastPolicyActions) ? 1 : 0;
+        }
+        bool prevWritten = false;
+        HIPCHK(launchPolicy(Q, pickStream(env, stream), &prevWritten));
+        env->polValid = prevWritten;
+        if (prevWritten) env->polParity ^= 1;
+        env->lastPolicyActions = d_actions;
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -719,6 +745,7 @@ void mrts_destroy(mrts_env* env) {
     if (env->stream) (void)hipStreamSynchronize(env->stream);
     (void)hipFree(env->d_static);
     (void)hipFree(env->d_state);
+    (void)hipFree(env->d_polPrev);
     (void)hipFree(env->d_tmpl);
     (void)hipFree(env->d_tmplOff);
     (void)hipFree(env->d_gameKind);

@@ -92,6 +92,9 @@ struct PolicyParams {
     const uint8_t* masks;
     const uint32_t* source;        // optional [n_slots][maskWords(HW)]
     int32_t* actions;
+    const uint32_t* prev;          // delta: candidate set of the previous write to actions
+    uint32_t* prev_out;            // optional (with source): where this write records its candidate set
+    int32_t delta;                 // 1: actions holds the previous output; rewrite only prev|source rows
 };
 
 }  // namespace mrts

@@ -34,15 +34,20 @@ enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2 };
 #ifdef MRTS_PHASE_TIMING
 constexpr int PH_GAMES = 1 << 16;
 __device__ unsigned long long g_phase[16 * PH_GAMES];  // [phase][game], no contention
-#define PHASE(i)                                                                          \
-    do {                                                                                  \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                 \
-        if (lane_id() == 0 && G.g < PH_GAMES) g_phase[(i) * PH_GAMES + G.g] += t_ - tph_; \
-        tph_ = t_;                                                                        \
+#define PHASE_IN(gg, tt, i)                                                           \
+    do {                                                                              \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                             \
+        if (lane_id() == 0 && (gg) < PH_GAMES) g_phase[(i) * PH_GAMES + (gg)] += t_ - (tt); \
+        (tt) = t_;                                                                    \
     } while (0)
+#define PHASE(i) PHASE_IN(G.g, G.tph_, i)  // in the kernel body
+#define MPHASE(i) PHASE_IN(g, tph_, i)     // inside Game methods
 #else
 #define PHASE(i) \
     do {         \
+    } while (0)
+#define MPHASE(i) \
+    do {          \
     } while (0)
 #endif
 enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2 };  // game_kind & 15
@@ -123,6 +128,12 @@ DEV uint64_t rng_of(int lo, int hi) { return (uint64_t)(uint32_t)lo | ((uint64_t
 DEV int snap_in(uint32_t b, int p) { return (b >> p) & 1; }
 DEV int snap_act(uint32_t b, int p) { return (int)((b >> (2 + 3 * p)) & 7); }
 
+// The unit-type table is read with lane-varying indices all over the step; an LDS copy turns those
+// global loads into LDS reads.
+constexpr int UTT_WORDS = (int)(sizeof(DevUtt) / 4);
+constexpr int UTT_LDS = (int)((sizeof(DevUtt) + 15) & ~(size_t)15);
+static_assert(sizeof(DevUtt) % 4 == 0 && UTT_WORDS <= 192, "DevUtt copy: 3 words per lane");
+
 struct Game {
     const KStatic& P;
     const KDyn D;
@@ -146,12 +157,23 @@ struct Game {
     // wave-uniform scalars (only ever modified in uniform control flow)
     int time, nu, pres0, pres1, seq, steps, ccnt, deaths;
     int snapLimit0, snapLimit1;  // seq counter when player 0 / 1's snapshot was taken
+    // issue index (valid while ixValid): `bits` = target cells (+W) of present MOVE/PRODUCE
+    // assignments, whether any exists, and per player the largest present PRODUCE cost (-1 = none)
+#ifdef MRTS_PHASE_TIMING
+    uint64_t tph_;
+#endif
+    bool ixValid;
+    bool anyMP;
+    uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
+    int readySlot;         // per lane: the unit slot of ready item lane_id() (-1 outside cycle)
+    int maxProd0, maxProd1;
     uint32_t err;
     JRand rngCancel, rngDamage, rngSampler;
 
     DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem)
-        : P(p), D(d), U(p.utt), g((int)blockIdx.x), H(p.H), W(p.W), HW(p.HW), CAP(p.CAP), po(p.partial_obs != 0) {
-        uint8_t* q = smem;
+        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(p.H), W(p.W), HW(p.HW), CAP(p.CAP),
+          po(p.partial_obs != 0) {
+        uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
         ua = (uint32_t*)q; q += 4 * CAP;
         at = (int32_t*)q; q += 4 * CAP;
@@ -167,6 +189,9 @@ struct Game {
         rslot = (uint16_t*)q; q += 2 * 64;
         snap = (uint8_t*)q;
         snapLimit0 = snapLimit1 = 0;
+        ixValid = false;
+        killedLanes = 0;
+        readySlot = -1;
     }
     DEV int pres(int p) const { return p == 0 ? pres0 : pres1; }
     DEV void addPres(int p, int v) {
@@ -203,6 +228,12 @@ struct Game {
     DEV void initCells() {  // terrain walls from the map template
         const int32_t* t = tmpl() + T_TERR;
         for (int w = lane_id(); w < (HW + 3) / 4; w += 64) setTerrainWord(w, (uint32_t)t[w]);
+        wsync();
+    }
+    DEV void copyUtt() {  // the LDS copy of the unit-type table, when load() does not fetch it
+        const int32_t* ug = (const int32_t*)&P.utt;
+        int32_t* ul = (int32_t*)&U;
+        for (int i = lane_id(); i < UTT_WORDS; i += 64) ul[i] = ug[i];
         wsync();
     }
     DEV uint32_t* prevG() const { return (uint32_t*)(st() + H_WORDS + N_ARRAYS * CAP); }
@@ -242,12 +273,20 @@ struct Game {
         const int l = lane_id();
         const int TW = (HW + 3) / 4, PW = 2 * maskWords(HW);
         const int hv = l < H_WORDS ? s[l] : 0;
+        const int32_t* ug = (const int32_t*)&P.utt;
+        const int32_t u0 = ug[l], u1 = l + 64 < UTT_WORDS ? ug[l + 64] : 0, u2 = l + 128 < UTT_WORDS ? ug[l + 128] : 0;
         int32_t r[N_ARRAYS];
 #pragma unroll
         for (int a = 0; a < N_ARRAYS; a++) r[a] = arr[a * CAP + l];
         const uint32_t tw = l < TW ? (uint32_t)terr[l] : 0u;
         const uint32_t pv = (wantPrev && l < PW) ? (uint32_t)arr[N_ARRAYS * CAP + l] : 0u;
         loadHeader(hv);
+        {
+            int32_t* ul = (int32_t*)&U;
+            ul[l] = u0;
+            if (l + 64 < UTT_WORDS) ul[l + 64] = u1;
+            if (l + 128 < UTT_WORDS) ul[l + 128] = u2;
+        }
         if (l < nu) {
             uc[l] = (uint32_t)r[A_UC];
             hp[l] = (int16_t)r[A_HP];
@@ -412,6 +451,12 @@ struct Game {
     DEV void decode(int p) {
         int run0, run1;
         baseReservations(p, run0, run1);
+        MPHASE(13);
+        ixValid = false;
+        if (nu <= 64) {
+            decodeUnits(p, run0, run1);
+            return;
+        }
         for (int c0 = 0; c0 < HW; c0 += 64) {
             const int c = c0 + lane_id();
             const int s = c < HW ? cell[c] : EMPTY;
@@ -421,38 +466,101 @@ struct Game {
                 a = ua[s];
                 cand = uplay(uc[s]) == p && (a & UA_DEC) && !(a & (UA_PRESENT | UA_BAD));
             }
-            uint64_t m = ballot(cand);
+            const uint64_t m = ballot(cand);
             if (m == 0) continue;
             const int t = ua_type(a), pr = par[s < CAP ? s : 0];
-            const bool usesPos = cand && (t == T_MOVE || t == T_PRODUCE);
-            const int tpos = c + dyo(pr) * W + dxo(pr) + W;  // ResourceUsage position (UnitAction.java:254-291)
-            const int cost = (cand && t == T_PRODUCE) ? U.cost[ua_ut(a)] : 0;
-            uint64_t acc = 0;
-            while (m) {
-                const int k = __builtin_ctzll(m);
-                m &= m - 1;
-                const bool up = rl(usesPos, k);
-                const int bi = rl(tpos, k), cst = rl(cost, k);
-                bool ok = true;
-                if (up) ok = !((uniu(bits[bi >> 5]) >> (bi & 31)) & 1u);
-                if (run0 != 0) {
-                    const int sum = (p == 0 ? cst : 0) + run0;
-                    if (sum > 0 && sum > pres0) ok = false;
-                }
-                if (run1 != 0) {
-                    const int sum = (p == 1 ? cst : 0) + run1;
-                    if (sum > 0 && sum > pres1) ok = false;
-                }
-                if (ok) {
-                    if (up && lane_id() == 0) bits[bi >> 5] |= 1u << (bi & 31);
-                    if (p == 0) run0 += cst;
-                    else run1 += cst;
-                    acc |= 1ull << k;
-                }
-            }
+            const uint64_t acc = acceptChain(p, run0, run1, cand, lanes_below(m), __popcll(m), t, pr, c, a);
             if ((acc >> lane_id()) & 1ull) ua[s] = a | UA_PA;
             wsync();
         }
+    }
+    // Unit-parallel form (all units in one wave): the candidates' ascending-cell order is a rank
+    // computed in registers, so the serial part is the acceptance chain alone.
+    DEV void decodeUnits(int p, int& run0, int& run1) {
+        const int o = lane_id();
+        uint32_t a = 0, cu = 0;
+        bool cand = false;
+        if (o < nu) {
+            cu = uc[o];
+            a = ua[o];
+            cand = !(cu & UC_DEAD) && uplay(cu) == p && (a & UA_DEC) && !(a & (UA_PRESENT | UA_BAD));
+        }
+        const uint64_t m = ballot(cand);
+        if (m == 0) return;
+        const int c = uy(cu) * W + ux(cu);
+        const int pr = o < nu ? par[o] : 0;
+        MPHASE(12);
+        const int rank = cellRank(m, cand, c);
+        MPHASE(14);
+        const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), ua_type(a), pr, c, a);
+        if ((acc >> o) & 1ull) ua[o] = a | UA_PA;
+        wsync();
+    }
+    // rank of each candidate lane among the candidates m by cell c (cells are distinct)
+    DEV int cellRank(uint64_t m, bool cand, int c) const {
+        int rank = 0;
+        for (uint64_t mm = m; mm; mm &= mm - 1) rank += rl(c, __builtin_ctzll(mm)) < c;
+        return cand ? rank : -1;
+    }
+    // acceptChain with the reservation bitmap held one word per lane (readlane instead of LDS reads)
+    DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB) {
+        uint32_t bv = lane_id() < NB ? bits[lane_id()] : 0u;
+        uint64_t acc = 0;
+        for (int r = 0; r < n; r++) {
+            const int k = __builtin_ctzll(ballot(rank == r));
+            const bool up = rl(usesPos, k);
+            const int bi = rl(tpos, k), cst = rl(cost, k);
+            bool ok = true;
+            if (up) ok = !(((uint32_t)rl((int)bv, bi >> 5) >> (bi & 31)) & 1u);
+            if (run0 != 0) {
+                const int sum = (p == 0 ? cst : 0) + run0;
+                if (sum > 0 && sum > pres0) ok = false;
+            }
+            if (run1 != 0) {
+                const int sum = (p == 1 ? cst : 0) + run1;
+                if (sum > 0 && sum > pres1) ok = false;
+            }
+            if (ok) {
+                if (up && lane_id() == (bi >> 5)) bv |= 1u << (bi & 31);
+                if (p == 0) run0 += cst;
+                else run1 += cst;
+                acc |= 1ull << k;
+            }
+        }
+        if (lane_id() < NB) bits[lane_id()] = bv;
+        return acc;
+    }
+    // ua.ru.consistentWith(running ru) for the n candidates in rank order (PlayerAction.java:503-520);
+    // returns the accepted lanes
+    DEV uint64_t acceptChain(int p, int& run0, int& run1, bool cand, int rank, int n, int t, int pr, int c, uint32_t a) {
+        const bool usesPos = cand && (t == T_MOVE || t == T_PRODUCE);
+        const int tpos = c + dyo(pr) * W + dxo(pr) + W;  // ResourceUsage position (UnitAction.java:254-291)
+        const int cost = (cand && t == T_PRODUCE) ? U.cost[ua_ut(a)] : 0;
+        const int NB = (HW + 2 * W + 31) / 32;
+        if (NB <= 64) return acceptChainReg(p, run0, run1, rank, n, usesPos, tpos, cost, NB);
+        uint64_t acc = 0;
+        for (int r = 0; r < n; r++) {
+            const int k = __builtin_ctzll(ballot(rank == r));
+            const bool up = rl(usesPos, k);
+            const int bi = rl(tpos, k), cst = rl(cost, k);
+            bool ok = true;
+            if (up) ok = !((uniu(bits[bi >> 5]) >> (bi & 31)) & 1u);
+            if (run0 != 0) {
+                const int sum = (p == 0 ? cst : 0) + run0;
+                if (sum > 0 && sum > pres0) ok = false;
+            }
+            if (run1 != 0) {
+                const int sum = (p == 1 ? cst : 0) + run1;
+                if (sum > 0 && sum > pres1) ok = false;
+            }
+            if (ok) {
+                if (up && lane_id() == 0) bits[bi >> 5] |= 1u << (bi & 31);
+                if (p == 0) run0 += cst;
+                else run1 += cst;
+                acc |= 1ull << k;
+            }
+        }
+        return acc;
     }
 
     // ------------------------------------------------------------------ issueSafe / issue
@@ -622,10 +730,97 @@ struct Game {
         wsync();
     }
 
-    // GameState.issueSafe(pa) (rts/GameState.java:338-408).  Agent pa = [accepted rows in cell order]
-    // + PlayerAction.fillWithNones(gs, p, fillDur) (rts/PlayerAction.java:328-346) in list order;
-    // AI pa (RandomBiasedAI / PassiveAI) = its units in list order (listOrder).
-    DEV void issuePA(int s, bool isPA, uint64_t m) {
+    // Issue index over ALL units (GameState.issue checks every present assignment, :255-262).
+    DEV void buildIssueIndex() {
+        const int NB = (HW + 2 * W + 31) / 32;
+        for (int i = lane_id(); i < NB; i += 64) bits[i] = 0;
+        wsync();
+        bool mp = false;
+        int mc0 = -1, mc1 = -1;
+        for (int o = lane_id(); o < nu; o += 64) {
+            const uint32_t a = ua[o];
+            const int t = ua_type(a);
+            if (!(a & UA_PRESENT) || (t != T_MOVE && t != T_PRODUCE)) continue;
+            mp = true;
+            const uint32_t c = uc[o];
+            const int d = par[o];
+            const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
+            atomicOr(&bits[pos >> 5], 1u << (pos & 31));
+            if (t == T_PRODUCE) {
+                if (uplay(c) == 0) mc0 = max(mc0, U.cost[ua_ut(a)]);
+                else mc1 = max(mc1, U.cost[ua_ut(a)]);
+            }
+        }
+        anyMP = ballot(mp) != 0;
+        maxProd0 = -wave_min(-mc0);
+        maxProd1 = -wave_min(-mc1);
+        ixValid = true;
+        wsync();
+    }
+
+    // GameState.issue (rts/GameState.java:252-326) for a batch of (unit s, action) lanes in rank order
+    // 0..n-1.  When no new MOVE/PRODUCE conflicts with a present assignment or an earlier one of the
+    // batch, every issue() takes its no-conflict branch and the batch is issued in parallel (seq =
+    // seq + rank); otherwise the batch runs one pair at a time through issueOne.
+    DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut) {
+        const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
+        const bool np = act && t == T_PRODUCE;
+        const uint64_t mpm = ballot(mp);
+        bool conf = false;
+        int ntgt = 0, ncost = 0, pl = 0;
+        if (mpm) {
+            if (!ixValid) buildIssueIndex();
+            if (mp) {
+                const uint32_t cu = uc[s];
+                pl = uplay(cu);
+                ntgt = (uy(cu) + dyo(prm)) * W + ux(cu) + dxo(prm);
+                ncost = np ? U.cost[ut] : 0;
+                const int pr = pl == 0 ? pres0 : pres1;
+                conf = (bits[(ntgt + W) >> 5] >> ((ntgt + W) & 31)) & 1u;
+                if (np) {
+                    if (anyMP && ncost > 0 && ncost > pr) conf = true;
+                    const int mc = pl == 0 ? maxProd0 : maxProd1;
+                    if (mc >= 0 && mc + ncost > 0 && mc + ncost > pr) conf = true;
+                }
+            }
+            for (uint64_t mm = mpm; mm; mm &= mm - 1) {  // earlier MOVE/PRODUCE lanes of the batch
+                const int k = __builtin_ctzll(mm);
+                const int rk = rl(rank, k), tk = rl(ntgt, k), pk = rl(pl, k), ck = rl(np ? ncost : -1, k);
+                if (mp && rk < rank) {
+                    if (tk == ntgt) conf = true;
+                    if (np) {
+                        const int sum = ((ck >= 0 && pk == pl) ? ck : 0) + ncost;
+                        if (sum > 0 && sum > (pl == 0 ? pres0 : pres1)) conf = true;
+                    }
+                }
+            }
+        }
+        if (ballot(conf) == 0) {
+            if (act) {
+                ua[s] = pack_ua(t, ut, tx, ty) | UA_PRESENT;
+                par[s] = (int16_t)prm;
+                at[s] = time;
+                as[s] = seq + rank;
+                if (mp && ixValid) atomicOr(&bits[(ntgt + W) >> 5], 1u << ((ntgt + W) & 31));
+            }
+            seq += n;
+            if (mpm) {
+                anyMP = true;
+                maxProd0 = max(maxProd0, -wave_min(np && pl == 0 ? -ncost : 1));
+                maxProd1 = max(maxProd1, -wave_min(np && pl == 1 ? -ncost : 1));
+            }
+            wsync();
+        } else {
+            for (int r = 0; r < n; r++) {
+                const int k = __builtin_ctzll(ballot(act && rank == r));
+                issueOne(rl(s, k), rl(t, k), rl(prm, k), rl(tx, k), rl(ty, k), rl(ut, k));
+            }
+            ixValid = false;
+        }
+    }
+
+    // GameState.issueSafe(pa) (rts/GameState.java:338-408) of the lanes' decoded actions.
+    DEV void issuePA(int s, bool isPA, int rank, int n) {
         int t = 0, prm = 0, tx = 0, ty = 0, ut = 0;
         if (isPA) {
             const uint32_t a = ua[s];
@@ -637,29 +832,40 @@ struct Game {
             legality(s, t, prm, tx, ty, ut);
         }
         wsync();
-        while (m) {
-            const int k = __builtin_ctzll(m);
-            m &= m - 1;
-            issueOne(rl(s, k), rl(t, k), rl(prm, k), rl(tx, k), rl(ty, k), rl(ut, k));
-        }
+        issueBatch(isPA, rank, n, s, t, prm, tx, ty, ut);
     }
+    // Agent pa = [accepted rows in cell order] + PlayerAction.fillWithNones(gs, p, fillDur)
+    // (rts/PlayerAction.java:328-346) in list order; AI pa (RandomBiasedAI / PassiveAI) = its units
+    // in list order (listOrder).
     DEV void issuePlayer(int p, int fillDur, bool listOrder) {
-        if (!listOrder) {
+        ixValid = false;
+        if (!listOrder && nu <= 64) {
+            const int o = lane_id();
+            uint32_t cu = 0;
+            bool isPA = false;
+            if (o < nu) {
+                cu = uc[o];
+                isPA = !(cu & UC_DEAD) && uplay(cu) == p && (ua[o] & UA_PA);
+            }
+            const uint64_t m = ballot(isPA);
+            if (m) issuePA(o, isPA, cellRank(m, isPA, uy(cu) * W + ux(cu)), __popcll(m));
+        } else if (!listOrder) {
             for (int c0 = 0; c0 < HW; c0 += 64) {
                 const int c = c0 + lane_id();
                 const int s = c < HW ? cell[c] : EMPTY;
                 const bool isPA = s < CAP && uplay(uc[s]) == p && (ua[s] & UA_PA);
                 const uint64_t m = ballot(isPA);
-                if (m) issuePA(s, isPA, m);
+                if (m) issuePA(s, isPA, lanes_below(m), __popcll(m));
             }
         } else {
             for (int o0 = 0; o0 < nu; o0 += 64) {
                 const int o = o0 + lane_id();
                 const bool isPA = o < nu && !(uc[o] & UC_DEAD) && uplay(uc[o]) == p && (ua[o] & UA_PA);
                 const uint64_t m = ballot(isPA);
-                if (m) issuePA(o, isPA, m);
+                if (m) issuePA(o, isPA, lanes_below(m), __popcll(m));
             }
         }
+        // the NONE fills never conflict (issue() checks MOVE/PRODUCE only): parallel, seq in list order
         for (int o0 = 0; o0 < nu; o0 += 64) {
             const int o = o0 + lane_id();
             bool fill = false;
@@ -667,13 +873,16 @@ struct Game {
                 const uint32_t c = uc[o];
                 fill = !(c & UC_DEAD) && uplay(c) == p && !(ua[o] & (UA_PRESENT | UA_PA));
             }
-            uint64_t m = ballot(fill);
-            while (m) {
-                const int k = __builtin_ctzll(m);
-                m &= m - 1;
-                issueOne(o0 + k, T_NONE, fillDur, 0, 0, 0);
+            const uint64_t m = ballot(fill);
+            if (fill) {
+                ua[o] = pack_ua(T_NONE, 0, 0, 0) | UA_PRESENT;
+                par[o] = (int16_t)fillDur;
+                at[o] = time;
+                as[o] = seq + lanes_below(m);
             }
+            seq += __popcll(m);
         }
+        wsync();
     }
 
     // ------------------------------------------------------------------ RandomBiasedAI
@@ -908,6 +1117,7 @@ struct Game {
 
     // ------------------------------------------------------------------ cycle
     DEV void kill(int k) {  // GameState.removeUnit (rts/GameState.java:79-82)
+        killedLanes |= ballot(readySlot == k);
         if (lane_id() == 0) {
             const uint32_t c = uc[k];
             uc[k] = c | UC_DEAD;
@@ -918,13 +1128,12 @@ struct Game {
         wsync();
     }
     // UnitAction.execute (rts/UnitAction.java:338-465) — also for units killed earlier in the loop
-    DEV void execute(int s) {
-        const uint32_t cu = uniu(uc[s]);
+    DEV void execute(int s) { execute(s, uniu(uc[s]), uniu(ua[s]), uni(par[s])); }
+    // cu / a / prm: the unit's core word, its assignment and parameter (wave-uniform)
+    DEV void execute(int s, uint32_t cu, uint32_t a, int prm) {
         const bool dead = cu & UC_DEAD;
         const int x = ux(cu), y = uy(cu), typ = utyp(cu), pl = uplay(cu);
-        const uint32_t a = uniu(ua[s]);
         const int t = ua_type(a);
-        const int prm = uni(par[s]);
         switch (t) {
             case T_MOVE: {
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
@@ -1039,12 +1248,31 @@ struct Game {
             wsync();
             if (k < R) rslot[rank] = (uint16_t)myslot;
             wsync();
-            for (int r = 0; r < R; r++) {
-                const int os = uni(rslot[r]);
-                if (lane_id() == 0) ua[os] &= ~(UA_READY | UA_PRESENT);
-                wsync();
-                execute(os);
+            // lane r now holds ready item r (insertion order).  Every ready assignment leaves the
+            // map (ua's PRESENT/READY) before any executes: no execute reads another unit's flags.
+            // NONE executes as a no-op, so only the other types run, one by one, from registers —
+            // a unit's core word changes under another's execute only by a kill (tracked in `killed`).
+            const int os = k < R ? rslot[k] : 0;
+            uint32_t a = 0, cu = 0;
+            int prm = 0;
+            if (k < R) {
+                a = ua[os];
+                cu = uc[os];
+                prm = par[os];
+                ua[os] = a & ~(UA_READY | UA_PRESENT);
             }
+            wsync();
+            uint64_t work = ballot(k < R && ua_type(a) != T_NONE);
+            killedLanes = 0;
+            readySlot = k < R ? os : -1;
+            while (work) {
+                const int r = __builtin_ctzll(work);
+                work &= work - 1;
+                uint32_t c = uniu(rl((int)cu, r));
+                if ((killedLanes >> r) & 1ull) c |= UC_DEAD;
+                execute(rl(os, r), c, uniu(rl((int)a, r)) & ~(UA_READY | UA_PRESENT), rl(prm, r));
+            }
+            readySlot = -1;
         } else {  // > 64 ready assignments: repeated minimum search
             while (true) {
                 int best = INF;
@@ -1380,6 +1608,7 @@ struct Game {
         const bool delta = D.mask_delta && (total & 15) == 0;
         uint32_t* pg = prevG();
         const int l = lane_id();
+        if (delta && nu <= 64 && nslots * MW <= 64 && writeMasksUnits(slot0, nslots, pl0, pl1)) return;
         int nlist = 0;
         for (int i = 0; i < nslots; i++) {
             const int p = i ? pl1 : pl0;
@@ -1407,6 +1636,7 @@ struct Game {
                 }
             }
         }
+        MPHASE(11);
         if (delta) {
             if (nlist) flushDirty(nlist, slot0, pl0, pl1);
             return;
@@ -1426,6 +1656,52 @@ struct Game {
                 }
             }
         }
+    }
+    // Delta form with all units in one wave: the new row sets come from the units (one atomicOr per
+    // idle unit), old|new per bit word gives the dirty cells, and a wave prefix sum lists them.
+    // Returns false (nothing written) when the list would exceed 64 cells.
+    DEV bool writeMasksUnits(int slot0, int nslots, int pl0, int pl1) {
+        const int MW = maskWords(HW), NW = nslots * MW;
+        const int l = lane_id();
+        uint32_t* nb = (uint32_t*)rseq;  // cycle() scratch, free here: [slot i][MW] new bits
+        if (l < NW) nb[l] = 0;
+        wsync();
+        if (l < nu) {
+            const uint32_t cu = uc[l];
+            if (!(cu & UC_DEAD) && !(ua[l] & UA_PRESENT)) {
+                const int op = uplay(cu), c = uy(cu) * W + ux(cu);
+                if (op >= 0 && op == pl0) atomicOr(&nb[c >> 5], 1u << (c & 31));
+                if (nslots > 1 && op >= 0 && op == pl1) atomicOr(&nb[MW + (c >> 5)], 1u << (c & 31));
+            }
+        }
+        wsync();
+        uint32_t cur = 0, old = 0;
+        int i = 0, w = 0;
+        if (l < NW) {
+            i = l >= MW;
+            w = l - i * MW;
+            cur = nb[l];
+            old = mprev[(i ? pl1 : pl0) * MW + w];
+        }
+        const uint32_t dirty = cur | old;
+        const int n = __popc(dirty);
+        int incl = n;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int t = __shfl_up(incl, off);
+            if (l >= off) incl += t;
+        }
+        const int total = rl(incl, 63);
+        if (total > 64) return false;
+        if (l < NW) {
+            if (D.source) D.source[(size_t)(slot0 + i) * MW + w] = cur;
+            prevG()[(i ? pl1 : pl0) * MW + w] = cur;
+        }
+        if (total == 0) return true;
+        int k = incl - n;
+        for (uint32_t d = dirty; d; d &= d - 1) rslot[k++] = (uint16_t)((i << 15) | (32 * w + __builtin_ctz(d)));
+        flushDirty(total, slot0, pl0, pl1);
+        return true;
     }
     // rewrite the chunks of the listed dirty cells (rslot[0..n): slot index << 15 | cell)
     DEV void flushDirty(int n, int slot0, int pl0, int pl1) {
@@ -1467,10 +1743,11 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     const int side = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
     bool freshObs = true;  // observation comes from the current (post-step or fresh) state
 #ifdef MRTS_PHASE_TIMING
-    uint64_t tph_ = __builtin_amdgcn_s_memtime();
+    G.tph_ = __builtin_amdgcn_s_memtime();
 #endif
 
     if (MODE == MODE_RESET) {
+        G.copyUtt();
         G.loadHeader(G.st());
         G.err = 0;
         G.initCells();
@@ -1699,6 +1976,35 @@ __global__ __launch_bounds__(64) void k_policy_tiled(PolicyParams Q) {
     for (int i = 4 * nw4 + lane; i < nw; i += 64) dst[i] = sa[i];
 }
 
+// one candidate cell's action from its K-byte mask record: record bits 0..K-1 gathered from the
+// covering aligned 16-B chunks (chunk q's byte 0 sits at record bit pos = 16q - b0)
+DEV void sampleRecord(const PolicyParams& Q, const uint8_t* mrec, int slot, int c, int32_t row[7]) {
+    const int b0 = c * Q.K, j0 = b0 >> 4, j1 = (b0 + Q.K - 1) >> 4;
+    uint64_t r0 = 0, r1 = 0;
+    for (int q = j0; q <= j1; q++) {
+        const uint64_t b16 = pack16(((const uint4*)mrec)[q]);
+        const int pos = 16 * q - b0;
+        if (pos < 0) {
+            r0 |= b16 >> (-pos);
+        } else if (pos < 64) {
+            r0 |= b16 << pos;
+            if (pos > 48) r1 |= b16 >> (64 - pos);
+        } else {
+            r1 |= b16 << (pos - 64);
+        }
+    }
+    // record bits 1..K-1 -> lo/hi (bit i -> bit i-1)
+    uint64_t lo = (r0 >> 1) | (r1 << 63), hi = r1 >> 1;
+    const int nb = Q.K - 1;
+    if (nb < 64) {
+        lo &= (1ull << nb) - 1;
+        hi = 0;
+    } else {
+        hi &= (1ull << (nb - 64)) - 1;
+    }
+    sampleBits(Q, lo, hi, slot, c, row);
+}
+
 // Source-bit form: one wave = one slot.  Candidate cells come from the env's source bits; only their
 // mask records are read (the <= 6 aligned 16-B chunks covering each).  Rows are composed in LDS,
 // 256 cells (7 KB) at a time, and leave with coalesced dwordx4 stores.
@@ -1715,34 +2021,7 @@ __global__ __launch_bounds__(64) void k_policy_src(PolicyParams Q) {
         for (int j = 0; j < 4; j++) {
             const int c = c0 + 64 * j + lane;
             int32_t row[7] = {0, 0, 0, 0, 0, 0, 0};
-            if (c < Q.HW && ((src[c >> 5] >> (c & 31)) & 1u)) {
-                // record bytes [b0, b0+K) -> record bits 0..K-1 in (r0, r1), from the covering
-                // aligned 16-B chunks; chunk q's byte 0 sits at record bit pos = 16q - b0
-                const int b0 = c * Q.K, j0 = b0 >> 4, j1 = (b0 + Q.K - 1) >> 4;
-                uint64_t r0 = 0, r1 = 0;
-                for (int q = j0; q <= j1; q++) {
-                    const uint64_t b16 = pack16(((const uint4*)mrec)[q]);
-                    const int pos = 16 * q - b0;
-                    if (pos < 0) {
-                        r0 |= b16 >> (-pos);
-                    } else if (pos < 64) {
-                        r0 |= b16 << pos;
-                        if (pos > 48) r1 |= b16 >> (64 - pos);
-                    } else {
-                        r1 |= b16 << (pos - 64);
-                    }
-                }
-                // record bits 1..K-1 -> lo/hi (bit i -> bit i-1)
-                uint64_t lo = (r0 >> 1) | (r1 << 63), hi = r1 >> 1;
-                const int nb = Q.K - 1;
-                if (nb < 64) {
-                    lo &= (1ull << nb) - 1;
-                    hi = 0;
-                } else {
-                    hi &= (1ull << (nb - 64)) - 1;
-                }
-                sampleBits(Q, lo, hi, slot, c, row);
-            }
+            if (c < Q.HW && ((src[c >> 5] >> (c & 31)) & 1u)) sampleRecord(Q, mrec, slot, c, row);
             const int r = 64 * j + lane;  // stride-7 words: conflict-free LDS writes
 #pragma unroll
             for (int k = 0; k < 7; k++) sa[r * 7 + k] = row[k];
@@ -1753,6 +2032,51 @@ __global__ __launch_bounds__(64) void k_policy_src(PolicyParams Q) {
         for (int i = lane; i < nw4; i += 64) ((int4*)d)[i] = ((const int4*)sa)[i];
         for (int i = 4 * nw4 + lane; i < nw; i += 64) d[i] = sa[i];
         __syncthreads();
+    }
+    if (Q.prev_out)
+        for (int w = lane; w < MW; w += 64) Q.prev_out[(size_t)slot * MW + w] = src[w];
+}
+
+// Delta form (actions holds this policy's previous output, whose candidate set is prev): only rows
+// in prev | source change — candidates get a fresh action, former candidates a zero row.  A wave
+// takes 64 (slot, 32-cell bit word) items in one load round, compacts their dirty cells into an LDS
+// list (wave prefix sum), and spreads the list over its lanes, so each dirty row costs one record
+// round trip in parallel with the others.  The candidate set is double-buffered (prev -> prev_out).
+__global__ __launch_bounds__(64) void k_policy_delta(PolicyParams Q) {
+    __shared__ uint32_t list[64 * 32];
+    const int lane = (int)threadIdx.x;
+    const uint32_t MW = (uint32_t)(Q.HW + 31) / 32;
+    const uint32_t nitems = (uint32_t)Q.n_slots * MW;
+    const uint32_t item = blockIdx.x * 64u + (uint32_t)lane;
+    const bool valid = item < nitems;
+    const uint32_t cur = valid ? Q.source[item] : 0u, old = valid ? Q.prev[item] : 0u;
+    if (valid) Q.prev_out[item] = cur;
+    const uint32_t dirty = cur | old;
+    const int n = __popc(dirty);
+    int incl = n;  // inclusive prefix sum over lanes
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int t = __shfl_up(incl, off);
+        if (lane >= off) incl += t;
+    }
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    if (total == 0) return;
+    const uint32_t slot = item / MW, w = item - slot * MW;
+    int k = incl - n;
+    for (uint32_t d = dirty; d; d &= d - 1) {
+        const int b = __builtin_ctz(d);
+        // row index slot*HW + cell (< 2^31 by the host's size checks), bit 31 = candidate
+        list[k++] = (slot * (uint32_t)Q.HW + 32u * w + (uint32_t)b) | (((cur >> b) & 1u) << 31);
+    }
+    __syncthreads();
+    for (int i = lane; i < total; i += 64) {
+        const uint32_t e = list[i], r = e & 0x7FFFFFFFu;
+        const int sl = (int)(r / (uint32_t)Q.HW), c = (int)(r - (uint32_t)sl * Q.HW);
+        int32_t row[7] = {0, 0, 0, 0, 0, 0, 0};
+        if (e >> 31) sampleRecord(Q, Q.masks + (size_t)sl * Q.HW * Q.K, sl, c, row);
+        int32_t* dst = Q.actions + (size_t)r * 7;
+#pragma unroll
+        for (int q = 0; q < 7; q++) dst[q] = row[q];
     }
 }
 
@@ -1793,7 +2117,7 @@ hipError_t phaseTimes(unsigned long long* out, int reset) {
 }
 #endif
 size_t ldsBytes(int HW, int W, int CAP, int po) {
-    return (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) +
+    return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) +
            (po ? 4 * (size_t)HW : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
 }
@@ -1813,9 +2137,15 @@ hipError_t prepareLds(size_t bytes) {
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_MASKS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     return e;
 }
-hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream) {
+// *prevWritten: the launch recorded its candidate set in Q.prev (a later call may use the delta form)
+hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream, bool* prevWritten) {
     dim3 grid((unsigned)((Q.HW + 63) / 64), (unsigned)Q.n_slots), block(64);
-    if (Q.source && ((size_t)Q.HW * Q.K) % 16 == 0 && Q.HW % 4 == 0 && Q.K <= 96 && Q.K >= 65)
+    const bool srcOk = Q.source && ((size_t)Q.HW * Q.K) % 16 == 0 && Q.HW % 4 == 0 && Q.K <= 96 && Q.K >= 65;
+    *prevWritten = srcOk && Q.prev_out;
+    if (srcOk && Q.delta && Q.prev)
+        hipLaunchKernelGGL(k_policy_delta, dim3((unsigned)(((size_t)Q.n_slots * ((Q.HW + 31) / 32) + 63) / 64)), block,
+                           0, stream, Q);
+    else if (srcOk)
         hipLaunchKernelGGL(k_policy_src, dim3((unsigned)Q.n_slots), block, 0, stream, Q);
     else if (((size_t)Q.HW * Q.K) % 16 == 0 && (64 * Q.K) % 16 == 0 && Q.HW % 4 == 0 && Q.K <= 96)
         hipLaunchKernelGGL(k_policy_tiled, grid, block, 0, stream, Q);

@@ -230,6 +230,7 @@ class DeviceVecEnv:
         if self.source is not None:
             _lib.check(h.L.mrts_set_source_output(h.h, self._p(self.source)))
         self.mask_player = 0
+        self._policy_out, self._policy_version = None, -1
         torch.cuda.synchronize(dev)
 
     @staticmethod
@@ -262,7 +263,12 @@ class DeviceVecEnv:
         m = self.masks if masks is None else masks
         out = self.actions if out is None else out
         src = self.source if masks is None else None
+        # the library rewrites only changed rows when `out` still holds its previous output; an
+        # in-place write by anyone else bumps the tensor's version counter -> full rewrite
+        if self._policy_out is not out or out._version != self._policy_version:
+            _lib.check(h.L.mrts_policy_invalidate(h.h))
         _lib.check(h.L.mrts_policy_dev(h.h, self._p(m), self._p(src), seed, step, self._p(out), self._s(stream)))
+        self._policy_out, self._policy_version = out, out._version
         return out
 
     def synchronize(self):

@@ -238,13 +238,20 @@ def test_delta_masks_and_source_policy_match_full(mp, po, n_bot):
     b = DeviceVecEnv(n_sp, n_bot, 150, maps, seed=11, partial_obs=po, ai2s=bots, mask_delta=False, source_bits=False)
     a.reset()
     b.reset()
+    rng = np.random.default_rng(2)
+    S, H, W = len(maps), a.dims[1], a.dims[2]
     for step in range(400):
-        a.random_policy(SEED, step)
-        b.random_policy(SEED, step)
+        if step % 37 == 5:  # caller-written actions: the next policy call must rewrite every row
+            acts = torch.as_tensor(rng.integers(0, 3, (S, H * W, 7)).astype(np.int32), device=a.actions.device)
+            a.actions.copy_(acts)
+            b.actions.copy_(acts)
+        else:
+            a.random_policy(SEED, step)
+            b.random_policy(SEED, step)
         a.synchronize()
         b.synchronize()
         assert torch.equal(a.masks, b.masks), f"delta masks differ at step {step}"
-        assert torch.equal(a.actions, b.actions), f"source-bit policy differs at step {step}"
+        assert torch.equal(a.actions, b.actions), f"source-bit / delta policy differs at step {step}"
         src = a.source.cpu().numpy().view(np.uint32)
         m0 = b.masks.cpu().numpy()[..., 0].reshape(len(maps), -1)
         bits = (src[:, np.arange(m0.shape[1]) >> 5] >> (np.arange(m0.shape[1]) & 31)) & 1

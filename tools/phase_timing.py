@@ -17,8 +17,8 @@ L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_timing.so"))
 L.mrts_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_int]
 from microrts_amd import DeviceVecEnv  # noqa: E402
 
-NAMES = ["load", "predecode", "decode", "issue", "cycle", "outcome+reset", "obs", "compact", "stashMasks",
-         "writeMasks", "store"]
+NAMES = ["load", "predecode", "decode(chain)", "issue", "cycle", "outcome+reset", "obs", "compact", "stashMasks",
+         "writeMasks(flush)", "store", "writeMasks(scan)", "decode(unitLoads)", "decode(baseRes)", "decode(cellRank)"]
 E = int(os.environ.get("E", 4096))
 MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
 SEED = 0x5EEDC0DE
