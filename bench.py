@@ -6,7 +6,9 @@ self-play games per GPU (8192 player slots), UTT VERSION_ORIGINAL + CANCEL_BOTH,
 masked uniform random policy (Philox, seed 0x5EEDC0DE), legal-action masks and observations written
 every step.  One "step" = one batched gameStep of every game on every GPU: the policy kernel reads
 the masks and writes the int32 action tensor, then the fused step kernel (decode -> issueSafe ->
-cycle -> WinLoss -> auto-reset -> observation -> masks) consumes it.  An env-step is one game-cycle
+cycle -> WinLoss -> auto-reset -> observation -> masks) consumes it.  Default mask mode "delta":
+the mask / action tensors are persistent and only rows that changed are rewritten (identical
+contents to a full rewrite, tested); --mask-mode full rewrites every byte.  An env-step is one game-cycle
 (a self-play game counts once, not twice).  Inputs are resident in HBM; nothing crosses PCIe in
 the timed region.
 
@@ -136,12 +138,31 @@ def main():
     flags = env.error_flags()
     assert not flags.any(), f"engine error flags set: {np.unique(flags)}"
 
-    # B per player slot = A + O + M + S_slot, A = HW*7*4, O = C*HW*4, M = HW*K,
-    # S = 2*(16*U + 2*HW + 16) per game (read + write), split over its two slots.
+    # Roofline bytes per step-kernel launch.  The step's HBM contract under the persistent-buffer
+    # (delta) mask mode — what any implementation must move:
+    #   A = idle-unit action rows read (28 B each; other rows are ignored by the Java decode),
+    #   O = C*HW*4 observation written per slot,
+    #   M = K bytes per mask row that changed (delta) or HW*K per slot (full rewrite),
+    #   S = per game: header 64 B + 28 B/unit, read and written; terrain HW B read; previous row sets
+    #       (2 * maskWords * 4 B) read and written; per slot the source bits (maskWords * 4 B) written.
+    # SURVEY.md §8(d)'s figure assumed a full mask rewrite and all rows read; it is reported next to it.
     HW = H * W
-    per_slot = HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16)
-    alg_bytes = per_slot * S
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    MWB = 4 * ((HW + 31) // 32)
+    dirty = rows
+    if env.source is not None and a.mask_mode == "delta":
+        lut = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int64, device=env.device)
+        tot, n_probe = 0, 5
+        for k in range(n_probe):  # untimed probe steps after the timed window
+            before = env.source.clone()
+            one_step(a.burnin + a.warmup + a.steps + k)
+            env.synchronize()
+            tot += int(lut[(before | env.source).view(torch.uint8).long()].sum().item())
+        dirty = tot / (n_probe * S)
+    n_games = S // 2
+    m_bytes = dirty * K if a.mask_mode == "delta" else HW * K
+    contract = S * (rows * 28 + C * HW * 4 + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
+    survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16))
+    achieved = contract / (kern_ms * 1e-3) / 1e9
     total_games = E * world
     value = total_games * a.steps / t
     out = {
@@ -177,7 +198,11 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": a.pmc_traffic,
             "kernel": "k_env<MODE_STEP>",
-            "alg_bytes_per_launch": alg_bytes,
+            "alg_bytes_per_launch": contract,
+            "alg_bytes_note": f"step contract bytes, {a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "
+                              f"changed mask rows per slot (DESIGN.md §5)",
+            "survey_8d_bytes_per_launch": survey,
+            "survey_8d_equivalent_GBps": survey / (kern_ms * 1e-3) / 1e9,
         },
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -23,6 +23,7 @@ size_t ldsBytes(int HW, int W, int CAP, int po);
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream);
 #ifdef MRTS_PHASE_TIMING
 hipError_t phaseTimes(unsigned long long* out, int reset);
+hipError_t phaseSpans(unsigned long long* out, int n);
 #endif
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream, bool* prevWritten);
 hipError_t prepareLds(size_t bytes);
@@ -765,5 +766,6 @@ void mrts_destroy(mrts_env* env) {
 #ifdef MRTS_PHASE_TIMING
 // diagnostic build only: per-phase cycle sums of k_env (tools/phase_timing.py)
 int mrts_phase_times(unsigned long long* out, int reset) { return mrts::phaseTimes(out, reset) == hipSuccess ? 0 : -EIO; }
+int mrts_phase_spans(unsigned long long* out, int n) { return mrts::phaseSpans(out, n) == hipSuccess ? 0 : -EIO; }
 #endif
 }  // extern "C"

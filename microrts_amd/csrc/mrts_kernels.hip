@@ -34,14 +34,15 @@ enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2 };
 #ifdef MRTS_PHASE_TIMING
 constexpr int PH_GAMES = 1 << 16;
 __device__ unsigned long long g_phase[16 * PH_GAMES];  // [phase][game], no contention
-#define PHASE_IN(gg, tt, i)                                                           \
-    do {                                                                              \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();                             \
-        if (lane_id() == 0 && (gg) < PH_GAMES) g_phase[(i) * PH_GAMES + (gg)] += t_ - (tt); \
-        (tt) = t_;                                                                    \
+__device__ unsigned long long g_span[2 * PH_GAMES];    // last launch: [game] start / end, s_memrealtime (100 MHz)
+#define PHASE_IN(acc, tt, i)                          \
+    do {                                              \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+        (acc)[i] += t_ - (tt);                        \
+        (tt) = t_;                                    \
     } while (0)
-#define PHASE(i) PHASE_IN(G.g, G.tph_, i)  // in the kernel body
-#define MPHASE(i) PHASE_IN(g, tph_, i)     // inside Game methods
+#define PHASE(i) PHASE_IN(G.phAcc, G.tph_, i)  // in the kernel body
+#define MPHASE(i) PHASE_IN(phAcc, tph_, i)     // inside Game methods
 #else
 #define PHASE(i) \
     do {         \
@@ -158,15 +159,17 @@ struct Game {
     int time, nu, pres0, pres1, seq, steps, ccnt, deaths;
     int snapLimit0, snapLimit1;  // seq counter when player 0 / 1's snapshot was taken
     // issue index (valid while ixValid): `bits` = target cells (+W) of present MOVE/PRODUCE
-    // assignments, whether any exists, and per player the largest present PRODUCE cost (-1 = none)
+    // assignments, whether any exists, per player the largest present PRODUCE cost (-1 = none) and
+    // the sum of present PRODUCE costs
 #ifdef MRTS_PHASE_TIMING
     uint64_t tph_;
+    uint64_t phAcc[16];  // per-phase cycles (registers: constant indices), flushed at kernel end
 #endif
     bool ixValid;
     bool anyMP;
     uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
     int readySlot;         // per lane: the unit slot of ready item lane_id() (-1 outside cycle)
-    int maxProd0, maxProd1;
+    int maxProd0, maxProd1, sumProd0, sumProd1;
     uint32_t err;
     JRand rngCancel, rngDamage, rngSampler;
 
@@ -379,48 +382,73 @@ struct Game {
     // player(s), lane-parallel, in ONE round of global loads: a pure function of (row, unit).  The
     // decoded action is parked in the unit's empty assignment fields with UA_DEC.
     DEV void predecode(const int32_t* rows0, const int32_t* rows1, int only) {
-        const int R = U.maxAttackRadius, ctr = R / 2;
         bool bad_any = false;
-        for (int o = lane_id(); o < nu; o += 64) {
+        const int l = lane_id();
+        // units 0..63: rows requested first, the issue index (LDS only) is built while they are in
+        // flight, then decoded
+        int32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
+        bool act = false;
+        if (l < nu) {
+            const uint32_t cu = uc[l];
+            const int pl = uplay(cu);
+            act = !(pl < 0 || (ua[l] & UA_PRESENT) || (only >= 0 && pl != only));
+            if (act) {
+                const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)(uy(cu) * W + ux(cu)) * 7;
+#pragma unroll
+                for (int k = 0; k < 7; k++) a[k] = r[k];
+            }
+        }
+        if (!po && (HW + 2 * W + 31) / 32 <= 64) buildIndex();
+        if (act) bad_any |= decodeRow(l, a);
+        for (int o = l + 64; o < nu; o += 64) {
             const uint32_t cu = uc[o];
             const int pl = uplay(cu);
             if (pl < 0 || (ua[o] & UA_PRESENT) || (only >= 0 && pl != only)) continue;
-            const int x = ux(cu), y = uy(cu), c = y * W + x;
-            const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)c * 7;
-            const int a0 = r[0], a1 = r[1], a2 = r[2], a3 = r[3], a4 = r[4], a5 = r[5], a6 = r[6];
-            int t = (a0 >= 0 && a0 <= 5) ? a0 : ACT_INVALID, pr = -1, ut = 0, tx = 0, ty = 0;
-            bool bad = false;
-            switch (t) {
-                case T_MOVE: pr = clampdir(a1); break;
-                case T_HARVEST: pr = clampdir(a2); break;
-                case T_RETURN: pr = clampdir(a3); break;
-                case T_PRODUCE:
-                    pr = clampdir(a4);
-                    if (a5 < 0 || a5 >= U.ntypes) bad = true;  // utt.getUnitType(int) throws (:697)
-                    else ut = a5;
-                    break;
-                case T_ATTACK: {
-                    const int ax = x + (a6 % R - ctr), ay = y + (a6 / R - ctr);
-                    if (inb(ax, ay)) {
-                        tx = ax;
-                        ty = ay;
-                    } else {
-                        tx = ty = 255;  // off-map target: never legal
-                    }
-                } break;
-            }
-            bad_any |= bad;
-            ua[o] = pack_ua(t, ut, tx, ty) | UA_DEC | (bad ? UA_BAD : 0u);
-            par[o] = (int16_t)pr;
+            const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)(uy(cu) * W + ux(cu)) * 7;
+            int32_t b[7];
+#pragma unroll
+            for (int k = 0; k < 7; k++) b[k] = r[k];
+            bad_any |= decodeRow(o, b);
         }
         if (ballot(bad_any)) err |= E_PRODUCE_TYPE;
         wsync();
+    }
+    // UnitAction.fromVectorAction of row a for unit o; returns "produce type out of range"
+    DEV bool decodeRow(int o, const int32_t a[7]) {
+        const int R = U.maxAttackRadius, ctr = R / 2;
+        const uint32_t cu = uc[o];
+        const int x = ux(cu), y = uy(cu);
+        int t = (a[0] >= 0 && a[0] <= 5) ? a[0] : ACT_INVALID, pr = -1, ut = 0, tx = 0, ty = 0;
+        bool bad = false;
+        switch (t) {
+            case T_MOVE: pr = clampdir(a[1]); break;
+            case T_HARVEST: pr = clampdir(a[2]); break;
+            case T_RETURN: pr = clampdir(a[3]); break;
+            case T_PRODUCE:
+                pr = clampdir(a[4]);
+                if (a[5] < 0 || a[5] >= U.ntypes) bad = true;  // utt.getUnitType(int) throws (:697)
+                else ut = a[5];
+                break;
+            case T_ATTACK: {
+                const int ax = x + (a[6] % R - ctr), ay = y + (a[6] / R - ctr);
+                if (inb(ax, ay)) {
+                    tx = ax;
+                    ty = ay;
+                } else {
+                    tx = ty = 255;  // off-map target: never legal
+                }
+            } break;
+        }
+        ua[o] = pack_ua(t, ut, tx, ty) | UA_DEC | (bad ? UA_BAD : 0u);
+        par[o] = (int16_t)pr;
+        return bad;
     }
 
     // Base reservations of every current assignment the deciding view holds (PlayerAction.java:497-505,
     // merged as ResourceUsage.java:92-97); in a PO view only snapshot units' assignments count.
     DEV void baseReservations(int p, int& r0, int& r1) {
         const int NB = (HW + 2 * W + 31) / 32;
+        ixValid = false;  // `bits` now holds this view's set
         for (int i = lane_id(); i < NB; i += 64) bits[i] = 0;
         wsync();
         int s0 = 0, s1 = 0;
@@ -450,13 +478,22 @@ struct Game {
     // acceptance chain is serial; accepted units get UA_PA.
     DEV void decode(int p) {
         int run0, run1;
-        baseReservations(p, run0, run1);
+        // full observability: the base reservations are the issue index (every present MOVE/PRODUCE
+        // target + per-player PRODUCE cost sums), kept current across issue batches
+        const bool useIx = !po && (HW + 2 * W + 31) / 32 <= 64;
+        if (useIx) {
+            if (!ixValid) buildIndex();
+            run0 = sumProd0;
+            run1 = sumProd1;
+        } else {
+            baseReservations(p, run0, run1);
+        }
         MPHASE(13);
-        ixValid = false;
         if (nu <= 64) {
-            decodeUnits(p, run0, run1);
+            decodeUnits(p, run0, run1, useIx);
             return;
         }
+        ixValid = false;  // the chain below adds to `bits`
         for (int c0 = 0; c0 < HW; c0 += 64) {
             const int c = c0 + lane_id();
             const int s = c < HW ? cell[c] : EMPTY;
@@ -469,14 +506,14 @@ struct Game {
             const uint64_t m = ballot(cand);
             if (m == 0) continue;
             const int t = ua_type(a), pr = par[s < CAP ? s : 0];
-            const uint64_t acc = acceptChain(p, run0, run1, cand, lanes_below(m), __popcll(m), t, pr, c, a);
+            const uint64_t acc = acceptChain(p, run0, run1, cand, lanes_below(m), __popcll(m), t, pr, c, a, false);
             if ((acc >> lane_id()) & 1ull) ua[s] = a | UA_PA;
             wsync();
         }
     }
     // Unit-parallel form (all units in one wave): the candidates' ascending-cell order is a rank
     // computed in registers, so the serial part is the acceptance chain alone.
-    DEV void decodeUnits(int p, int& run0, int& run1) {
+    DEV void decodeUnits(int p, int& run0, int& run1, bool keepBits) {
         const int o = lane_id();
         uint32_t a = 0, cu = 0;
         bool cand = false;
@@ -492,7 +529,7 @@ struct Game {
         MPHASE(12);
         const int rank = cellRank(m, cand, c);
         MPHASE(14);
-        const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), ua_type(a), pr, c, a);
+        const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), ua_type(a), pr, c, a, keepBits);
         if ((acc >> o) & 1ull) ua[o] = a | UA_PA;
         wsync();
     }
@@ -503,7 +540,8 @@ struct Game {
         return cand ? rank : -1;
     }
     // acceptChain with the reservation bitmap held one word per lane (readlane instead of LDS reads)
-    DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB) {
+    DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB,
+                                bool keepBits) {
         uint32_t bv = lane_id() < NB ? bits[lane_id()] : 0u;
         uint64_t acc = 0;
         for (int r = 0; r < n; r++) {
@@ -527,17 +565,19 @@ struct Game {
                 acc |= 1ull << k;
             }
         }
-        if (lane_id() < NB) bits[lane_id()] = bv;
+        if (!keepBits && lane_id() < NB) bits[lane_id()] = bv;
         return acc;
     }
     // ua.ru.consistentWith(running ru) for the n candidates in rank order (PlayerAction.java:503-520);
     // returns the accepted lanes
-    DEV uint64_t acceptChain(int p, int& run0, int& run1, bool cand, int rank, int n, int t, int pr, int c, uint32_t a) {
+    // keepBits: `bits` is left as it was (the chain's additions stay in registers)
+    DEV uint64_t acceptChain(int p, int& run0, int& run1, bool cand, int rank, int n, int t, int pr, int c, uint32_t a,
+                             bool keepBits) {
         const bool usesPos = cand && (t == T_MOVE || t == T_PRODUCE);
         const int tpos = c + dyo(pr) * W + dxo(pr) + W;  // ResourceUsage position (UnitAction.java:254-291)
         const int cost = (cand && t == T_PRODUCE) ? U.cost[ua_ut(a)] : 0;
         const int NB = (HW + 2 * W + 31) / 32;
-        if (NB <= 64) return acceptChainReg(p, run0, run1, rank, n, usesPos, tpos, cost, NB);
+        if (NB <= 64) return acceptChainReg(p, run0, run1, rank, n, usesPos, tpos, cost, NB, keepBits);
         uint64_t acc = 0;
         for (int r = 0; r < n; r++) {
             const int k = __builtin_ctzll(ballot(rank == r));
@@ -730,13 +770,17 @@ struct Game {
         wsync();
     }
 
-    // Issue index over ALL units (GameState.issue checks every present assignment, :255-262).
-    DEV void buildIssueIndex() {
+    // Issue index over ALL units (GameState.issue checks every present assignment, :255-262); under
+    // full observability it is also every view's base ResourceUsage (PlayerAction.java:497-505).
+    DEV void buildIndex() {
+#ifdef MRTS_PHASE_TIMING
+        phAcc[15] += 1000;  // call counter (x1000 so the per-step mean shows)
+#endif
         const int NB = (HW + 2 * W + 31) / 32;
         for (int i = lane_id(); i < NB; i += 64) bits[i] = 0;
         wsync();
         bool mp = false;
-        int mc0 = -1, mc1 = -1;
+        int mc0 = -1, mc1 = -1, s0 = 0, s1 = 0;
         for (int o = lane_id(); o < nu; o += 64) {
             const uint32_t a = ua[o];
             const int t = ua_type(a);
@@ -747,13 +791,21 @@ struct Game {
             const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
             atomicOr(&bits[pos >> 5], 1u << (pos & 31));
             if (t == T_PRODUCE) {
-                if (uplay(c) == 0) mc0 = max(mc0, U.cost[ua_ut(a)]);
-                else mc1 = max(mc1, U.cost[ua_ut(a)]);
+                const int k = U.cost[ua_ut(a)];
+                if (uplay(c) == 0) {
+                    mc0 = max(mc0, k);
+                    s0 += k;
+                } else {
+                    mc1 = max(mc1, k);
+                    s1 += k;
+                }
             }
         }
         anyMP = ballot(mp) != 0;
         maxProd0 = -wave_min(-mc0);
         maxProd1 = -wave_min(-mc1);
+        sumProd0 = wave_sum(s0);
+        sumProd1 = wave_sum(s1);
         ixValid = true;
         wsync();
     }
@@ -769,7 +821,7 @@ struct Game {
         bool conf = false;
         int ntgt = 0, ncost = 0, pl = 0;
         if (mpm) {
-            if (!ixValid) buildIssueIndex();
+            if (!ixValid) buildIndex();
             if (mp) {
                 const uint32_t cu = uc[s];
                 pl = uplay(cu);
@@ -808,9 +860,14 @@ struct Game {
                 anyMP = true;
                 maxProd0 = max(maxProd0, -wave_min(np && pl == 0 ? -ncost : 1));
                 maxProd1 = max(maxProd1, -wave_min(np && pl == 1 ? -ncost : 1));
+                sumProd0 += wave_sum(np && pl == 0 ? ncost : 0);
+                sumProd1 += wave_sum(np && pl == 1 ? ncost : 0);
             }
             wsync();
         } else {
+#ifdef MRTS_PHASE_TIMING
+            phAcc[11] += 1000;  // slow-path batches
+#endif
             for (int r = 0; r < n; r++) {
                 const int k = __builtin_ctzll(ballot(act && rank == r));
                 issueOne(rl(s, k), rl(t, k), rl(prm, k), rl(tx, k), rl(ty, k), rl(ut, k));
@@ -838,7 +895,6 @@ struct Game {
     // (rts/PlayerAction.java:328-346) in list order; AI pa (RandomBiasedAI / PassiveAI) = its units
     // in list order (listOrder).
     DEV void issuePlayer(int p, int fillDur, bool listOrder) {
-        ixValid = false;
         if (!listOrder && nu <= 64) {
             const int o = lane_id();
             uint32_t cu = 0;
@@ -1218,6 +1274,7 @@ struct Game {
     // (ETA + issue time <= time) in insertion order, then remove + execute each in that order.
     DEV void cycle() {
         time++;
+        ixValid = false;
         // gather the ready list into LDS (slot order), count R
         int R = 0;
         for (int o0 = 0; o0 < nu; o0 += 64) {
@@ -1743,7 +1800,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     const int side = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
     bool freshObs = true;  // observation comes from the current (post-step or fresh) state
 #ifdef MRTS_PHASE_TIMING
+    for (int i = 0; i < 16; i++) G.phAcc[i] = 0;
     G.tph_ = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();
 #endif
 
     if (MODE == MODE_RESET) {
@@ -1849,6 +1908,13 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         G.store();
     }
     PHASE(10);
+#ifdef MRTS_PHASE_TIMING
+    if (lane_id() == 0 && G.g < PH_GAMES) {
+        for (int i = 0; i < 16; i++) g_phase[i * PH_GAMES + G.g] += G.phAcc[i];
+        g_span[G.g] = rt0_;
+        g_span[PH_GAMES + G.g] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- random policy (bench / rollouts)
@@ -2112,6 +2178,16 @@ hipError_t phaseTimes(unsigned long long* out, int reset) {
     if (reset) {
         std::fill(h.begin(), h.end(), 0ull);
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_phase), h.data(), h.size() * sizeof(h[0]));
+    }
+    return e;
+}
+hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts then [n] ends of the last launch
+    std::vector<unsigned long long> h((size_t)2 * PH_GAMES);
+    hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_span), h.size() * sizeof(h[0]));
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < n && i < PH_GAMES; i++) {
+        out[i] = h[i];
+        out[n + i] = h[PH_GAMES + i];
     }
     return e;
 }

@@ -15,10 +15,12 @@ from microrts_amd import _lib  # noqa: E402
 
 L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_timing.so"))
 L.mrts_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.mrts_phase_spans.argtypes = [ctypes.c_void_p, ctypes.c_int]
 from microrts_amd import DeviceVecEnv  # noqa: E402
 
 NAMES = ["load", "predecode", "decode(chain)", "issue", "cycle", "outcome+reset", "obs", "compact", "stashMasks",
-         "writeMasks(flush)", "store", "writeMasks(scan)", "decode(unitLoads)", "decode(baseRes)", "decode(cellRank)"]
+         "writeMasks(flush)", "store", "slowIssueBatches(x1000)", "decode(unitLoads)", "decode(baseRes)", "decode(cellRank)",
+         "buildIndexCalls(x1000)"]
 E = int(os.environ.get("E", 4096))
 MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
 SEED = 0x5EEDC0DE
@@ -49,8 +51,18 @@ for delta in (True, False):
         e.synchronize()
         ms += s.elapsed_time(e)
     ph = read(1)
+    sp = (ctypes.c_ulonglong * (2 * E))()
+    _lib.check(L.mrts_phase_spans(sp, E))
+    import numpy as np
+    st = np.array(sp[:E], dtype=np.float64)
+    en = np.array(sp[E:], dtype=np.float64)
+    t0 = st.min()
+    spans = {"dispatch_spread_us": (st.max() - t0) / 100.0, "kernel_span_us": (en.max() - t0) / 100.0,
+             "game_us_mean": float((en - st).mean()) / 100.0, "game_us_p99": float(np.percentile(en - st, 99)) / 100.0,
+             "game_us_max": float((en - st).max()) / 100.0,
+             "start_us_percentiles": [float(np.percentile(st - t0, q)) / 100.0 for q in (10, 50, 90, 99)]}
     per = {NAMES[i]: round(ph[i] / (n * E)) for i in range(len(NAMES))}
-    print(json.dumps({"mask_delta": delta, "k_env_us": 1e3 * ms / n, "mean_cycles_per_game_step": per,
+    print(json.dumps({"mask_delta": delta, "k_env_us": 1e3 * ms / n, "last_launch": spans, "mean_cycles_per_game_step": per,
                       "total_cycles": sum(per.values()),
                       "max_game_cycles_over_100_steps": {NAMES[i]: ph[16 + i] for i in range(len(NAMES))}}), flush=True)
     env.close()
