@@ -81,6 +81,13 @@ int mrts_dims(const mrts_env* env, int32_t* n_slots, int32_t* H, int32_t* W, int
 int mrts_reset(mrts_env* env, const int32_t* players, mrts_responses* out);                       /* reset(int[]) :179-211 */
 int mrts_step(mrts_env* env, const int32_t* actions, const int32_t* players, mrts_responses* out); /* gameStep :213-297 */
 int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out /* [n_slots][H][W][K] */);          /* getMasks :307-316 */
+/* gameStep with the Java layout, int[][][] action (:213), as flat int32 [n_slots][n_rows][8]: row =
+ * [pos, type, move dir, harvest dir, return dir, produce dir, produce type, attack index], any order,
+ * any count, a unit may be named twice — exactly PlayerAction.fromVectorAction's list semantics
+ * (rts/PlayerAction.java:384-417) followed by issueSafe (rts/GameState.java:338-408). */
+int mrts_step_rows(mrts_env* env, const int32_t* rows, int32_t n_rows, const int32_t* players, mrts_responses* out);
+/* getMasks in the Java element type: int32 [n_slots][H][W][K] (int[][][][], :307-316) */
+int mrts_get_masks_i32(mrts_env* env, int32_t player, int32_t* out);
 
 /* Device-pointer API: same semantics, caller-owned HBM buffers, stream-ordered on `stream`
  * (a hipStream_t; NULL = HIP's default stream, as everywhere in HIP; mrts_stream() gives the handle's
@@ -92,6 +99,10 @@ int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, doub
 int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                   uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream);
 int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stream);
+/* device forms of mrts_step_rows / mrts_get_masks_i32 (d_out 16-byte aligned) */
+int mrts_step_rows_dev(mrts_env* env, const int32_t* d_rows, int32_t n_rows, const int32_t* d_players, int32_t* d_obs,
+                       double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream);
+int mrts_get_masks_i32_dev(mrts_env* env, int32_t player, int32_t* d_out, void* stream);
 
 /* Synthetic masked-uniform random policy (bench / rollouts): per own idle cell a uniform action
  * type among the mask's set type bits, then a uniform parameter among that type's set bits

@@ -14,8 +14,8 @@ ERR_BITS = {
 
 # every symbol include/mrts.h declares
 EXPORTS = [
-    "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_reset_dev", "mrts_step_dev",
-    "mrts_get_masks_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_step_rows", "mrts_get_masks_i32",
+    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
 ]
 
@@ -72,6 +72,10 @@ def load(path=LIB_PATH):
     L.mrts_reset.argtypes = [P, P, ctypes.POINTER(MrtsResponses)]
     L.mrts_step.argtypes = [P, P, P, ctypes.POINTER(MrtsResponses)]
     L.mrts_get_masks.argtypes = [P, I32, P]
+    L.mrts_step_rows.argtypes = [P, P, I32, P, ctypes.POINTER(MrtsResponses)]
+    L.mrts_get_masks_i32.argtypes = [P, I32, P]
+    L.mrts_step_rows_dev.argtypes = [P, P, I32, P, P, P, P, P, I32, P]
+    L.mrts_get_masks_i32_dev.argtypes = [P, I32, P, P]
     L.mrts_reset_dev.argtypes = [P, P, P, P, P, P, I32, P]
     L.mrts_step_dev.argtypes = [P, P, P, P, P, P, P, I32, P]
     L.mrts_get_masks_dev.argtypes = [P, I32, P, P]

@@ -26,6 +26,7 @@ hipError_t phaseTimes(unsigned long long* out, int reset);
 hipError_t phaseSpans(unsigned long long* out, int n);
 #endif
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream, bool* prevWritten);
+hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t stream);
 hipError_t prepareLds(size_t bytes);
 }  // namespace mrts
 
@@ -281,6 +282,12 @@ struct mrts_env {
     uint32_t* d_source = nullptr;
     // delta policy writes: candidate set of the last source-form policy write, and where it went
     uint32_t* d_polPrev = nullptr;
+    // Java row layout (mrts_step_rows*): accepted-pair scratch [n_games][n_rows][2] and host staging
+    uint32_t* d_pairs = nullptr;
+    int pairsRows = 0;
+    int32_t* d_rowsStage = nullptr;
+    size_t rowsStageInts = 0;
+    int32_t* d_masks32 = nullptr;
     const int32_t* lastPolicyActions = nullptr;
     bool polValid = false;
     int polParity = 0;
@@ -537,6 +544,51 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
     }
 }
 
+int mrts_step_rows_dev(mrts_env* env, const int32_t* d_rows, int32_t n_rows, const int32_t* d_players, int32_t* d_obs,
+                       double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream) {
+    try {
+        if (!d_rows && n_rows > 0) throw Fail{-EINVAL, "rows is null"};
+        if (n_rows < 0 || (size_t)n_rows * env->nSlots * 8 >= ((size_t)1 << 31)) throw Fail{-EINVAL, "bad n_rows"};
+        HIPCHK(hipSetDevice(env->device));
+        if (n_rows > env->pairsRows) {
+            hipStream_t s = pickStream(env, stream);
+            HIPCHK(hipStreamSynchronize(s));  // the old scratch may still be in use on the stream
+            (void)hipFree(env->d_pairs);
+            env->d_pairs = nullptr;
+            HIPCHK(hipMalloc(&env->d_pairs, (size_t)env->nGames * n_rows * 2 * 4));
+            env->pairsRows = n_rows;
+        }
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.rows = d_rows;
+        D.n_rows = n_rows;
+        D.pairs = env->d_pairs;
+        D.players = d_players;
+        D.obs = d_obs;
+        D.reward = d_reward;
+        D.done = d_done;
+        D.masks = d_masks;
+        D.mask_player = mask_player;
+        env->prepMasks(D);
+        HIPCHK(env->launch(0, D, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_get_masks_i32_dev(mrts_env* env, int32_t player, int32_t* d_out, void* stream) {
+    try {
+        if (!d_out) throw Fail{-EINVAL, "out is null"};
+        int r = mrts_get_masks_dev(env, player, env->d_masks, stream);
+        if (r) return r;
+        HIPCHK(launchWiden(env->d_masks, d_out, (size_t)env->nSlots * env->HW * env->K, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
 int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stream) {
     try {
         if (!d_out) throw Fail{-EINVAL, "out is null"};
@@ -648,6 +700,48 @@ int mrts_step(mrts_env* env, const int32_t* actions, const int32_t* players, mrt
     }
 }
 
+int mrts_step_rows(mrts_env* env, const int32_t* rows, int32_t n_rows, const int32_t* players, mrts_responses* out) {
+    try {
+        if (!rows && n_rows > 0) throw Fail{-EINVAL, "rows is null"};
+        if (n_rows < 0) throw Fail{-EINVAL, "bad n_rows"};
+        HIPCHK(hipSetDevice(env->device));
+        const size_t S = (size_t)env->nSlots, n = S * (size_t)n_rows * 8;
+        if (n > env->rowsStageInts) {
+            HIPCHK(hipStreamSynchronize(env->stream));
+            (void)hipFree(env->d_rowsStage);
+            env->d_rowsStage = nullptr;
+            HIPCHK(hipMalloc(&env->d_rowsStage, n * 4));
+            env->rowsStageInts = n;
+        }
+        if (n) HIPCHK(hipMemcpyAsync(env->d_rowsStage, rows, n * 4, hipMemcpyHostToDevice, env->stream));
+        if (players) HIPCHK(hipMemcpyAsync(env->d_players, players, S * 4, hipMemcpyHostToDevice, env->stream));
+        else HIPCHK(hipMemsetAsync(env->d_players, 0, S * 4, env->stream));
+        int r = mrts_step_rows_dev(env, env->d_rowsStage, n_rows, env->d_players, env->d_obs, env->d_reward, env->d_done,
+                                   nullptr, 0, env->stream);
+        if (r) return r;
+        fillResponses(env, out);
+        checkFlagsAfter(env);
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_get_masks_i32(mrts_env* env, int32_t player, int32_t* out) {
+    try {
+        if (!out) throw Fail{-EINVAL, "out is null"};
+        const size_t n = (size_t)env->nSlots * env->HW * env->K;
+        if (!env->d_masks32) HIPCHK(hipMalloc(&env->d_masks32, n * 4));
+        int r = mrts_get_masks_i32_dev(env, player, env->d_masks32, env->stream);
+        if (r) return r;
+        HIPCHK(hipMemcpyAsync(out, env->d_masks32, n * 4, hipMemcpyDeviceToHost, env->stream));
+        HIPCHK(hipStreamSynchronize(env->stream));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
 int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out) {
     try {
         if (!out) throw Fail{-EINVAL, "out is null"};
@@ -747,6 +841,9 @@ void mrts_destroy(mrts_env* env) {
     (void)hipFree(env->d_static);
     (void)hipFree(env->d_state);
     (void)hipFree(env->d_polPrev);
+    (void)hipFree(env->d_pairs);
+    (void)hipFree(env->d_rowsStage);
+    (void)hipFree(env->d_masks32);
     (void)hipFree(env->d_tmpl);
     (void)hipFree(env->d_tmplOff);
     (void)hipFree(env->d_gameKind);

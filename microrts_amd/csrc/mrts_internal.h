@@ -83,6 +83,9 @@ struct KDyn {
     uint32_t* source;              // [n_slots][maskWords(HW)] mask slot 0 as bits, or null
     int32_t mask_player;           // player whose masks bot-env slots receive
     int32_t mask_delta;            // 1: `masks` holds the previous masks of this handle -> rewrite changed rows only
+    const int32_t* rows;           // Java row layout [n_slots][n_rows][8] (replaces `actions`) or null
+    int32_t n_rows;
+    uint32_t* pairs;               // rows mode: per game [n_rows][2] accepted-pair scratch
 };
 
 struct PolicyParams {

@@ -415,10 +415,20 @@ struct Game {
     }
     // UnitAction.fromVectorAction of row a for unit o; returns "produce type out of range"
     DEV bool decodeRow(int o, const int32_t a[7]) {
+        int t, pr, ut, tx, ty;
+        const bool bad = decodeFields(uc[o], a, t, pr, ut, tx, ty);
+        ua[o] = pack_ua(t, ut, tx, ty) | UA_DEC | (bad ? UA_BAD : 0u);
+        par[o] = (int16_t)pr;
+        return bad;
+    }
+    // UnitAction.fromVectorAction (rts/UnitAction.java:675-709) of row components a[0..6] for a unit
+    // with core word cu
+    DEV bool decodeFields(uint32_t cu, const int32_t a[7], int& t, int& pr, int& ut, int& tx, int& ty) const {
         const int R = U.maxAttackRadius, ctr = R / 2;
-        const uint32_t cu = uc[o];
         const int x = ux(cu), y = uy(cu);
-        int t = (a[0] >= 0 && a[0] <= 5) ? a[0] : ACT_INVALID, pr = -1, ut = 0, tx = 0, ty = 0;
+        t = (a[0] >= 0 && a[0] <= 5) ? a[0] : ACT_INVALID;
+        pr = -1;
+        ut = tx = ty = 0;
         bool bad = false;
         switch (t) {
             case T_MOVE: pr = clampdir(a[1]); break;
@@ -439,9 +449,79 @@ struct Game {
                 }
             } break;
         }
-        ua[o] = pack_ua(t, ut, tx, ty) | UA_DEC | (bad ? UA_BAD : 0u);
-        par[o] = (int16_t)pr;
         return bad;
+    }
+
+    // ------------------------------------------------------------------ Java row layout
+    // PlayerAction.fromVectorAction over Java rows [pos, 7 comps] in list order (rts/PlayerAction.java:
+    // 384-417): a row counts iff an own unit with no assignment stands at (pos % W, pos / W); rows may
+    // name a unit twice (both can be accepted).  Accepted pairs go, in order, to the game's scratch.
+    // Returns the pair count.
+    DEV int rowsDecode(int p, const int32_t* rows) {
+        int run0, run1;
+        baseReservations(p, run0, run1);
+        const int l = lane_id();
+        uint32_t* pairs = D.pairs + (size_t)g * D.n_rows * 2;
+        int npairs = 0;
+        bool badAny = false;
+        for (int r0 = 0; r0 < D.n_rows; r0 += 64) {
+            const int r = r0 + l;
+            int32_t a[8] = {-1, 0, 0, 0, 0, 0, 0, 0};
+            if (r < D.n_rows)
+#pragma unroll
+                for (int k = 0; k < 8; k++) a[k] = rows[(size_t)r * 8 + k];
+            const int pos = a[0];
+            bool cand = false;
+            int s = 0, t = 0, pr = 0, ut = 0, tx = 0, ty = 0;
+            uint32_t cu = 0;
+            if (pos >= 0 && pos < HW) {
+                s = cell[pos];
+                if (s < CAP) {
+                    cu = uc[s];
+                    cand = uplay(cu) == p && !(ua[s] & UA_PRESENT);
+                }
+            }
+            if (cand) {
+                const bool bad = decodeFields(cu, a + 1, t, pr, ut, tx, ty);
+                badAny |= bad;
+                cand = !bad;  // Java throws here (UnitAction.java:697): reported as E_PRODUCE_TYPE
+            }
+            const uint64_t m = ballot(cand);
+            if (m == 0) continue;
+            const uint32_t av = pack_ua(t, ut, 0, 0);
+            const uint64_t acc = acceptChain(p, run0, run1, cand, cand ? lanes_below(m) : -1, __popcll(m), t, pr, pos, av, false);
+            if ((acc >> l) & 1ull) {
+                const int idx = npairs + lanes_below(acc);
+                pairs[(size_t)idx * 2] = (uint32_t)s | ((uint32_t)t << 16) | ((uint32_t)ut << 20);
+                pairs[(size_t)idx * 2 + 1] = (uint32_t)(uint16_t)pr | ((uint32_t)tx << 16) | ((uint32_t)ty << 24);
+            }
+            npairs += __popcll(acc);
+        }
+        if (ballot(badAny)) err |= E_PRODUCE_TYPE;
+        __threadfence();  // the pairs are read back (by other lanes) in rowsIssue
+        return npairs;
+    }
+    // issueSafe(pa) for the pairs of rowsDecode + fillWithNones(gs, p, fillDur) (PlayerAction.java:217-235)
+    DEV void rowsIssue(int p, int npairs, int fillDur) {
+        const uint32_t* pairs = D.pairs + (size_t)g * D.n_rows * 2;
+        for (int b0 = 0; b0 < npairs; b0 += 64) {
+            const int k = b0 + lane_id();
+            const bool act = k < npairs;
+            int s = 0, t = 0, prm = 0, tx = 0, ty = 0, ut = 0;
+            if (act) {
+                const uint32_t w0 = pairs[(size_t)k * 2], w1 = pairs[(size_t)k * 2 + 1];
+                s = (int)(w0 & 0xFFFFu);
+                t = (int)((w0 >> 16) & 0xFu);
+                ut = (int)((w0 >> 20) & 0xFu);
+                prm = (int)(int16_t)(w1 & 0xFFFFu);
+                tx = (int)((w1 >> 16) & 0xFFu);
+                ty = (int)(w1 >> 24);
+                legality(s, t, prm, tx, ty, ut);
+            }
+            wsync();
+            issueBatch(act, lane_id(), min(64, npairs - b0), s, t, prm, tx, ty, ut, true);
+        }
+        issueFills(p, fillDur);
     }
 
     // Base reservations of every current assignment the deciding view holds (PlayerAction.java:497-505,
@@ -506,7 +586,7 @@ struct Game {
             const uint64_t m = ballot(cand);
             if (m == 0) continue;
             const int t = ua_type(a), pr = par[s < CAP ? s : 0];
-            const uint64_t acc = acceptChain(p, run0, run1, cand, lanes_below(m), __popcll(m), t, pr, c, a, false);
+            const uint64_t acc = acceptChain(p, run0, run1, cand, cand ? lanes_below(m) : -1, __popcll(m), t, pr, c, a, false);
             if ((acc >> lane_id()) & 1ull) ua[s] = a | UA_PA;
             wsync();
         }
@@ -760,13 +840,16 @@ struct Game {
                 }
             }
         }
+        // a unit with an assignment here got it from an earlier pair of this pa (Java rows may name a
+        // unit twice): LinkedHashMap.put replaces the value and keeps the entry's position
+        const bool again = (uniu(ua[s]) & UA_PRESENT) != 0;
         if (lane_id() == 0) {
             ua[s] = pack_ua(t, ut, tx, ty) | UA_PRESENT;
             par[s] = (int16_t)prm;
             at[s] = time;
-            as[s] = seq;
+            if (!again) as[s] = seq;
         }
-        seq++;
+        if (!again) seq++;
         wsync();
     }
 
@@ -814,11 +897,20 @@ struct Game {
     // 0..n-1.  When no new MOVE/PRODUCE conflicts with a present assignment or an earlier one of the
     // batch, every issue() takes its no-conflict branch and the batch is issued in parallel (seq =
     // seq + rank); otherwise the batch runs one pair at a time through issueOne.
-    DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut) {
+    // checkDup (Java rows): a unit named by an earlier pair of this pa (same batch, or already issued)
+    // forces the one-at-a-time path
+    DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut, bool checkDup = false) {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
         const uint64_t mpm = ballot(mp);
         bool conf = false;
+        if (checkDup) {
+            if (act && (ua[s] & UA_PRESENT)) conf = true;
+            for (uint64_t mm = ballot(act); mm; mm &= mm - 1) {
+                const int k = __builtin_ctzll(mm);
+                if (act && rl(s, k) == s && rl(rank, k) < rank) conf = true;
+            }
+        }
         int ntgt = 0, ncost = 0, pl = 0;
         if (mpm) {
             if (!ixValid) buildIndex();
@@ -828,7 +920,7 @@ struct Game {
                 ntgt = (uy(cu) + dyo(prm)) * W + ux(cu) + dxo(prm);
                 ncost = np ? U.cost[ut] : 0;
                 const int pr = pl == 0 ? pres0 : pres1;
-                conf = (bits[(ntgt + W) >> 5] >> ((ntgt + W) & 31)) & 1u;
+                if ((bits[(ntgt + W) >> 5] >> ((ntgt + W) & 31)) & 1u) conf = true;
                 if (np) {
                     if (anyMP && ncost > 0 && ncost > pr) conf = true;
                     const int mc = pl == 0 ? maxProd0 : maxProd1;
@@ -921,7 +1013,10 @@ struct Game {
                 if (m) issuePA(o, isPA, lanes_below(m), __popcll(m));
             }
         }
-        // the NONE fills never conflict (issue() checks MOVE/PRODUCE only): parallel, seq in list order
+        issueFills(p, fillDur);
+    }
+    // the NONE fills never conflict (issue() checks MOVE/PRODUCE only): parallel, seq in list order
+    DEV void issueFills(int p, int fillDur) {
         for (int o0 = 0; o0 < nu; o0 += 64) {
             const int o = o0 + lane_id();
             bool fill = false;
@@ -1824,7 +1919,22 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
-        if (gtype == GT_SELFPLAY) {
+        if (D.rows && gtype == GT_SELFPLAY) {
+            for (int p = 0; p < 2; p++) {
+                if (G.po) G.snapshot(p);
+                const int np = G.rowsDecode(p, D.rows + (size_t)(slot0 + p) * D.n_rows * 8);
+                G.rowsIssue(p, np, 1);
+            }
+        } else if (D.rows && gtype == GT_AGENT_VS_BOT) {
+            if (G.po) {
+                G.snapshot(side);
+                G.snapshot(1 - side);
+            }
+            const int np = G.rowsDecode(side, D.rows + (size_t)slot0 * D.n_rows * 8);
+            aiGetAction(G, ai2, 1 - side);
+            G.rowsIssue(side, np, 1);
+            G.issuePlayer(1 - side, 10, true);
+        } else if (gtype == GT_SELFPLAY) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
             G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1);
             PHASE(1);
@@ -2196,6 +2306,27 @@ size_t ldsBytes(int HW, int W, int CAP, int po) {
     return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) +
            (po ? 4 * (size_t)HW : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
+}
+// int32 copy of a uint8 mask buffer (the Java int[][][][] layout), 16 mask bytes per thread
+__global__ __launch_bounds__(256) void k_widen(const uint8_t* __restrict__ in, int32_t* __restrict__ out, size_t n) {
+    const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;
+    if (i + 16 <= n) {
+        const uint4 v = *(const uint4*)(in + i);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            *(int4*)(out + i + 4 * q) = make_int4((int)(w[q] & 0xFF), (int)((w[q] >> 8) & 0xFF), (int)((w[q] >> 16) & 0xFF),
+                                                  (int)(w[q] >> 24));
+    } else {
+        for (size_t k = i; k < n; k++) out[k] = in[k];
+    }
+}
+hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (((uintptr_t)in & 15) || ((uintptr_t)out & 15)) return hipErrorInvalidValue;
+    const size_t threads = (n + 15) / 16;
+    hipLaunchKernelGGL(k_widen, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, in, out, n);
+    return hipGetLastError();
 }
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
     const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);

@@ -160,18 +160,32 @@ class JNIGridnetVecClient:
         return self._responses()
 
     def gameStep(self, action, players=None):
-        """gameStep(int[][][] action, int[] players) (:213-297); action = [slots][H*W][7]."""
+        """gameStep(int[][][] action, int[] players) (:213-297).
+
+        action is either the Java layout [slots][n_rows][8] (rows [pos, 7 components], any order,
+        duplicates allowed: PlayerAction.fromVectorAction list semantics) or the grid layout
+        [slots][H*W][7] (row r = cell r, ascending — what MicroRTS-Py sends)."""
+        h = self._h
         if action is None:  # bot-only clients take no actions (JNIGridnetVecClient.java:214-216)
-            action = np.zeros((self._h.S, self._h.H * self._h.W, 7), np.int32)
-        a = np.ascontiguousarray(action, np.int32).reshape(self._h.S, self._h.H * self._h.W, 7)
+            action = np.zeros((h.S, h.H * h.W, 7), np.int32)
+        a = np.ascontiguousarray(action, np.int32)
         p = None if players is None else np.ascontiguousarray(players, np.int32)
-        _lib.check(self._h.L.mrts_step(self._h.h, a.ctypes.data_as(ctypes.c_void_p),
-                                       None if p is None else p.ctypes.data_as(ctypes.c_void_p), ctypes.byref(self._resp)))
+        pp = None if p is None else p.ctypes.data_as(ctypes.c_void_p)
+        if a.ndim == 3 and a.shape[0] == h.S and a.shape[2] == 8:
+            _lib.check(h.L.mrts_step_rows(h.h, a.ctypes.data_as(ctypes.c_void_p), a.shape[1], pp, ctypes.byref(self._resp)))
+        else:
+            a = a.reshape(h.S, h.H * h.W, 7)
+            _lib.check(h.L.mrts_step(h.h, a.ctypes.data_as(ctypes.c_void_p), pp, ctypes.byref(self._resp)))
         return self._responses()
 
-    def getMasks(self, player=0):
-        """getMasks(int player) (:307-316) → uint8 [slots][H][W][79]."""
+    def getMasks(self, player=0, dtype=np.uint8):
+        """getMasks(int player) (:307-316) → [slots][H][W][79]; dtype np.int32 gives the Java int[][][][]
+        element type."""
         h = self._h
+        if np.dtype(dtype) == np.int32:
+            m = np.empty((h.S, h.H, h.W, h.K), np.int32)
+            _lib.check(h.L.mrts_get_masks_i32(h.h, player, m.ctypes.data_as(ctypes.c_void_p)))
+            return m
         m = np.empty((h.S, h.H, h.W, h.K), np.uint8)
         _lib.check(h.L.mrts_get_masks(h.h, player, m.ctypes.data_as(ctypes.c_void_p)))
         return m
@@ -251,6 +265,16 @@ class DeviceVecEnv:
         a = self.actions if actions is None else actions
         _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self.reward),
                                      self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
+
+    def step_rows(self, rows, stream=None):
+        """gameStep with Java rows: int32 [slots][n_rows][8] on this device (any order, duplicates ok)."""
+        h = self._h
+        assert rows.dtype == self.torch.int32 and rows.is_contiguous() and rows.dim() == 3 and rows.shape[2] == 8
+        assert rows.shape[0] == h.S and rows.device == self.device
+        _lib.check(h.L.mrts_step_rows_dev(h.h, self._p(rows), rows.shape[1], self._p(self.players), self._p(self.obs),
+                                          self._p(self.reward), self._p(self.done),
+                                          self._p(self.masks) if self.masks is not None else None, self.mask_player,
+                                          self._s(stream)))
 
     def get_masks(self, out=None, stream=None):
         h = self._h

@@ -183,12 +183,23 @@ struct VecClient {
         for (size_t j = 0; j < bots.size(); j++) bots[j]->reset(players ? players[nsp + (int)j] : 0);
         std::fill(envSteps.begin(), envSteps.end(), 0);
     }
-    // gameStep (:213-297)
+    // gameStep (:213-297) with the grid layout [slot][HW][7] (row r = cell r, ascending)
     void step(const int32_t* actions, const int32_t* players) {
         const size_t asz = (size_t)world->H * world->W * 7;
+        stepWith([&](Env& e, int s) { return e.rowsFromGrid(actions + (size_t)s * asz); }, players);
+    }
+    // gameStep with the Java layout: action[slot] = n_rows rows [pos, 7 comps], any order, duplicates
+    void stepRows(const int32_t* rows, int nrows, const int32_t* players) {
+        stepWith([&](Env&, int s) {
+            const int32_t* r = rows + (size_t)s * nrows * 8;
+            return std::vector<int>(r, r + (size_t)nrows * 8);
+        }, players);
+    }
+    template <class RowsOf>
+    void stepWith(RowsOf rowsOf, const int32_t* players) {
         for (size_t i = 0; i < selfPlay.size(); i++) {
             Env& e = *selfPlay[i];
-            e.stepSelfPlay(e.rowsFromGrid(actions + (2 * i) * asz), e.rowsFromGrid(actions + (2 * i + 1) * asz));
+            e.stepSelfPlay(rowsOf(e, (int)(2 * i)), rowsOf(e, (int)(2 * i + 1)));
             envSteps[2 * i] += 1;
             envSteps[2 * i + 1] += 1;
             if (e.resp[0].done || envSteps[2 * i] >= maxSteps) {
@@ -211,7 +222,7 @@ struct VecClient {
             Env& e = *bots[j];
             int pl = players ? players[s] : 0;
             envSteps[(size_t)s] += 1;
-            e.stepBot(e.rowsFromGrid(actions + (size_t)s * asz), pl);
+            e.stepBot(rowsOf(e, s), pl);
             if (e.resp[0].done || envSteps[(size_t)s] >= maxSteps) {
                 double tr = e.resp[0].reward;
                 uint8_t td = e.resp[0].done;
@@ -359,6 +370,20 @@ int oref_step(void* h, const int32_t* actions, const int32_t* players, int32_t* 
     try {
         auto v = (VecClient*)h;
         v->step(actions, players);
+        v->collect(obs, reward, done);
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -22;
+    }
+}
+
+// gameStep(int[][][] action, players) with Java rows: rows = [slots][n_rows][8]
+int oref_step_rows(void* h, const int32_t* rows, int n_rows, const int32_t* players, int32_t* obs, double* reward,
+                   uint8_t* done) {
+    try {
+        auto v = (VecClient*)h;
+        v->stepRows(rows, n_rows, players);
         v->collect(obs, reward, done);
         return 0;
     } catch (std::exception& e) {

@@ -35,6 +35,7 @@ def load():
         L.oref_dims.argtypes = [P, P, P, P, P, P]
         L.oref_reset.argtypes = [P, P, P, P, P]
         L.oref_step.argtypes = [P, P, P, P, P, P]
+        L.oref_step_rows.argtypes = [P, P, I, P, P, P, P]
         L.oref_get_masks.argtypes = [P, I, P]
         L.oref_dump_state.argtypes = [P, I, P, I]
         L.oref_env_steps.argtypes = [P, I]
@@ -90,6 +91,15 @@ class OracleVecClient:
         a = np.ascontiguousarray(actions, dtype=np.int32).reshape(self.S, self.H * self.W, 7)
         p = np.asarray(players, np.int32) if players is not None else None
         self._chk(self.L.oref_step(self.h, _ptr(a), _ptr(p), _ptr(self.obs), _ptr(self.reward), _ptr(self.done)))
+        return self.obs.copy(), self.reward.copy(), self.done.copy()
+
+    def step_rows(self, rows, players=None):
+        """gameStep with Java rows [slots][n_rows][8] (PlayerAction.fromVectorAction list semantics)."""
+        r = np.ascontiguousarray(rows, dtype=np.int32)
+        assert r.ndim == 3 and r.shape[0] == self.S and r.shape[2] == 8
+        p = np.asarray(players, np.int32) if players is not None else None
+        self._chk(self.L.oref_step_rows(self.h, _ptr(r), r.shape[1], _ptr(p), _ptr(self.obs), _ptr(self.reward),
+                                        _ptr(self.done)))
         return self.obs.copy(), self.reward.copy(), self.done.copy()
 
     def get_masks(self, player=0):

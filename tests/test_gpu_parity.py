@@ -33,7 +33,12 @@ def _compare_step(env, ref, step, dump_every, tag=""):
     if dump_every and step % dump_every == 0:
         for s in range(ref.S):
             a, b = env.dump_state(s), ref.dump(s)
-            assert np.array_equal(a, b), f"{tag} state mismatch slot {s} step {step}:\n gpu {a[:60]}\n ref {b[:60]}"
+            if not np.array_equal(a, b):
+                n = min(len(a), len(b))
+                i = int(np.argmax(a[:n] != b[:n])) if (a[:n] != b[:n]).any() else n
+                raise AssertionError(f"{tag} state mismatch slot {s} step {step} at word {i} (len {len(a)} vs {len(b)}):"
+                                     f"\n gpu {a[max(0, i - 14):i + 14]}\n ref {b[max(0, i - 14):i + 14]}\n gpu {a.tolist()}"
+                                     f"\n ref {b.tolist()}")
 
 
 def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, policy="masked", dump_every=10, seed=3,
@@ -263,3 +268,125 @@ def test_delta_masks_and_source_policy_match_full(mp, po, n_bot):
     assert torch.equal(a.obs, b.obs)
     a.close()
     b.close()
+
+
+def _java_rows(rng, acts, mode):
+    """Java-layout rows [slots][n][8] from grid actions [slots][HW][7]: shuffled order, duplicate rows
+    for the same cell (with different actions), out-of-map positions."""
+    S, HW, _ = acts.shape
+    rows = []
+    for s in range(S):
+        r = np.concatenate([np.arange(HW, dtype=np.int32)[:, None], acts[s]], axis=1)
+        if mode != "ascending":
+            dup = r[rng.integers(0, HW, HW // 4)].copy()
+            dup[:, 1:] = np.stack([rng.integers(0, 6, len(dup)), rng.integers(0, 4, len(dup)), rng.integers(0, 4, len(dup)),
+                                   rng.integers(0, 4, len(dup)), rng.integers(0, 4, len(dup)), rng.integers(0, 7, len(dup)),
+                                   rng.integers(0, 49, len(dup))], axis=1)
+            junk = np.zeros((4, 8), np.int32)
+            junk[:, 0] = [-1, HW, HW + 7, -HW]
+            r = np.concatenate([r, dup, junk])
+            r = r[rng.permutation(len(r))]
+        rows.append(r)
+    return np.ascontiguousarray(np.stack(rows), np.int32)
+
+
+@pytest.mark.parametrize("mp,n_sp,n_bot,po,crs,mode", [
+    ("maps/8x8/basesWorkers8x8.xml", 8, 0, False, 1, "ascending"),
+    ("maps/8x8/basesWorkers8x8.xml", 8, 0, False, 1, "java"),
+    ("maps/16x16/basesWorkers16x16.xml", 4, 4, False, 3, "java"),
+    ("maps/10x10/basesWorkers10x10.xml", 4, 3, True, 2, "java"),
+    ("maps/4x4/base4x4.xml", 6, 2, False, 1, "java"),
+])
+def test_java_rows_layout(mp, n_sp, n_bot, po, crs, mode):
+    """mrts_step_rows (Java int[][][] rows: any order, duplicate rows, off-map positions) vs the oracle
+    running PlayerAction.fromVectorAction over the same row lists; rows in ascending cell order must
+    also equal the grid path."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv, JNIGridnetVecClient, UnitTypeTable
+
+    maps = [mp] * (n_sp + n_bot)
+    bots = ["RandomBiasedAI"] * n_bot if n_bot else None
+    kinds = [1] * n_bot if n_bot else None
+    env = DeviceVecEnv(n_sp, n_bot, 120, maps, utt=UnitTypeTable(1, crs), seed=4, partial_obs=po, ai2s=bots)
+    ref = oracle_py.OracleVecClient(n_sp, n_bot, 120, maps, crs=crs, seed=4, partial_obs=po, bot_kinds=kinds)
+    grid = DeviceVecEnv(n_sp, n_bot, 120, maps, utt=UnitTypeTable(1, crs), seed=4, partial_obs=po, ai2s=bots) \
+        if mode == "ascending" else None
+    env.reset()
+    ref.reset()
+    if grid is not None:
+        grid.reset()
+    rng = np.random.default_rng(8)
+    S, HW = ref.S, ref.H * ref.W
+    for step in range(150):
+        m = ref.get_masks(0)
+        env.synchronize()
+        assert np.array_equal(env.masks.cpu().numpy(), m), f"mask mismatch step {step}"
+        acts = np.stack([oracle_py.policy(m[s], SEED, s, step, 0) for s in range(S)])
+        if step % 3 == 1:  # unmasked components: illegal actions, conflicts
+            acts = np.stack([rng.integers(0, 6, (S, HW)), rng.integers(0, 4, (S, HW)), rng.integers(0, 4, (S, HW)),
+                             rng.integers(0, 4, (S, HW)), rng.integers(0, 4, (S, HW)), rng.integers(0, 7, (S, HW)),
+                             rng.integers(0, 49, (S, HW))], axis=-1).astype(np.int32)
+        rows = _java_rows(rng, acts, mode)
+        env.step_rows(torch.as_tensor(rows, device=env.device))
+        ref.step_rows(rows)
+        _compare_step(env, ref, step + 1, 5, f"rows[{mode}]")
+        if grid is not None:
+            grid.step(torch.as_tensor(acts, device=grid.device))
+            grid.synchronize()
+            assert torch.equal(grid.obs, env.obs) and torch.equal(grid.masks, env.masks), f"grid != rows at {step}"
+    assert not env.error_flags().any()
+    env.close()
+    ref.close()
+    if grid is not None:
+        grid.close()
+    # host API: Java rows + int32 masks through the JNIGridnetVecClient mirror
+    cl = JNIGridnetVecClient(n_sp, n_bot, 120, ["WinLossRewardFunction"], "", maps, bots, UnitTypeTable(1, crs), po)
+    ref = oracle_py.OracleVecClient(n_sp, n_bot, 120, maps, crs=crs, seed=0, partial_obs=po, bot_kinds=kinds)
+    cl.reset()
+    ref.reset()
+    for step in range(20):
+        m = ref.get_masks(0)
+        m32 = cl.getMasks(0, dtype=np.int32)
+        assert m32.dtype == np.int32 and np.array_equal(m32, m.astype(np.int32))
+        acts = np.stack([oracle_py.policy(m[s], SEED, s, step, 0) for s in range(S)])
+        rows = _java_rows(rng, acts, mode)
+        r = cl.gameStep(rows)
+        o, rw, d = ref.step_rows(rows)
+        assert np.array_equal(r.observation, o) and np.array_equal(r.reward[:, 0], rw)
+    cl.close()
+    ref.close()
+
+
+@pytest.mark.parametrize("rows", [False, True])
+def test_more_than_64_units(rows):
+    """EightBasesWorkers16x16 starts with 64 units and grows past one wave's worth: exercises the
+    multi-block (nu > 64) decode / issue / ready-list paths, grid and Java-row layouts."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mp = "maps/16x16/EightBasesWorkers16x16.xml"
+    n = 4
+    env = DeviceVecEnv(n, 0, 2000, [mp] * n, seed=2)
+    ref = oracle_py.OracleVecClient(n, 0, 2000, [mp] * n, seed=2)
+    env.reset()
+    ref.reset()
+    rng = np.random.default_rng(1)
+    most = 0
+    for step in range(160):
+        m = ref.get_masks(0)
+        env.synchronize()
+        assert np.array_equal(env.masks.cpu().numpy(), m), f"mask mismatch step {step}"
+        acts = np.stack([oracle_py.policy(m[s], SEED, s, step, 0) for s in range(n)])
+        if rows:
+            r = _java_rows(rng, acts, "java")
+            env.step_rows(torch.as_tensor(r, device=env.device))
+            ref.step_rows(r)
+        else:
+            env.step(torch.as_tensor(acts, device=env.device))
+            ref.step(acts)
+        _compare_step(env, ref, step + 1, 10, "many-units")
+        most = max(most, int(ref.dump(0)[4]))
+    assert most > 64, f"test did not reach > 64 units (max {most})"
+    assert not env.error_flags().any()
+    env.close()
+    ref.close()
