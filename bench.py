@@ -163,6 +163,15 @@ def main():
     contract = S * (rows * 28 + C * HW * 4 + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
     survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16))
     achieved = contract / (kern_ms * 1e-3) / 1e9
+    # roofline.traffic: HBM bytes per k_env launch from the rocprofv3 --pmc passes of this same command
+    # (tools/gpu_profile.sh + tools/summarize_profile.py -> profiles/pmc_latest.json), when they exist
+    traffic, traffic_src = a.pmc_traffic, "--pmc-traffic" if a.pmc_traffic is not None else None
+    pl = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if traffic is None and os.path.exists(pl):
+        pj = json.load(open(pl))
+        if pj.get("mask_mode") == a.mask_mode and pj.get("envs_per_gpu") == E and a.map in (pj.get("workload") or ""):
+            traffic = pj["traffic_bytes_per_launch"]
+            traffic_src = f"profiles/pmc_latest.json ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes)"
     total_games = E * world
     value = total_games * a.steps / t
     out = {
@@ -196,7 +205,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": a.pmc_traffic,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "k_env<MODE_STEP>",
             "alg_bytes_per_launch": contract,
             "alg_bytes_note": f"step contract bytes, {a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "

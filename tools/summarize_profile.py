@@ -53,10 +53,18 @@ def main():
     for k in ("k_env", "k_policy"):
         f, wr = pmc.get((k, "FETCH_SIZE"), float("nan")), pmc.get((k, "WRITE_SIZE"), float("nan"))
         lines.append(f"| {k} | {f:.0f} | {2 * f:.0f} | {wr:.0f} |")
-    if ("k_env", "WRITE_SIZE") in pmc:
-        t = (pmc[("k_env", "FETCH_SIZE")] + pmc[("k_env", "WRITE_SIZE")]) * 1024
-        lines += ["", f"k_env HBM traffic per launch (FETCH + WRITE, uncorrected): {t / 1e6:.1f} MB; "
-                      f"algorithmic bytes per launch (SURVEY §8d): {bench['roofline']['alg_bytes_per_launch'] / 1e6:.1f} MB"]
+    if ("k_env", "WRITE_SIZE") in pmc and ("k_env", "FETCH_SIZE") in pmc:
+        f, wr = pmc[("k_env", "FETCH_SIZE")] * 1024, pmc[("k_env", "WRITE_SIZE")] * 1024
+        t = 2 * f + wr  # MI355X_MICROARCH.md §HBM: FETCH_SIZE x2 on gfx950; WRITE_SIZE as is
+        lines += ["", f"k_env HBM traffic per launch: 2 x FETCH_SIZE + WRITE_SIZE = {t / 1e6:.1f} MB "
+                      f"(uncorrected FETCH + WRITE {(f + wr) / 1e6:.1f} MB; the step's narrow loads are uncalibrated, so "
+                      f"the true value lies between); step-contract algorithmic bytes per launch: "
+                      f"{bench['roofline']['alg_bytes_per_launch'] / 1e6:.1f} MB"]
+        cfg = bench.get("config", {})
+        json.dump({"tag": a.tag, "kernel": "k_env<MODE_STEP>", "traffic_bytes_per_launch": t,
+                   "fetch_size_bytes": f, "write_size_bytes": wr, "workload": cfg.get("workload"),
+                   "mask_mode": cfg.get("mask_mode"), "envs_per_gpu": cfg.get("envs_per_gpu")},
+                  open(os.path.join(dst, "pmc_latest.json"), "w"), indent=1)
     open(os.path.join(dst, f"{a.tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     shutil.copy(os.path.join(a.src, "stats", "run_kernel_stats.csv"), os.path.join(dst, f"{a.tag}_kernel_stats.csv"))
     print("\n".join(lines))
