@@ -34,6 +34,18 @@ typedef struct mrts_env mrts_env;
 
 enum { MRTS_BOT_PASSIVE = 0, MRTS_BOT_RANDOM_BIASED = 1 };
 
+/* reward functions, a_rfs (:106): the classes of src/ai/reward */
+enum {
+    MRTS_RF_WIN_LOSS = 0,            /* WinLossRewardFunction: +1 / -1 at gameover, done = gameover */
+    MRTS_RF_RESOURCE_GATHER = 1,     /* ResourceGatherRewardFunction: +1 per HARVEST / RETURN issued; done = no resources */
+    MRTS_RF_PRODUCE_WORKER = 2,      /* ProduceWorkerRewardFunction */
+    MRTS_RF_PRODUCE_BUILDING = 3,    /* ProduceBuildingRewardFunction (Base, Barracks) */
+    MRTS_RF_ATTACK = 4,              /* AttackRewardFunction */
+    MRTS_RF_PRODUCE_COMBAT_UNIT = 5, /* ProduceCombatUnitRewardFunction (Light, Heavy, Ranged) */
+    MRTS_RF_CLOSER_TO_ENEMY_BASE = 6,/* CloserToEnemyBaseRewardFunction: fp64 sqrt distances */
+    MRTS_RF_CLOSER_TO_ENEMY_UNIT = 7 /* CloserToEnemyUnitRewardFunction (the reference's text is identical to 6) */
+};
+
 /* per-game error flag bits (mrts_error_flags) */
 enum {
     MRTS_ERR_CAPACITY = 1u << 0,      /* unit slots exhausted (no Java equivalent; env must be reset) */
@@ -63,12 +75,16 @@ typedef struct {
                                    handle's previous mask write, only rows that changed are rewritten; the
                                    buffer must not be modified by the caller in between (the Java client
                                    owns and reuses its mask array the same way, JNIGridnetClient.java:211) */
+    const int32_t* reward_kinds;/* a_rfs (:106): MRTS_RF_* in order, n_rewards of them; NULL/0 = {WIN_LOSS}.
+                                   reward / done become [n_slots][n_rewards]; the auto-reset follows done
+                                   of the FIRST function (rs.done[0], :247,272) */
+    int32_t n_rewards;          /* 0..8 */
 } mrts_config;
 
-typedef struct {               /* ai/jni/Responses.java:12-30 (one reward function: WinLoss) */
+typedef struct {               /* ai/jni/Responses.java:12-30 */
     const int32_t* obs;        /* [n_slots][C][H][W] */
-    const double* reward;      /* [n_slots][1] */
-    const uint8_t* done;       /* [n_slots][1] */
+    const double* reward;      /* [n_slots][n_rewards] */
+    const uint8_t* done;       /* [n_slots][n_rewards] */
 } mrts_responses;
 
 /* new JNIGridnetVecClient(...) (:106-142).  Parses the XML maps (PhysicalGameState.java:700-726). */

@@ -7,6 +7,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmrts.so")
 
 MRTS_BOT_PASSIVE, MRTS_BOT_RANDOM_BIASED = 0, 1
+# a_rfs names (src/ai/reward/*.java) -> MRTS_RF_* ids
+REWARD_FUNCTIONS = {"WinLossRewardFunction": 0, "ResourceGatherRewardFunction": 1, "ProduceWorkerRewardFunction": 2,
+                    "ProduceBuildingRewardFunction": 3, "AttackRewardFunction": 4, "ProduceCombatUnitRewardFunction": 5,
+                    "CloserToEnemyBaseRewardFunction": 6, "CloserToEnemyUnitRewardFunction": 7}
 ERR_BITS = {
     1 << 0: "CAPACITY", 1 << 1: "ADDUNIT", 1 << 2: "PRODUCE_TYPE", 1 << 3: "OLDER_CONFLICT",
     1 << 4: "NEG_RESOURCES", 1 << 5: "MOVE_COLLISION",
@@ -35,6 +39,8 @@ class MrtsConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("slot_id_base", ctypes.c_int32),
         ("mask_delta", ctypes.c_int32),
+        ("reward_kinds", ctypes.POINTER(ctypes.c_int32)),
+        ("n_rewards", ctypes.c_int32),
     ]
 
 

@@ -288,6 +288,7 @@ struct mrts_env {
     int32_t* d_rowsStage = nullptr;
     size_t rowsStageInts = 0;
     int32_t* d_masks32 = nullptr;
+    std::vector<int32_t> rewardKinds{RF_WINLOSS};  // a_rfs
     const int32_t* lastPolicyActions = nullptr;
     bool polValid = false;
     int polParity = 0;
@@ -308,6 +309,15 @@ struct mrts_env {
         hstatic.CAP = CAP;
         hstatic.n_games = nGames;
         hstatic.n_sp_games = nSpGames;
+        hstatic.n_rewards = (int32_t)rewardKinds.size();
+        hstatic.reward_need = 0;
+        for (size_t j = 0; j < rewardKinds.size(); j++) {
+            const int k = rewardKinds[j];
+            hstatic.reward_kinds[j] = k;
+            if (k >= RF_RESOURCE_GATHER && k <= RF_PRODUCE_COMBAT_UNIT) hstatic.reward_need |= RN_COUNTS;
+            if (k == RF_RESOURCE_GATHER) hstatic.reward_need |= RN_RESOURCES;
+            if (k == RF_CLOSER_TO_ENEMY_BASE || k == RF_CLOSER_TO_ENEMY_UNIT) hstatic.reward_need |= RN_CLOSER;
+        }
         hstatic.max_steps = maxSteps;
         hstatic.C = C;
         hstatic.partial_obs = partialObs;
@@ -375,6 +385,13 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         env->nGames = env->nSpGames + cfg->n_bot_envs;
         env->slotIdBase = (uint32_t)cfg->slot_id_base;
         env->maskDelta = cfg->mask_delta;
+        if (cfg->n_rewards < 0 || cfg->n_rewards > MAX_REWARDS) throw Fail{-EINVAL, "n_rewards must be 0..8"};
+        if (cfg->n_rewards > 0) {
+            if (!cfg->reward_kinds) throw Fail{-EINVAL, "reward_kinds is null"};
+            env->rewardKinds.assign(cfg->reward_kinds, cfg->reward_kinds + cfg->n_rewards);
+            for (int k : env->rewardKinds)
+                if (k < 0 || k >= RF_COUNT) throw Fail{-EINVAL, "unknown reward function"};
+        }
         if (cfg->ai1_kinds && cfg->n_selfplay_slots) throw Fail{-EINVAL, "the bot-only client has no self-play slots"};
         env->gameKindHost.assign((size_t)env->nGames, 0);  // self-play = 0
         for (int j = 0; j < cfg->n_bot_envs; j++) {
@@ -462,12 +479,13 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         HIPCHK(hipMalloc(&env->d_actions, S * env->HW * 7 * 4));
         HIPCHK(hipMalloc(&env->d_players, S * 4));
         HIPCHK(hipMalloc(&env->d_obs, S * env->C * env->HW * 4));
-        HIPCHK(hipMalloc(&env->d_reward, S * 8));
-        HIPCHK(hipMalloc(&env->d_done, S));
+        const size_t R = env->rewardKinds.size();
+        HIPCHK(hipMalloc(&env->d_reward, S * R * 8));
+        HIPCHK(hipMalloc(&env->d_done, S * R));
         HIPCHK(hipMalloc(&env->d_masks, S * env->HW * env->K));
         HIPCHK(hipHostMalloc(&env->h_obs, S * env->C * env->HW * 4, hipHostMallocDefault));
-        HIPCHK(hipHostMalloc(&env->h_reward, S * 8, hipHostMallocDefault));
-        HIPCHK(hipHostMalloc(&env->h_done, S, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&env->h_reward, S * R * 8, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&env->h_done, S * R, hipHostMallocDefault));
         HIPCHK(hipMemset(env->d_players, 0, S * 4));
         // static kernel parameters → device buffer
         env->buildStatic();
@@ -657,8 +675,9 @@ int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_sou
 static void fillResponses(mrts_env* env, mrts_responses* out) {
     const size_t S = (size_t)env->nSlots;
     HIPCHK(hipMemcpyAsync(env->h_obs, env->d_obs, S * env->C * env->HW * 4, hipMemcpyDeviceToHost, env->stream));
-    HIPCHK(hipMemcpyAsync(env->h_reward, env->d_reward, S * 8, hipMemcpyDeviceToHost, env->stream));
-    HIPCHK(hipMemcpyAsync(env->h_done, env->d_done, S, hipMemcpyDeviceToHost, env->stream));
+    const size_t R = env->rewardKinds.size();
+    HIPCHK(hipMemcpyAsync(env->h_reward, env->d_reward, S * R * 8, hipMemcpyDeviceToHost, env->stream));
+    HIPCHK(hipMemcpyAsync(env->h_done, env->d_done, S * R, hipMemcpyDeviceToHost, env->stream));
     HIPCHK(hipStreamSynchronize(env->stream));
     if (out) {
         out->obs = env->h_obs;

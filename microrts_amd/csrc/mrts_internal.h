@@ -6,6 +6,10 @@ namespace mrts {
 
 constexpr int MAX_TYPES = 8;
 constexpr int MAX_PRODUCES = 4;
+constexpr int MAX_REWARDS = 8;
+// reward functions (src/ai/reward/*.java), ids = include/mrts.h MRTS_RF_*
+enum { RF_WINLOSS = 0, RF_RESOURCE_GATHER = 1, RF_PRODUCE_WORKER = 2, RF_PRODUCE_BUILDING = 3, RF_ATTACK = 4,
+       RF_PRODUCE_COMBAT_UNIT = 5, RF_CLOSER_TO_ENEMY_BASE = 6, RF_CLOSER_TO_ENEMY_UNIT = 7, RF_COUNT = 8 };
 
 // UnitTypeTable constants (reference src/rts/units/UnitTypeTable.java:104-289), passed by value as
 // kernel arguments so that handles with different tables never share device globals.
@@ -71,14 +75,18 @@ struct KStatic {
     const int32_t* tmpl;           // template blob
     const int32_t* tmpl_off;       // [n_games] word offset of each game's template
     const int32_t* game_kind;      // [n_games]: type | ai1 << 4 | ai2 << 8 (see mrts_kernels.hip)
+    int32_t n_rewards;             // reward functions per slot (a_rfs), 1..MAX_REWARDS
+    int32_t reward_kinds[MAX_REWARDS];  // MRTS_RF_* in a_rfs order; reward / done are [n_slots][n_rewards]
+    uint32_t reward_need;          // RN_* bits: which per-step bookkeeping the kinds need
 };
+enum : uint32_t { RN_COUNTS = 1, RN_CLOSER = 2, RN_RESOURCES = 4 };
 // Per-call buffers (kernel arguments by value)
 struct KDyn {
     const int32_t* actions;        // [n_slots][HW][7]
     const int32_t* players;        // [n_slots] or null
     int32_t* obs;                  // [n_slots][C][HW] or null
-    double* reward;                // [n_slots] or null
-    uint8_t* done;                 // [n_slots] or null
+    double* reward;                // [n_slots][n_rewards] or null
+    uint8_t* done;                 // [n_slots][n_rewards] or null
     uint8_t* masks;                // [n_slots][HW][K] or null
     uint32_t* source;              // [n_slots][maskWords(HW)] mask slot 0 as bits, or null
     int32_t mask_player;           // player whose masks bot-env slots receive

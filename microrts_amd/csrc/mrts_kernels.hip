@@ -52,6 +52,13 @@ __device__ unsigned long long g_span[2 * PH_GAMES];    // last launch: [game] st
     } while (0)
 #endif
 enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2 };  // game_kind & 15
+// per-player counters of this step's issued pairs, as the TraceEntry holds them (after issueSafe's
+// legality rewrite, before issue()'s conflict cancellations): HARVEST, RETURN, ATTACK, and PRODUCE
+// of a Worker / a Base or Barracks / a Light, Heavy or Ranged
+enum { RC_HARVEST = 0, RC_RETURN = 1, RC_ATTACK = 2, RC_PROD_WORKER = 3, RC_PROD_BUILDING = 4, RC_PROD_COMBAT = 5, RC_N = 6 };
+DEV int prodCategory(int ut) {  // type ids: Resource 0, Base 1, Barracks 2, Worker 3, Light 4, Heavy 5, Ranged 6
+    return ut == 3 ? RC_PROD_WORKER : (ut == 1 || ut == 2) ? RC_PROD_BUILDING : (ut >= 4 && ut <= 6) ? RC_PROD_COMBAT : -1;
+}
 enum { GK_PASSIVE = 0, GK_RANDOM_BIASED = 1 };                    // AI kinds (bits 4-7 ai1, 8-11 ai2)
 enum : uint32_t {
     E_CAPACITY = 1u << 0, E_ADDUNIT = 1u << 1, E_PRODUCE_TYPE = 1u << 2, E_OLDER = 1u << 3,
@@ -149,6 +156,7 @@ struct Game {
     uint32_t* scell; // PO: last snapshot unit per cell (slot+1, 0 = none)
     int32_t* rseq;   // ready-list scratch (64)
     uint32_t* mprev; // previous mask row sets, [2][maskWords(HW)] (delta mask writes)
+    int32_t* rwc;    // reward counters [player][RC_*] of the pairs issued this step
     int16_t* hp;
     int16_t* res;
     int16_t* par;    // UnitAction.parameter (direction / NONE duration)
@@ -168,6 +176,10 @@ struct Game {
     bool ixValid;
     bool anyMP;
     uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
+    int curP;              // player whose pa is being issued
+    // CloserToEnemyBase/Unit: each player's first Base before the step (x | y << 8, -1 = none) and
+    // the smallest squared distance from the OTHER player's mobile units to it, before the step
+    int basePos0, basePos1, oldSq0, oldSq1;
     int readySlot;         // per lane: the unit slot of ready item lane_id() (-1 outside cycle)
     int maxProd0, maxProd1, sumProd0, sumProd1;
     uint32_t err;
@@ -184,6 +196,7 @@ struct Game {
         bits = (uint32_t*)q; q += 4 * ((HW + 2 * W + 31) / 32);
         rseq = (int32_t*)q; q += 4 * 64;
         mprev = (uint32_t*)q; q += 8 * maskWords(HW);
+        rwc = (int32_t*)q; q += 4 * 16;
         scell = (uint32_t*)q; q += po ? 4 * HW : 0;
         hp = (int16_t*)q; q += 2 * CAP;
         res = (int16_t*)q; q += 2 * CAP;
@@ -195,6 +208,9 @@ struct Game {
         ixValid = false;
         killedLanes = 0;
         readySlot = -1;
+        curP = 0;
+        basePos0 = basePos1 = -1;
+        oldSq0 = oldSq1 = INF;
     }
     DEV int pres(int p) const { return p == 0 ? pres0 : pres1; }
     DEV void addPres(int p, int v) {
@@ -503,6 +519,7 @@ struct Game {
     }
     // issueSafe(pa) for the pairs of rowsDecode + fillWithNones(gs, p, fillDur) (PlayerAction.java:217-235)
     DEV void rowsIssue(int p, int npairs, int fillDur) {
+        curP = p;
         const uint32_t* pairs = D.pairs + (size_t)g * D.n_rows * 2;
         for (int b0 = 0; b0 < npairs; b0 += 64) {
             const int k = b0 + lane_id();
@@ -787,6 +804,8 @@ struct Game {
                 any |= ballot(o < nu && conflicts(o, ntgt, nProduce, ncost, pl)) != 0;
             }
             int lastSeq = -1;
+            bool orig = true;  // p still names pa's own Pair (GameState.java:296 replaces only the loop variable)
+            const int tIn = t, utIn = ut;
             while (any) {  // rare: resolve the conflicting assignments in insertion order
                 int best = INF;
                 for (int o = lane_id(); o < nu; o += 64)
@@ -830,9 +849,17 @@ struct Game {
                         t = T_NONE;
                         prm = md;
                         tx = ty = ut = 0;
+                        orig = false;
                     }
                     wsync();
                 } else {  // older assignment: only the new one is cancelled (:298-317)
+                    // p.m_b = NONE mutates pa's own Pair unless a cancel already replaced p: the
+                    // TraceEntry (pa.clone() after issueSafe) then records NONE, not the PRODUCE
+                    if (orig && tIn == T_PRODUCE && (P.reward_need & RN_COUNTS) && lane_id() == 0) {
+                        const int pc = prodCategory(utIn);
+                        if (pc >= 0) rwc[curP * RC_N + pc] -= 1;
+                    }
+                    orig = false;
                     err |= E_OLDER;
                     t = T_NONE;
                     prm = -1;
@@ -902,6 +929,15 @@ struct Game {
     DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut, bool checkDup = false) {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
+        if (P.reward_need & RN_COUNTS) {  // the pairs as the TraceEntry records them (legality applied)
+            const int pc = np ? prodCategory(ut) : -1;
+            auto cnt = [](bool b) { return (int)__popcll(ballot(b)); };
+            const int c[RC_N] = {cnt(act && t == T_HARVEST), cnt(act && t == T_RETURN), cnt(act && t == T_ATTACK),
+                                 cnt(pc == RC_PROD_WORKER), cnt(pc == RC_PROD_BUILDING), cnt(pc == RC_PROD_COMBAT)};
+            if (lane_id() == 0)
+#pragma unroll
+                for (int k = 0; k < RC_N; k++) rwc[curP * RC_N + k] += c[k];
+        }
         const uint64_t mpm = ballot(mp);
         bool conf = false;
         if (checkDup) {
@@ -987,6 +1023,7 @@ struct Game {
     // (rts/PlayerAction.java:328-346) in list order; AI pa (RandomBiasedAI / PassiveAI) = its units
     // in list order (listOrder).
     DEV void issuePlayer(int p, int fillDur, bool listOrder) {
+        curP = p;
         if (!listOrder && nu <= 64) {
             const int o = lane_id();
             uint32_t cu = 0;
@@ -1495,6 +1532,93 @@ struct Game {
         placeUnits();
     }
 
+    // ------------------------------------------------------------------ reward functions
+    // CloserToEnemyBaseRewardFunction.java:22-66 (and the identical CloserToEnemyUnit text): the enemy
+    // Base is the first unit of minplayer named "Base" in the pre-cycle list; distances are from
+    // maxplayer's Light/Heavy/Ranged/Worker units.  Squared distances are exact integers and sqrt is
+    // monotone, so min(sqrt) = sqrt(min).
+    static DEV bool mobileType(int t) { return t == 3 || t == 4 || t == 5 || t == 6; }
+    DEV void closerBefore() {
+        int b0 = -1, b1 = -1;
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            const uint32_t c = o < nu ? uc[o] : UC_DEAD;
+            const bool base = !(c & UC_DEAD) && utyp(c) == 1;
+            const uint64_t m0 = ballot(base && uplay(c) == 0), m1 = ballot(base && uplay(c) == 1);
+            if (b0 < 0 && m0) b0 = o0 + __builtin_ctzll(m0);
+            if (b1 < 0 && m1) b1 = o0 + __builtin_ctzll(m1);
+        }
+        basePos0 = b0 >= 0 ? (int)(uniu(uc[b0]) & 0xFFFFu) : -1;
+        basePos1 = b1 >= 0 ? (int)(uniu(uc[b1]) & 0xFFFFu) : -1;
+        closerMin(oldSq0, oldSq1);
+    }
+    // smallest squared distance of player p's mobile units to the other player's base (INF if none)
+    DEV void closerMin(int& sq0, int& sq1) {
+        int m0 = INF, m1 = INF;
+        for (int o = lane_id(); o < nu; o += 64) {
+            const uint32_t c = uc[o];
+            if ((c & UC_DEAD) || !mobileType(utyp(c))) continue;
+            const int pl = uplay(c);
+            const int bp = pl == 0 ? basePos1 : basePos0;
+            if (pl < 0 || bp < 0) continue;
+            const int dx = (bp & 0xFF) - ux(c), dy = (bp >> 8) - uy(c), d = dx * dx + dy * dy;
+            if (pl == 0) m0 = min(m0, d);
+            else m1 = min(m1, d);
+        }
+        sq0 = wave_min(m0);
+        sq1 = wave_min(m1);
+    }
+    static DEV double closerDist(int sq) { return sq == INF ? 2000000000.0 : __builtin_sqrt((double)sq); }
+    // computeReward of every a_rfs entry for the game's external slots (slot0 + i is player pl(i)),
+    // written to reward / done [slot][R]; returns done of a_rfs[0] (drives the auto-reset,
+    // JNIGridnetVecClient.java:247,272).  WinLoss: WinLossRewardFunction.java:16-24; ResourceGather:
+    // ResourceGatherRewardFunction.java:22-44; ProduceWorker / ProduceBuilding / ProduceCombatUnit:
+    // Produce*RewardFunction.java:22-33; Attack: AttackRewardFunction.java:22-38 (a legal attack always
+    // targets a minplayer unit of the pre-cycle pgs).  Constants are float 1.
+    DEV bool writeRewards(int slot0, int nslots, int pl0, int pl1, bool gameover, int winner) {
+        const int R = P.n_rewards;
+        int newSq0 = INF, newSq1 = INF;
+        if (P.reward_need & RN_CLOSER) closerMin(newSq0, newSq1);
+        bool resLeft = false;
+        if (P.reward_need & RN_RESOURCES)
+            for (int o0 = 0; o0 < nu; o0 += 64) {
+                const int o = o0 + lane_id();
+                resLeft |= ballot(o < nu && !(uc[o] & UC_DEAD) && utyp(uc[o]) == 0 && res[o] > 0) != 0;
+            }
+        const int k0 = P.reward_kinds[0];
+        const bool done0 = k0 == RF_WINLOSS ? gameover : (k0 == RF_RESOURCE_GATHER ? !resLeft : false);
+        const int L = lane_id();
+        if (L < nslots * R && (D.reward || D.done)) {
+            const int i = L / R, j = L - i * R;
+            const int p = i ? pl1 : pl0;
+            const int kind = P.reward_kinds[j];
+            double r = 0.0;
+            bool d = false;
+            switch (kind) {
+                case RF_WINLOSS:
+                    d = gameover;
+                    r = gameover ? (winner == p ? 1.0 : -1.0) : 0.0;
+                    break;
+                case RF_RESOURCE_GATHER:
+                    r = (double)(rwc[p * RC_N + RC_HARVEST] + rwc[p * RC_N + RC_RETURN]);
+                    d = !resLeft;
+                    break;
+                case RF_PRODUCE_WORKER: r = (double)rwc[p * RC_N + RC_PROD_WORKER]; break;
+                case RF_PRODUCE_BUILDING: r = (double)rwc[p * RC_N + RC_PROD_BUILDING]; break;
+                case RF_PRODUCE_COMBAT_UNIT: r = (double)rwc[p * RC_N + RC_PROD_COMBAT]; break;
+                case RF_ATTACK: r = (double)rwc[p * RC_N + RC_ATTACK]; break;
+                case RF_CLOSER_TO_ENEMY_BASE:
+                case RF_CLOSER_TO_ENEMY_UNIT:
+                    if ((p == 0 ? basePos1 : basePos0) >= 0)
+                        r = closerDist(p == 0 ? oldSq0 : oldSq1) - closerDist(p == 0 ? newSq0 : newSq1);
+                    break;
+            }
+            if (D.reward) D.reward[(size_t)(slot0 + i) * R + j] = r;
+            if (D.done) D.done[(size_t)(slot0 + i) * R + j] = d ? 1 : 0;
+        }
+        return done0;
+    }
+
     // ------------------------------------------------------------------ observation
     // GameState.getVectorObservation (rts/GameState.java:922-968): 6 planes [C][H][W] int32.
     // Lane = 4 consecutive cells -> one dwordx4 store per plane.
@@ -1907,9 +2031,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         G.initCells();
         G.resetFromTemplate();
         if (D.mask_delta && D.masks) G.loadPrev();
-        if (lane_id() < nslots) {
-            if (D.reward) D.reward[slot0 + lane_id()] = 0.0;
-            if (D.done) D.done[slot0 + lane_id()] = 0;
+        for (int k = lane_id(); k < nslots * P.n_rewards; k += 64) {
+            if (D.reward) D.reward[(size_t)slot0 * P.n_rewards + k] = 0.0;
+            if (D.done) D.done[(size_t)slot0 * P.n_rewards + k] = 0;
         }
     } else {
         G.load(D.mask_delta && D.masks);
@@ -1919,6 +2043,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
+        if (P.reward_need & RN_COUNTS)
+            if (lane_id() < 2 * RC_N) G.rwc[lane_id()] = 0;
+        if (P.reward_need & RN_CLOSER) G.closerBefore();
         if (D.rows && gtype == GT_SELFPLAY) {
             for (int p = 0; p < 2; p++) {
                 if (G.po) G.snapshot(p);
@@ -1970,16 +2097,12 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         bool gameover;
         int winner;
         G.outcome(gameover, winner);
-        // WinLossRewardFunction (ai/reward/WinLossRewardFunction.java:16-24) + VecClient auto-reset
-        // keeping the terminal reward/done (tests/JNIGridnetVecClient.java:214-287)
+        // reward functions + VecClient auto-reset on done[0] or max steps, keeping the terminal
+        // reward/done and forcing done[0] (tests/JNIGridnetVecClient.java:214-287)
         G.steps++;
-        const bool reset = gameover || G.steps >= P.max_steps;
-        if (lane_id() < nslots) {
-            const int slot = slot0 + lane_id();
-            const int maxp = selfplay ? lane_id() : side;
-            if (D.reward) D.reward[slot] = gameover ? (winner == maxp ? 1.0 : -1.0) : 0.0;
-            if (D.done) D.done[slot] = (gameover || reset) ? 1 : 0;
-        }
+        const bool done0 = G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner);
+        const bool reset = done0 || G.steps >= P.max_steps;
+        if (reset && D.done && lane_id() < nslots) D.done[(size_t)(slot0 + lane_id()) * P.n_rewards] = 1;
         if (reset) {
             G.resetFromTemplate();
             if (G.po) G.clearSnap();
@@ -2303,7 +2426,7 @@ hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts then [n] 
 }
 #endif
 size_t ldsBytes(int HW, int W, int CAP, int po) {
-    return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) +
+    return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 +
            (po ? 4 * (size_t)HW : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
 }

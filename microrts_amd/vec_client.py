@@ -57,9 +57,19 @@ def _bot_kind(ai):
 
 
 def _check_rfs(rfs):
-    names = [r if isinstance(r, str) else type(r).__name__ for r in (rfs or ["WinLossRewardFunction"])]
-    if names != ["WinLossRewardFunction"]:
-        raise NotImplementedError("only [WinLossRewardFunction] is implemented on the GPU path")
+    """a_rfs (RewardFunctionInterface[], :106) -> MRTS_RF_* ids: class names or instances/classes with
+    those names (src/ai/reward/*.java); None = [WinLossRewardFunction]."""
+    out = []
+    for r in (rfs or ["WinLossRewardFunction"]):
+        name = r if isinstance(r, str) else (r.__name__ if isinstance(r, type) else type(r).__name__)
+        name = name.rsplit(".", 1)[-1]
+        if name not in _lib.REWARD_FUNCTIONS:
+            raise NotImplementedError(f"reward function {name!r} is not implemented on the GPU path "
+                                      f"(available: {sorted(_lib.REWARD_FUNCTIONS)})")
+        out.append(_lib.REWARD_FUNCTIONS[name])
+    if len(out) > 8:
+        raise ValueError("at most 8 reward functions")
+    return out
 
 
 def _kinds(ais, n):
@@ -70,18 +80,21 @@ def _kinds(ais, n):
 
 class _Handle:
     def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base,
-                 ai1s=None, mask_delta=False):
+                 ai1s=None, mask_delta=False, rewards=None):
         L = _lib.load()
         self.L = L
         self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
         self._kinds = _kinds(ai2s, n_bot)
         self._ai1 = _kinds(ai1s, n_bot) if ai1s is not None else None
         P32 = ctypes.POINTER(ctypes.c_int32)
+        self.rewards = list(rewards) if rewards else [0]
+        self._rk = (ctypes.c_int32 * len(self.rewards))(*self.rewards)
+        self.R = len(self.rewards)
         cfg = _lib.MrtsConfig(n_selfplay, n_bot, max_steps, int(bool(partial_obs)), utt.version, utt.crs,
                               ctypes.cast(self._kinds, P32),
                               ctypes.cast(self._ai1, P32) if self._ai1 is not None else None,
                               ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base,
-                              int(bool(mask_delta)))
+                              int(bool(mask_delta)), ctypes.cast(self._rk, P32), self.R)
         h = ctypes.c_void_p()
         _lib.check(L.mrts_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -123,11 +136,11 @@ class JNIGridnetVecClient:
 
     def __init__(self, a_num_selfplayenvs, a_num_envs, a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai2s=None,
                  a_utt=None, partial_obs=False, device=0, seed=0, slot_id_base=0, _ai1s=None):
-        _check_rfs(a_rfs)
+        rewards = _check_rfs(a_rfs)
         utt = a_utt or UnitTypeTable()
         paths = [_resolve(a_micrortsPath, p) for p in a_mapPaths]
         self._h = _Handle(a_num_selfplayenvs, a_num_envs, a_max_steps, paths, a_ai2s, utt, partial_obs, device, seed,
-                          slot_id_base, ai1s=_ai1s)
+                          slot_id_base, ai1s=_ai1s, rewards=rewards)
         self.botOnly = _ai1s is not None
         self.maxSteps = a_max_steps
         self.utt = utt
@@ -148,8 +161,8 @@ class JNIGridnetVecClient:
     def _responses(self):
         h, r = self._h, self._resp
         obs = None if getattr(self, "botOnly", False) else np.ctypeslib.as_array(r.obs, shape=(h.S, h.C, h.H, h.W))
-        rew = np.ctypeslib.as_array(r.reward, shape=(h.S, 1))
-        done = np.ctypeslib.as_array(r.done, shape=(h.S, 1)).view(np.bool_)
+        rew = np.ctypeslib.as_array(r.reward, shape=(h.S, h.R))
+        done = np.ctypeslib.as_array(r.done, shape=(h.S, h.R)).view(np.bool_)
         return Responses(obs, rew, done)
 
     def reset(self, players=None):
@@ -217,10 +230,12 @@ class DeviceVecEnv:
     no extra synchronisation."""
 
     def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
-                 device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None, mask_delta=True, source_bits=True):
+                 device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None, mask_delta=True, source_bits=True,
+                 rfs=None):
         """mask_delta: `masks` is owned by this object and reused every call, so only changed rows are
         rewritten (the tensor must not be written by the caller).  source_bits: also keep mask slot 0
-        as bits in `source` ([slots][ceil(H*W/32)] int32), which random_policy uses."""
+        as bits in `source` ([slots][ceil(H*W/32)] int32), which random_policy uses.  rfs: reward
+        function names (a_rfs); reward / done are [S] for one function, [S][R] otherwise."""
         import torch
 
         if not torch.cuda.is_available():
@@ -229,14 +244,15 @@ class DeviceVecEnv:
         utt = utt or UnitTypeTable()
         paths = [_resolve("", p) for p in map_paths]
         self._h = _Handle(num_selfplay_slots, num_bot_envs, max_steps, paths, ai2s, utt, partial_obs, device, seed,
-                          slot_id_base, ai1s=ai1s, mask_delta=mask_delta and with_masks)
+                          slot_id_base, ai1s=ai1s, mask_delta=mask_delta and with_masks, rewards=_check_rfs(rfs))
         h = self._h
         dev = torch.device("cuda", device)
         self.device = dev
         S, H, W, C, K = h.S, h.H, h.W, h.C, h.K
         self.obs = torch.zeros((S, C, H, W), dtype=torch.int32, device=dev)
-        self.reward = torch.zeros((S,), dtype=torch.float64, device=dev)
-        self.done = torch.zeros((S,), dtype=torch.uint8, device=dev)
+        rshape = (S,) if h.R == 1 else (S, h.R)
+        self.reward = torch.zeros(rshape, dtype=torch.float64, device=dev)
+        self.done = torch.zeros(rshape, dtype=torch.uint8, device=dev)
         self.masks = torch.zeros((S, H, W, K), dtype=torch.uint8, device=dev) if with_masks else None
         self.actions = torch.zeros((S, H * W, 7), dtype=torch.int32, device=dev)
         self.players = torch.zeros((S,), dtype=torch.int32, device=dev)

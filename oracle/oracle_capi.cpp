@@ -6,6 +6,7 @@
 // used by bench.py, behind a small C API consumed by ctypes from tests/.
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <mutex>
 #include <cstdio>
@@ -25,21 +26,112 @@ namespace {
 
 enum BotKind { BOT_PASSIVE = 0, BOT_RANDOM_BIASED = 1 };
 
-struct Resp {  // ai/jni/Response.java:12-30 (one reward function: WinLoss)
-    std::vector<int32_t> obs;
-    double reward = 0;
-    uint8_t done = 0;
+// ---------------------------------------------------------------- reward functions (src/ai/reward/*.java)
+// ids shared with include/mrts.h MRTS_RF_*
+enum RewardKind {
+    RF_WINLOSS = 0, RF_RESOURCE_GATHER = 1, RF_PRODUCE_WORKER = 2, RF_PRODUCE_BUILDING = 3, RF_ATTACK = 4,
+    RF_PRODUCE_COMBAT_UNIT = 5, RF_CLOSER_TO_ENEMY_BASE = 6, RF_CLOSER_TO_ENEMY_UNIT = 7, RF_COUNT = 8
 };
 
-// WinLossRewardFunction.computeReward (ai/reward/WinLossRewardFunction.java:16-24)
-static void winLoss(const GameState& after, int maxplayer, double& reward, uint8_t& done) {
+// rts/TraceEntry.java:18-63: a pgs clone + the issued pairs (PlayerAction.clone, PlayerAction.java:264-272:
+// new Pair objects holding the same unit and action objects)
+struct TraceEntry {
+    PGSP pgs;
+    int time;
+    std::vector<PairP> actions;
+    explicit TraceEntry(const GameState& gs) : pgs(gs.pgs->clone()), time(gs.time) {}
+    void addPlayerAction(const PlayerAction& pa) {
+        for (auto& p : pa.actions) actions.push_back(std::make_shared<Pair>(Pair{p->m_a, p->m_b}));
+    }
+};
+
+static bool named(const Unit& u, const char* n) { return u.type->name == n; }
+static bool mobile(const Unit& u) {  // the "Light" / "Heavy" / "Ranged" / "Worker" name tests
+    return named(u, "Light") || named(u, "Heavy") || named(u, "Ranged") || named(u, "Worker");
+}
+
+// RewardFunctionInterface.computeReward(maxplayer, minplayer, te, afterGs) for each kind
+static void computeReward(int kind, int maxplayer, int minplayer, const TraceEntry& te, const GameState& after,
+                          double& reward, uint8_t& done) {
     reward = 0.0;
     done = 0;
-    if (after.gameover()) {
-        done = 1;
-        reward = after.winner() == maxplayer ? 1.0 : -1.0;
+    switch (kind) {
+        case RF_WINLOSS:  // WinLossRewardFunction.java:16-24
+            if (after.gameover()) {
+                done = 1;
+                reward = after.winner() == maxplayer ? 1.0 : -1.0;
+            }
+            break;
+        case RF_RESOURCE_GATHER: {  // ResourceGatherRewardFunction.java:22-44 (float constants 1)
+            for (auto& p : te.actions) {
+                if (p->m_a->player == maxplayer && p->m_b->type == UnitAction::TYPE_HARVEST) reward += 1.0f;
+                else if (p->m_a->player == maxplayer && p->m_b->type == UnitAction::TYPE_RETURN) reward += 1.0f;
+            }
+            done = 1;
+            for (auto& u : after.pgs->units)
+                if (named(*u, "Resource") && u->resources > 0) {
+                    done = 0;
+                    break;
+                }
+        } break;
+        case RF_PRODUCE_WORKER:       // ProduceWorkerRewardFunction.java:22-33
+        case RF_PRODUCE_BUILDING:     // ProduceBuildingRewardFunction.java:22-33
+        case RF_PRODUCE_COMBAT_UNIT:  // ProduceCombatUnitRewardFunction.java:22-33
+            for (auto& p : te.actions) {
+                if (p->m_a->player != maxplayer || p->m_b->type != UnitAction::TYPE_PRODUCE || !p->m_b->unitType) continue;
+                const std::string& n = p->m_b->unitType->name;
+                bool hit = kind == RF_PRODUCE_WORKER ? n == "Worker"
+                         : kind == RF_PRODUCE_BUILDING ? (n == "Barracks" || n == "Base")
+                                                       : (n == "Light" || n == "Heavy" || n == "Ranged");
+                if (hit) reward += 1.0f;
+            }
+            break;
+        case RF_ATTACK:  // AttackRewardFunction.java:22-38
+            for (auto& p : te.actions) {
+                if (p->m_a->player == maxplayer && p->m_b->type == UnitAction::TYPE_ATTACK_LOCATION) {
+                    const Unit* other = te.pgs->getUnitAt(p->m_b->x, p->m_b->y);
+                    if (other) {
+                        if (other->player == minplayer) reward += 1.0f;
+                        else if (other->player == maxplayer) reward -= 1.0f;
+                    }
+                }
+            }
+            break;
+        case RF_CLOSER_TO_ENEMY_BASE:    // CloserToEnemyBaseRewardFunction.java:22-66
+        case RF_CLOSER_TO_ENEMY_UNIT: {  // CloserToEnemyUnitRewardFunction.java:22-66 (same text: enemy *Base*)
+            int baseX = 0, baseY = 0;
+            bool baseExists = false;
+            for (auto& t : te.pgs->units)
+                if (t->player == minplayer && named(*t, "Base")) {
+                    baseExists = true;
+                    baseX = t->x;
+                    baseY = t->y;
+                    break;
+                }
+            if (!baseExists) return;
+            double oldMin = 2000000000;
+            for (auto& t : te.pgs->units)
+                if (t->player == maxplayer && mobile(*t)) {
+                    double d = std::sqrt(std::pow((double)(baseX - t->x), 2.0) + std::pow((double)(baseY - t->y), 2.0));
+                    if (d < oldMin) oldMin = d;
+                }
+            double newMin = 2000000000;
+            for (auto& t : after.pgs->units)
+                if (t->player == maxplayer && mobile(*t)) {
+                    double d = std::sqrt(std::pow((double)(baseX - t->x), 2.0) + std::pow((double)(baseY - t->y), 2.0));
+                    if (d < newMin) newMin = d;
+                }
+            reward = oldMin - newMin;
+        } break;
+        default: throw std::runtime_error("unknown reward function");
     }
 }
+
+struct Resp {  // ai/jni/Response.java:12-30: per reward function
+    std::vector<int32_t> obs;
+    std::vector<double> reward;
+    std::vector<uint8_t> done;
+};
 
 struct Env;
 
@@ -49,6 +141,7 @@ struct World {
     int H = 0, W = 0, C = 6;
     bool partialObs = false;
     uint64_t seed = 0;
+    std::vector<int> rfs{RF_WINLOSS};  // a_rfs (JNIGridnetVecClient.java:106)
     World(int ver, int crs) : utt(ver, crs) {
         maxAttackRadius = utt.getMaxAttackRange() * 2 + 1;
         K = maskSlotsPerCell(utt);
@@ -74,7 +167,18 @@ struct Env {
             if (bk == BOT_PASSIVE) ai2.reset(new PassiveAI());
             else ai2.reset(new RandomBiasedAI(&samplerGen));
         }
-        for (auto& r : resp) r.obs.assign((size_t)w->C * w->H * w->W, 0);
+        for (auto& r : resp) {
+            r.obs.assign((size_t)w->C * w->H * w->W, 0);
+            r.reward.assign(w->rfs.size(), 0.0);
+            r.done.assign(w->rfs.size(), 0);
+        }
+    }
+    void rewards(Resp& r, int maxplayer, const TraceEntry& te) {
+        for (size_t j = 0; j < w->rfs.size(); j++) computeReward(w->rfs[j], maxplayer, 1 - maxplayer, te, *gs, r.reward[j], r.done[j]);
+    }
+    void clearRewards(Resp& r) {
+        std::fill(r.reward.begin(), r.reward.end(), 0.0);
+        std::fill(r.done.begin(), r.done.end(), 0);
     }
     GSP makeView(int player) {
         if (w->partialObs) return std::make_shared<PartiallyObservableGameState>(*gs, player);
@@ -92,14 +196,12 @@ struct Env {
         if (selfplay) {
             for (int i = 0; i < 2; i++) {
                 playergs[i] = makeView(i);
-                resp[i].reward = 0;
-                resp[i].done = 0;
+                clearRewards(resp[i]);
                 playergs[i]->getVectorObservation(i, resp[i].obs.data());
             }
         } else {
             playergs[0] = makeView(player);
-            resp[0].reward = 0;
-            resp[0].done = 0;
+            clearRewards(resp[0]);
             playergs[0]->getVectorObservation(player, resp[0].obs.data());
         }
     }
@@ -122,14 +224,16 @@ struct Env {
     // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
     void stepSelfPlay(const std::vector<int>& rows0, const std::vector<int>& rows1) {
         const std::vector<int>* rows[2] = {&rows0, &rows1};
+        TraceEntry te(*gs);  // before either issue (JNIGridnetClientSelfPlay.java:160)
         for (int i = 0; i < 2; i++) {
             playergs[i] = makeView(i);
             PlayerAction pa = jniGetAction(i, *playergs[i], *rows[i]);
             gs->issueSafe(pa);
+            te.addPlayerAction(pa);
         }
         gs->cycle();
         for (int i = 0; i < 2; i++) {
-            winLoss(*gs, i, resp[i].reward, resp[i].done);
+            rewards(resp[i], i, te);
             playergs[i]->getVectorObservation(i, resp[i].obs.data());
         }
     }
@@ -142,8 +246,11 @@ struct Env {
         PlayerAction pa2 = ai2->getAction(1 - player, *p2);
         gs->issueSafe(pa1);
         gs->issueSafe(pa2);
+        TraceEntry te(*gs);  // after both issues (JNIGridnetClient.java:182-184)
+        te.addPlayerAction(pa1);
+        te.addPlayerAction(pa2);
         gs->cycle();
-        winLoss(*gs, player, resp[0].reward, resp[0].done);
+        rewards(resp[0], player, te);
         p1->getVectorObservation(player, resp[0].obs.data());
     }
 };
@@ -165,15 +272,18 @@ struct VecClient {
         *player = 0;
         return bots[(size_t)(s - nsp)].get();
     }
-    void collect(int32_t* obs, double* reward, uint8_t* done) {
+    void collect(int32_t* obs, double* reward, uint8_t* done) {  // reward / done: [slots][R]
         const size_t osz = (size_t)world->C * world->H * world->W;
+        const size_t R = world->rfs.size();
         for (int s = 0; s < nSlots(); s++) {
             int p;
             Env* e = slotEnv(s, &p);
             Resp& r = e->resp[e->selfplay ? p : 0];
             if (obs) std::memcpy(obs + (size_t)s * osz, r.obs.data(), osz * sizeof(int32_t));
-            if (reward) reward[s] = r.reward;
-            if (done) done[s] = r.done;
+            for (size_t j = 0; j < R; j++) {
+                if (reward) reward[(size_t)s * R + j] = r.reward[j];
+                if (done) done[(size_t)s * R + j] = r.done[j];
+            }
         }
     }
     // reset (:179-211)
@@ -202,16 +312,16 @@ struct VecClient {
             e.stepSelfPlay(rowsOf(e, (int)(2 * i)), rowsOf(e, (int)(2 * i + 1)));
             envSteps[2 * i] += 1;
             envSteps[2 * i + 1] += 1;
-            if (e.resp[0].done || envSteps[2 * i] >= maxSteps) {
-                double tr0 = e.resp[0].reward, tr1 = e.resp[1].reward;
-                uint8_t td0 = e.resp[0].done, td1 = e.resp[1].done;
+            if (e.resp[0].done[0] || envSteps[2 * i] >= maxSteps) {  // done[0]: the first reward function's
+                std::vector<double> tr0 = e.resp[0].reward, tr1 = e.resp[1].reward;
+                std::vector<uint8_t> td0 = e.resp[0].done, td1 = e.resp[1].done;
                 e.reset(0);
                 e.resp[0].reward = tr0;
                 e.resp[0].done = td0;
                 e.resp[1].reward = tr1;
                 e.resp[1].done = td1;
-                e.resp[0].done = 1;
-                e.resp[1].done = 1;
+                e.resp[0].done[0] = 1;
+                e.resp[1].done[0] = 1;
                 envSteps[2 * i] = 0;
                 envSteps[2 * i + 1] = 0;
             }
@@ -223,13 +333,13 @@ struct VecClient {
             int pl = players ? players[s] : 0;
             envSteps[(size_t)s] += 1;
             e.stepBot(rowsOf(e, s), pl);
-            if (e.resp[0].done || envSteps[(size_t)s] >= maxSteps) {
-                double tr = e.resp[0].reward;
-                uint8_t td = e.resp[0].done;
+            if (e.resp[0].done[0] || envSteps[(size_t)s] >= maxSteps) {
+                std::vector<double> tr = e.resp[0].reward;
+                std::vector<uint8_t> td = e.resp[0].done;
                 e.reset(pl);
                 e.resp[0].reward = tr;
                 e.resp[0].done = td;
-                e.resp[0].done = 1;
+                e.resp[0].done[0] = 1;
                 envSteps[(size_t)s] = 0;
             }
         }
@@ -378,6 +488,25 @@ int oref_step(void* h, const int32_t* actions, const int32_t* players, int32_t* 
     }
 }
 
+// a_rfs (JNIGridnetVecClient.java:106): the reward functions (RewardKind ids), in order; call before
+// reset.  reward / done of reset / step are then [slots][n].
+int oref_set_rewards(void* h, const int32_t* kinds, int n) {
+    auto v = (VecClient*)h;
+    if (n < 1 || n > RF_COUNT) return -22;
+    for (int i = 0; i < n; i++)
+        if (kinds[i] < 0 || kinds[i] >= RF_COUNT) return -22;
+    v->world->rfs.assign(kinds, kinds + n);
+    auto fix = [&](Env& e) {
+        for (auto& r : e.resp) {
+            r.reward.assign((size_t)n, 0.0);
+            r.done.assign((size_t)n, 0);
+        }
+    };
+    for (auto& e : v->selfPlay) fix(*e);
+    for (auto& e : v->bots) fix(*e);
+    return 0;
+}
+
 // gameStep(int[][][] action, players) with Java rows: rows = [slots][n_rows][8]
 int oref_step_rows(void* h, const int32_t* rows, int n_rows, const int32_t* players, int32_t* obs, double* reward,
                    uint8_t* done) {
@@ -433,6 +562,7 @@ struct BotVec {
     }
     std::unique_ptr<AI> ai1, ai2;
     int envSteps = 0, maxSteps = 2000;
+    std::vector<int> rfs{RF_WINLOSS};
 };
 
 void* oref_botclient_create(const char* map_path, int ai1, int ai2, int max_steps, int utt_version, int crs, int64_t seed) {
@@ -457,6 +587,13 @@ void* oref_botclient_create(const char* map_path, int ai1, int ai2, int max_step
     }
 }
 void oref_botclient_destroy(void* h) { delete (BotVec*)h; }
+// a_rfs: the reward functions (RewardKind ids), in order; reward/done of oref_botclient_step get n values
+int oref_botclient_set_rewards(void* h, const int32_t* kinds, int n) {
+    auto b = (BotVec*)h;
+    if (n < 1 || n > RF_COUNT) return -22;
+    b->rfs.assign(kinds, kinds + n);
+    return 0;
+}
 // JNIBotClient.gameStep (:108-135) + VecClient bot-only auto-reset (:214-238); returns 0
 int oref_botclient_step(void* h, int player, double* reward, uint8_t* done) {
     try {
@@ -465,12 +602,16 @@ int oref_botclient_step(void* h, int player, double* reward, uint8_t* done) {
         PlayerAction pa2 = b->ai2->getAction(1 - player, *b->gs);
         b->gs->issueSafe(pa1);
         b->gs->issueSafe(pa2);
+        TraceEntry te(*b->gs);  // JNIBotClient.java:114-116
+        te.addPlayerAction(pa1);
+        te.addPlayerAction(pa2);
         b->gs->cycle();
-        winLoss(*b->gs, player, *reward, *done);
+        const size_t R = b->rfs.size();
+        for (size_t j = 0; j < R; j++) computeReward(b->rfs[j], player, 1 - player, te, *b->gs, reward[j], done[j]);
         b->envSteps++;
-        if (*done || b->envSteps >= b->maxSteps) {
+        if (done[0] || b->envSteps >= b->maxSteps) {  // rs[i].done[0] (JNIGridnetVecClient.java:218-230)
             b->newGame();
-            *done = 1;
+            done[0] = 1;
             b->envSteps = 0;
         }
         return 0;

@@ -36,6 +36,8 @@ def load():
         L.oref_reset.argtypes = [P, P, P, P, P]
         L.oref_step.argtypes = [P, P, P, P, P, P]
         L.oref_step_rows.argtypes = [P, P, I, P, P, P, P]
+        L.oref_set_rewards.argtypes = [P, P, I]
+        L.oref_botclient_set_rewards.argtypes = [P, P, I]
         L.oref_get_masks.argtypes = [P, I, P]
         L.oref_dump_state.argtypes = [P, I, P, I]
         L.oref_env_steps.argtypes = [P, I]
@@ -62,7 +64,9 @@ class OracleVecClient:
     """Mirror of tests.JNIGridnetVecClient (src/tests/JNIGridnetVecClient.java) on the CPU oracle."""
 
     def __init__(self, n_selfplay_slots, n_bot_envs, max_steps, map_paths, partial_obs=False, utt_version=1, crs=1,
-                 bot_kinds=None, seed=0, slot_id_base=0):
+                 bot_kinds=None, seed=0, slot_id_base=0, rewards=None):
+        """rewards: reward function ids (REWARD_IDS); None = [WinLoss].  reward / done are [S] for one
+        reward function, [S][R] otherwise."""
         L = load()
         self.L = L
         paths = (ctypes.c_char_p * len(map_paths))(*[os.path.join(ROOT, p).encode() for p in map_paths])
@@ -75,8 +79,14 @@ class OracleVecClient:
         L.oref_dims(self.h, *[ctypes.byref(x) for x in d])
         self.S, self.H, self.W, self.C, self.K = [x.value for x in d]
         self.obs = np.zeros((self.S, self.C, self.H, self.W), np.int32)
-        self.reward = np.zeros((self.S,), np.float64)
-        self.done = np.zeros((self.S,), np.uint8)
+        R = 1
+        if rewards is not None:
+            k = np.asarray(rewards, np.int32)
+            self._chk(L.oref_set_rewards(self.h, _ptr(k), len(k)))
+            R = len(k)
+        shape = (self.S,) if R == 1 else (self.S, R)
+        self.reward = np.zeros(shape, np.float64)
+        self.done = np.zeros(shape, np.uint8)
 
     def _chk(self, r):
         if r != 0:
@@ -125,6 +135,12 @@ class OracleVecClient:
         self.close()
 
 
+# reward function ids (oracle_capi.cpp RewardKind = include/mrts.h MRTS_RF_*)
+REWARD_IDS = {"WinLossRewardFunction": 0, "ResourceGatherRewardFunction": 1, "ProduceWorkerRewardFunction": 2,
+              "ProduceBuildingRewardFunction": 3, "AttackRewardFunction": 4, "ProduceCombatUnitRewardFunction": 5,
+              "CloserToEnemyBaseRewardFunction": 6, "CloserToEnemyUnitRewardFunction": 7}
+
+
 def policy(mask, seed, env_id, step, player, n_types=7):
     """Philox masked-uniform policy (bit-identical to the GPU policy kernel). mask: u8[H,W,K]."""
     L = load()
@@ -138,19 +154,28 @@ def policy(mask, seed, env_id, step, player, n_types=7):
 class OracleBotClient:
     """tests.JNIBotClient (src/tests/JNIBotClient.java) + the bot-only VecClient auto-reset, one game."""
 
-    def __init__(self, map_path, ai1, ai2, max_steps=2000, utt_version=1, crs=1, seed=0):
+    def __init__(self, map_path, ai1, ai2, max_steps=2000, utt_version=1, crs=1, seed=0, rewards=None):
         L = load()
         self.L = L
         self.h = L.oref_botclient_create(os.path.join(ROOT, map_path).encode(), ai1, ai2, max_steps, utt_version, crs, seed)
         if not self.h:
             raise RuntimeError(L.oref_last_error().decode())
+        self.R = 1
+        if rewards is not None:
+            k = np.asarray(rewards, np.int32)
+            if L.oref_botclient_set_rewards(self.h, _ptr(k), len(k)) != 0:
+                raise RuntimeError("bad reward functions")
+            self.R = len(k)
 
     def step(self, player=0):
-        r = ctypes.c_double()
-        d = ctypes.c_uint8()
-        if self.L.oref_botclient_step(self.h, player, ctypes.byref(r), ctypes.byref(d)) != 0:
+        """-> (reward, done): scalars for one reward function, arrays [R] otherwise."""
+        r = np.zeros(self.R, np.float64)
+        d = np.zeros(self.R, np.uint8)
+        if self.L.oref_botclient_step(self.h, player, _ptr(r), _ptr(d)) != 0:
             raise RuntimeError(self.L.oref_last_error().decode())
-        return r.value, d.value
+        if self.R == 1:
+            return float(r[0]), int(d[0])
+        return r, d
 
     def dump(self):
         buf = np.zeros(1 << 16, np.int32)

@@ -31,15 +31,24 @@ def test_library_loads_and_exports_every_symbol():
 
 def test_config_struct_layout():
     # mrts_config: 6 int32, pointer, pointer, int32, uint64, int32 (natural alignment)
-    assert ctypes.sizeof(_lib.MrtsConfig) == 6 * 4 + 8 + 8 + 8 + 4 + 4 + 8 + 8
+    assert ctypes.sizeof(_lib.MrtsConfig) == 88
     assert _lib.MrtsConfig.seed.offset == 56
     assert _lib.MrtsConfig.mask_delta.offset == 68
+    assert _lib.MrtsConfig.reward_kinds.offset == 72 and _lib.MrtsConfig.n_rewards.offset == 80
 
 
 def test_argument_validation():
     with pytest.raises(NotImplementedError):
-        _check_rfs(["AttackRewardFunction"])
-    _check_rfs(["WinLossRewardFunction"])
+        _check_rfs(["ScoreRewardFunction"])
+    assert _check_rfs(None) == [0]
+    assert _check_rfs(["WinLossRewardFunction", "ResourceGatherRewardFunction", "ProduceWorkerRewardFunction",
+                       "ProduceBuildingRewardFunction", "AttackRewardFunction", "ProduceCombatUnitRewardFunction",
+                       "CloserToEnemyBaseRewardFunction", "CloserToEnemyUnitRewardFunction"]) == list(range(8))
+
+    class AttackRewardFunction:  # an instance named like the Java class is accepted (JPype proxies)
+        pass
+
+    assert _check_rfs([AttackRewardFunction()]) == [4]
     with pytest.raises(NotImplementedError):
         _bot_kind("WorkerRush")
     assert _bot_kind("PassiveAI") == 0

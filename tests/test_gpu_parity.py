@@ -42,15 +42,16 @@ def _compare_step(env, ref, step, dump_every, tag=""):
 
 
 def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, policy="masked", dump_every=10, seed=3,
-             players=None, partial_obs=False, bots=None):
+             players=None, partial_obs=False, bots=None, rfs=None):
     torch = _torch()
     from microrts_amd import DeviceVecEnv, UnitTypeTable
 
     env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=UnitTypeTable(utt, crs), seed=seed, partial_obs=partial_obs,
-                       ai2s=bots)
+                       ai2s=bots, rfs=rfs)
     kinds = [1 if b == "RandomBiasedAI" else 0 for b in bots] if bots else None
     ref = oracle_py.OracleVecClient(n_sp, n_bot, max_steps, maps, utt_version=utt, crs=crs, seed=seed,
-                                    partial_obs=partial_obs, bot_kinds=kinds)
+                                    partial_obs=partial_obs, bot_kinds=kinds,
+                                    rewards=[oracle_py.REWARD_IDS[r] for r in rfs] if rfs else None)
     S = ref.S
     if players is not None:
         env.players.copy_(torch.as_tensor(players, dtype=torch.int32))
@@ -81,6 +82,8 @@ def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, polic
         env.step()
         ref.step(acts, players)
         _compare_step(env, ref, step + 1, dump_every)
+        if rfs:
+            _rollout.nonzero |= (ref.reward != 0).reshape(ref.S, -1).any(axis=0)
     flags = env.error_flags()
     env.close()
     ref.close()
@@ -390,3 +393,58 @@ def test_more_than_64_units(rows):
     assert not env.error_flags().any()
     env.close()
     ref.close()
+
+
+ALL_RFS = ["WinLossRewardFunction", "ResourceGatherRewardFunction", "ProduceWorkerRewardFunction",
+           "ProduceBuildingRewardFunction", "AttackRewardFunction", "ProduceCombatUnitRewardFunction",
+           "CloserToEnemyBaseRewardFunction", "CloserToEnemyUnitRewardFunction"]
+
+
+@pytest.mark.parametrize("mp,n_sp,n_bot,po,policy,crs", [
+    ("maps/16x16/basesWorkers16x16.xml", 8, 0, False, "masked", 1),
+    ("maps/8x8/basesWorkers8x8.xml", 4, 4, False, "uniform", 1),
+    ("maps/10x10/basesWorkers10x10.xml", 4, 4, True, "masked", 1),
+    ("maps/8x8/basesWorkers8x8.xml", 4, 4, True, "uniform", 3),
+    ("maps/4x4/base4x4.xml", 6, 2, False, "masked", 1),
+])
+def test_all_reward_functions(mp, n_sp, n_bot, po, policy, crs):
+    """The eight reward functions of src/ai/reward in MicroRTS-Py's order: reward [S][8] and done [S][8]
+    bit-exact (the Closer* ones are fp64 sqrt differences) after every step, self-play + RandomBiasedAI
+    opponents, full and partial observability."""
+    bots = ["RandomBiasedAI"] * n_bot if n_bot else None
+    _rollout.nonzero = np.zeros(len(ALL_RFS), bool)
+    assert not _rollout([mp] * (n_sp + n_bot), n_sp, n_bot, steps=400, max_steps=300, crs=crs, policy=policy,
+                        partial_obs=po, bots=bots, rfs=ALL_RFS, dump_every=25).any()
+    # non-vacuous: under the masked policy the gather / worker / attack / distance functions fire (WinLoss
+    # and the building / combat-unit ones can stay 0 in 400 random steps); unmasked actions are mostly
+    # illegal, so only the distance functions are certain to
+    must = [1, 2, 4, 6, 7] if policy == "masked" else [6, 7]
+    assert _rollout.nonzero[must].all(), _rollout.nonzero
+
+
+def test_first_reward_function_drives_reset():
+    """done[0] of the FIRST reward function triggers the auto-reset (JNIGridnetVecClient.java:247):
+    with ResourceGather first, a game resets only when its resources are gone, not at gameover."""
+    rfs = ["ResourceGatherRewardFunction", "WinLossRewardFunction", "AttackRewardFunction"]
+    _rollout.nonzero = np.zeros(len(rfs), bool)
+    assert not _rollout(["maps/4x4/base4x4.xml"] * 8, 8, 0, steps=600, max_steps=5000, rfs=rfs, dump_every=50).any()
+
+
+def test_bot_only_reward_functions():
+    """Config c1 clients with all eight reward functions (JNIBotClient.java:108-135)."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n, mp = 4, "maps/8x8/basesWorkers8x8.xml"
+    env = DeviceVecEnv(0, n, 300, [mp] * n, ai1s=["RandomBiasedAI"] * n, ai2s=["RandomBiasedAI"] * n, seed=5, rfs=ALL_RFS)
+    refs = [oracle_py.OracleBotClient(mp, 1, 1, max_steps=300, seed=5 + j,
+                                      rewards=[oracle_py.REWARD_IDS[r] for r in ALL_RFS]) for j in range(n)]
+    env.reset()
+    for step in range(500):
+        env.step()
+        env.synchronize()
+        rw, dn = env.reward.cpu().numpy(), env.done.cpu().numpy()
+        for j, r in enumerate(refs):
+            er, ed = r.step(0)
+            assert np.array_equal(rw[j], er) and np.array_equal(dn[j], ed), f"env {j} step {step}: {rw[j]} {er}"
+    env.close()

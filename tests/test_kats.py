@@ -70,11 +70,12 @@ def row(pos, t=NONE, move=0, harvest=0, ret=0, pdir=0, ptype=0, attack=0):
 class Runner:
     """Self-play pair (slots 0 = player 0, 1 = player 1) on the oracle or on the GPU."""
 
-    def __init__(self, backend, map_path, partial_obs=False, max_steps=2000):
+    def __init__(self, backend, map_path, partial_obs=False, max_steps=2000, rfs=None):
         self.backend = backend
         self.po = partial_obs
         if backend == "oracle":
-            self.e = oracle_py.OracleVecClient(2, 0, max_steps, [map_path] * 2, partial_obs=partial_obs)
+            self.e = oracle_py.OracleVecClient(2, 0, max_steps, [map_path] * 2, partial_obs=partial_obs,
+                                               rewards=[oracle_py.REWARD_IDS[r] for r in rfs] if rfs else None)
             self.e.reset()
         else:
             import torch
@@ -83,7 +84,7 @@ class Runner:
             from microrts_amd import DeviceVecEnv
 
             self.torch = torch
-            self.e = DeviceVecEnv(2, 0, max_steps, [map_path] * 2, partial_obs=partial_obs)
+            self.e = DeviceVecEnv(2, 0, max_steps, [map_path] * 2, partial_obs=partial_obs, rfs=rfs)
             self.e.reset()
 
     def step(self, rows0=(), rows1=()):
@@ -310,9 +311,39 @@ def kat_mask_record(tmp, backend):
     r.close()
 
 
+def kat_reward_functions(tmp, backend):
+    """§8f — src/ai/reward/*.java over the TraceEntry of the step (the pairs issued this step, after
+    issueSafe; JNIGridnetClientSelfPlay.java:160-169) and the post-cycle state.  Step 1: player 0
+    issues HARVEST (ResourceGather +1), PRODUCE Worker (ProduceWorker +1) and an ATTACK on player 1's
+    worker E (Attack +1) — counted when issued, not when executed.  Step 5: the attack executes, E
+    dies; player 1 had E at distance sqrt(5) from player 0's Base and now has no mobile unit, so
+    CloserToEnemyBase = sqrt(5) - 2000000000 (the initial value of newMinDistance,
+    CloserToEnemyBaseRewardFunction.java:52).  Step 6: both minima are 2e9 -> 0."""
+    rfs = ["WinLossRewardFunction", "ResourceGatherRewardFunction", "ProduceWorkerRewardFunction", "AttackRewardFunction",
+           "CloserToEnemyBaseRewardFunction"]
+    units = [(RESOURCE, -1, 0, 0, 5), (WORKER, 0, 0, 1), (BASE, 0, 1, 1), (LIGHT, 0, 2, 2), (WORKER, 1, 3, 2),
+             (BASE, 1, 4, 4)]
+    m = write_map(tmp / "k11.xml", 5, 5, units)
+    r = Runner(backend, m, rfs=rfs)
+    _, rew, done = r.step([row(5, HARVEST, harvest=UP), row(6, PRODUCE, pdir=DOWN, ptype=WORKER),
+                           row(12, ATTACK, attack=atk(1, 0))])
+    assert rew.tolist() == [[0.0, 1.0, 1.0, 1.0, 0.0], [0.0, 0.0, 0.0, 0.0, 0.0]]
+    assert done.tolist() == [[0, 0, 0, 0, 0], [0, 0, 0, 0, 0]]
+    for _ in range(3):
+        _, rew, _ = r.step()
+        assert not rew.any()
+    _, rew, _ = r.step()  # time 5
+    assert rew[0].tolist() == [0.0] * 5
+    assert rew[1].tolist() == [0.0, 0.0, 0.0, 0.0, float(np.sqrt(5.0)) - 2000000000.0]
+    _, rew, _ = r.step()
+    assert not rew.any()
+    r.close()
+
+
 KATS = [kat_illegal_becomes_none_eta, kat_resource_quirk_row_order, kat_rows_that_do_not_count,
         kat_player1_sees_player0_reservations, kat_dead_unit_still_executes, kat_simultaneous_kill_is_a_draw,
-        kat_harvest_deplete_return, kat_duplicate_row_keeps_map_position, kat_po_killed_unit_in_view, kat_mask_record]
+        kat_harvest_deplete_return, kat_duplicate_row_keeps_map_position, kat_po_killed_unit_in_view, kat_mask_record,
+        kat_reward_functions]
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k.__name__ for k in KATS])
