@@ -45,6 +45,8 @@ def parse():
                     help="delta: the persistent mask tensor is updated in place (only changed rows written); "
                          "full: every mask byte is rewritten each step")
     ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of observations each step")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch the timed steps eagerly instead of replaying them as one captured hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc-traffic", type=float, default=None,
@@ -101,10 +103,10 @@ def main():
     def one_step(k, ev=None):
         env.random_policy(SEED, k)
         if ev is not None:
-            ev[0].record(stream)
+            ev[0].record(torch.cuda.current_stream(env.device))
         env.step()
         if ev is not None:
-            ev[1].record(stream)
+            ev[1].record(torch.cuda.current_stream(env.device))
         if gather_buf is not None:
             mdist.gather_observations(env.obs, gather_buf)
 
@@ -119,19 +121,46 @@ def main():
         units.append(env.dump_state(s)[4])
     mean_units = float(np.mean(units))
 
+    # The K timed steps (policy kernel + step kernel each) are captured once into a hipGraph and
+    # replayed as one launch, so host launch overhead does not pace the GPU ("capture launch-bound
+    # inner loops in hipGraphs").  Same kernels, same arguments.  Events cannot be timed inside a
+    # replayed graph on ROCm, so the step kernel's duration comes from HIP events around each launch
+    # in an eager pass over the K steps that follow (same stream, same episode phase).
+    base = a.burnin + a.warmup
+    graph = None
+    if not a.no_graph and gather_buf is None:
+        try:
+            graph = torch.cuda.CUDAGraph()
+            cap = torch.cuda.Stream(env.device)
+            cap.wait_stream(torch.cuda.current_stream(env.device))
+            with torch.cuda.graph(graph, stream=cap):
+                for k in range(a.steps):
+                    one_step(base + k)
+            torch.cuda.synchronize(env.device)
+        except Exception as ex:  # capture unsupported here: time eagerly instead
+            print(f"bench: hipGraph capture failed ({ex!r}); eager launches", file=sys.stderr)
+            graph = None
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(env.device)
     env.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.steps):
-        one_step(a.burnin + a.warmup + k, evs[k])
-    env.synchronize()
+    if graph is not None:
+        graph.replay()
+    else:
+        for k in range(a.steps):
+            one_step(base + k, evs[k])
     torch.cuda.synchronize(env.device)
+    env.synchronize()
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
+    if graph is not None:  # kernel-duration pass (untimed for `value`)
+        for k in range(a.steps):
+            one_step(base + a.steps + k, evs[k])
+        torch.cuda.synchronize(env.device)
+        base += a.steps
     t = mdist.max_over_ranks(t, env.device)
     step_ms = [s.elapsed_time(e) for s, e in evs]
     kern_ms = float(np.mean(step_ms))
@@ -154,7 +183,7 @@ def main():
         tot, n_probe = 0, 5
         for k in range(n_probe):  # untimed probe steps after the timed window
             before = env.source.clone()
-            one_step(a.burnin + a.warmup + a.steps + k)
+            one_step(base + a.steps + k)  # after the timed (and kernel-timing) windows
             env.synchronize()
             tot += int(lut[(before | env.source).view(torch.uint8).long()].sum().item())
         dirty = tot / (n_probe * S)
@@ -194,6 +223,9 @@ def main():
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": a.mask_mode,
+            "launch": "hipGraph replay of the K timed steps" if graph is not None else "eager",
+            "kernel_timing": ("HIP events around each step-kernel launch, eager pass over the next K steps"
+                              if graph is not None else "HIP events around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (", RCCL int16 obs all-gather" if gather_buf is not None else ""),
         },
         "step_kernel_ms": kern_ms,
