@@ -326,7 +326,17 @@ struct mrts_env {
         hstatic.tmpl_off = d_tmplOff;
         hstatic.game_kind = d_gameKind;
     }
-    hipError_t launch(int mode, const KDyn& D, hipStream_t s) const { return launchEnv(mode, hstatic, d_static, D, s); }
+    hipError_t launch(int mode, const KDyn& Din, hipStream_t s) const {
+        KDyn D = Din;
+        D.state = d_state;
+        D.state_words = stateWords(CAP, HW);
+        D.H = H;
+        D.W = W;
+        D.HW = HW;
+        D.CAP = CAP;
+        D.n_sp_games = nSpGames;
+        return launchEnv(mode, hstatic, d_static, D, s);
+    }
     int gameOfSlot(int slot, int* player) const {
         if (slot < 2 * nSpGames) {
             *player = slot & 1;

@@ -41,6 +41,7 @@ enum {
     H_RNG_CANCEL = 8, // 2 words: java.util.Random for CANCEL_RANDOM (GameState.r)
     H_RNG_DAMAGE = 10,// 2 words: java.util.Random for non-deterministic damage (UnitAction.r)
     H_RNG_SAMPLER = 12,// 2 words: java.util.Random for RandomBiasedAI (Sampler.generator)
+    H_KIND = 14,      // game kind (KStatic.game_kind), copied here so a step needs no dependent load
     H_WORDS = 16
 };
 // followed by 7 SoA arrays of CAP int32: UC, HP, RES, UA, PAR, AT, AS (see mrts_kernels.hip)
@@ -48,7 +49,10 @@ enum { A_UC = 0, A_HP = 1, A_RES = 2, A_UA = 3, A_PAR = 4, A_AT = 5, A_AS = 6, N
 // followed by 2 x maskWords(HW): per player, the cells whose mask rows were non-zero in the mask buffer
 // written last (delta mask writes, mrts_config.mask_delta)
 constexpr int maskWords(int hw) { return (hw + 31) / 32; }
-constexpr int stateWords(int cap, int hw) { return H_WORDS + N_ARRAYS * cap + 2 * maskWords(hw); }  // host + device
+// after the arrays: the previous mask row sets (2 x maskWords), then the map's terrain bytes (copied
+// from the template at reset, so a step's first memory round needs nothing but the state block)
+constexpr int stateTerrOff(int cap, int hw) { return H_WORDS + N_ARRAYS * cap + 2 * maskWords(hw); }
+constexpr int stateWords(int cap, int hw) { return stateTerrOff(cap, hw) + (hw + 3) / 4; }  // host + device
 
 // unit core word
 constexpr uint32_t UC_DEAD = 1u << 31;
@@ -91,6 +95,9 @@ struct KDyn {
     uint32_t* source;              // [n_slots][maskWords(HW)] mask slot 0 as bits, or null
     int32_t mask_player;           // player whose masks bot-env slots receive
     int32_t mask_delta;            // 1: `masks` holds the previous masks of this handle -> rewrite changed rows only
+    // copies of KStatic fields the first memory round needs (kernel arguments: no dependent load)
+    int32_t* state;
+    int32_t state_words, H, W, HW, CAP, n_sp_games;
     const int32_t* rows;           // Java row layout [n_slots][n_rows][8] (replaces `actions`) or null
     int32_t n_rows;
     uint32_t* pairs;               // rows mode: per game [n_rows][2] accepted-pair scratch

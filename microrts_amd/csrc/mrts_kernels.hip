@@ -164,7 +164,7 @@ struct Game {
     uint16_t* rslot; // ready-list scratch (64)
     uint8_t* snap;   // PO snapshot bits
     // wave-uniform scalars (only ever modified in uniform control flow)
-    int time, nu, pres0, pres1, seq, steps, ccnt, deaths;
+    int time, nu, pres0, pres1, seq, steps, ccnt, deaths, kind;
     int snapLimit0, snapLimit1;  // seq counter when player 0 / 1's snapshot was taken
     // issue index (valid while ixValid): `bits` = target cells (+W) of present MOVE/PRODUCE
     // assignments, whether any exists, per player the largest present PRODUCE cost (-1 = none) and
@@ -186,7 +186,7 @@ struct Game {
     JRand rngCancel, rngDamage, rngSampler;
 
     DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem)
-        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(p.H), W(p.W), HW(p.HW), CAP(p.CAP),
+        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(d.H), W(d.W), HW(d.HW), CAP(d.CAP),
           po(p.partial_obs != 0) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
@@ -219,7 +219,7 @@ struct Game {
     }
     DEV bool inb(int x, int y) const { return x >= 0 && x < W && y >= 0 && y < H; }
     DEV const int32_t* tmpl() const { return P.tmpl + P.tmpl_off[g]; }
-    DEV int32_t* st() const { return P.state + (size_t)g * stateWords(CAP, HW); }
+    DEV int32_t* st() const { return D.state + (size_t)g * D.state_words; }
 
     // UnitAction.ETA (rts/UnitAction.java:307-329)
     DEV int eta(int t, int prm, int ut, int unitType) const {
@@ -255,6 +255,11 @@ struct Game {
         for (int i = lane_id(); i < UTT_WORDS; i += 64) ul[i] = ug[i];
         wsync();
     }
+    DEV void storeTerrain() {  // the template's terrain words into the state block (at reset)
+        const int32_t* t = tmpl() + T_TERR;
+        int32_t* d = st() + stateTerrOff(CAP, HW);
+        for (int w = lane_id(); w < (HW + 3) / 4; w += 64) d[w] = t[w];
+    }
     DEV uint32_t* prevG() const { return (uint32_t*)(st() + H_WORDS + N_ARRAYS * CAP); }
     DEV void loadPrev() {  // previous mask row sets (delta mask writes), when not fetched by load()
         const uint32_t* pg = prevG();
@@ -278,6 +283,7 @@ struct Game {
         steps = rl(hv, H_STEPS);
         err = (uint32_t)rl(hv, H_ERR);
         ccnt = rl(hv, H_CANCEL_CNT);
+        kind = rl(hv, H_KIND);
         rngCancel.s = rng_of(rl(hv, H_RNG_CANCEL), rl(hv, H_RNG_CANCEL + 1));
         rngDamage.s = rng_of(rl(hv, H_RNG_DAMAGE), rl(hv, H_RNG_DAMAGE + 1));
         rngSampler.s = rng_of(rl(hv, H_RNG_SAMPLER), rl(hv, H_RNG_SAMPLER + 1));
@@ -288,7 +294,7 @@ struct Game {
     DEV void load(bool wantPrev) {
         const int32_t* s = st();
         const int32_t* arr = s + H_WORDS;
-        const int32_t* terr = tmpl() + T_TERR;
+        const int32_t* terr = s + stateTerrOff(CAP, HW);
         const int l = lane_id();
         const int TW = (HW + 3) / 4, PW = 2 * maskWords(HW);
         const int hv = l < H_WORDS ? s[l] : 0;
@@ -346,6 +352,7 @@ struct Game {
             case H_STEPS: hv = steps; break;
             case H_ERR: hv = (int)err; break;
             case H_CANCEL_CNT: hv = ccnt; break;
+            case H_KIND: hv = kind; break;
             case H_RNG_CANCEL: hv = (int)(uint32_t)rngCancel.s; break;
             case H_RNG_CANCEL + 1: hv = (int)(uint32_t)(rngCancel.s >> 32); break;
             case H_RNG_DAMAGE: hv = (int)(uint32_t)rngDamage.s; break;
@@ -2010,10 +2017,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
     Game G(P, D, smem);
-    const int kind = P.game_kind[G.g];
-    const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
-    const bool selfplay = gtype == GT_SELFPLAY;
-    const int slot0 = selfplay ? 2 * G.g : 2 * P.n_sp_games + (G.g - P.n_sp_games);
+    // games [0, n_sp_games) are self-play (mrts_create's layout): no load needed to place the slots
+    const bool selfplay = G.g < D.n_sp_games;
+    const int slot0 = selfplay ? 2 * G.g : 2 * D.n_sp_games + (G.g - D.n_sp_games);
     const int nslots = selfplay ? 2 : 1;
     // agent-vs-bot: the agent's side; bot-vs-bot: the side ai1 plays (JNIBotClient.gameStep(player))
     const int side = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
@@ -2027,8 +2033,10 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     if (MODE == MODE_RESET) {
         G.copyUtt();
         G.loadHeader(G.st());
+        G.kind = P.game_kind[G.g];
         G.err = 0;
         G.initCells();
+        G.storeTerrain();
         G.resetFromTemplate();
         if (D.mask_delta && D.masks) G.loadPrev();
         for (int k = lane_id(); k < nslots * P.n_rewards; k += 64) {
@@ -2038,6 +2046,8 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     } else {
         G.load(D.mask_delta && D.masks);
     }
+    const int kind = G.kind;
+    const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
     if (G.po) G.clearSnap();
     PHASE(0);
 
