@@ -14,8 +14,10 @@ the timed region.
 
 Multi-GPU: one process per GPU (torch.distributed.run), each rank steps its own disjoint shard of
 games (weak scaling, no collective in the step); barrier + synchronize bracket the timed region and
-the max time over ranks is reported.  --gather-obs adds the north-star RCCL all-gather of the int32
-observation tensor each step (reported in the JSON, not the default).
+the max time over ranks is reported.  --gather-obs [allgather|learner] adds the north-star RCCL
+exchange of the observation tensor every step (int16 transport, double-buffered, on its own stream so
+it overlaps the next step; all-gather to every rank or gather to rank 0) — not the default, since
+nothing in the step consumes it.
 """
 import argparse
 import json
@@ -44,7 +46,9 @@ def parse():
     ap.add_argument("--mask-mode", choices=["delta", "full"], default="delta",
                     help="delta: the persistent mask tensor is updated in place (only changed rows written); "
                          "full: every mask byte is rewritten each step")
-    ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of observations each step")
+    ap.add_argument("--gather-obs", nargs="?", const="allgather", choices=["allgather", "learner"], default=None,
+                    help="per-step RCCL exchange of the observation tensor (int16 transport, on its own stream, "
+                         "overlapped with the next step): all-gather to every rank, or gather to rank 0")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the timed steps eagerly instead of replaying them as one captured hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -98,7 +102,7 @@ def main():
     stream = torch.cuda.current_stream(env.device)
     gather_buf = None
     if a.gather_obs and world > 1:
-        gather_buf = torch.empty((world,) + tuple(env.obs.shape), dtype=torch.int16, device=env.device)
+        gather_buf = mdist.ObservationGather(env.obs.shape, env.device, mode=a.gather_obs)
 
     def one_step(k, ev=None):
         env.random_policy(SEED, k)
@@ -108,7 +112,7 @@ def main():
         if ev is not None:
             ev[1].record(torch.cuda.current_stream(env.device))
         if gather_buf is not None:
-            mdist.gather_observations(env.obs, gather_buf)
+            gather_buf.push(env.obs)
 
     env.reset()
     for k in range(a.burnin + a.warmup):
@@ -151,6 +155,8 @@ def main():
     else:
         for k in range(a.steps):
             one_step(base + k, evs[k])
+    if gather_buf is not None:
+        gather_buf.wait()  # the last step's exchange belongs to the timed window
     torch.cuda.synchronize(env.device)
     env.synchronize()
     if world > 1:
@@ -226,7 +232,9 @@ def main():
             "launch": "hipGraph replay of the K timed steps" if graph is not None else "eager",
             "kernel_timing": ("HIP events around each step-kernel launch, eager pass over the next K steps"
                               if graph is not None else "HIP events around each step-kernel launch in the timed window"),
-            "parallelism": f"dp{world} (independent env shards)" + (", RCCL int16 obs all-gather" if gather_buf is not None else ""),
+            "parallelism": f"dp{world} (independent env shards)" + (
+                f", per-step RCCL int16 observation {a.gather_obs} overlapped on a comm stream" if gather_buf is not None
+                else ", no collective in the step"),
         },
         "step_kernel_ms": kern_ms,
         "mean_units": mean_units,

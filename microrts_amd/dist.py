@@ -34,3 +34,73 @@ def gather_observations(obs, out=None, transport=torch.int16):
     else:
         dist.all_gather_into_tensor(out.view(-1), send.view(-1))
     return out
+
+
+class ObservationGather:
+    """The north-star observation exchange of every step, overlapped with the next
+    step's compute: the observation of step t is narrowed to the int16 transport (hp <= 10,
+    resources <= 32767 by map validation) into buffer t % 2 on the compute stream, and a separate
+    communication stream runs the collective while step t+1 computes; buffer t % 2 is reused only
+    after the collective of step t-2 finished.
+
+    mode "allgather": every rank receives [world, *obs.shape] (RCCL all-gather, ring, per-link bound);
+    mode "learner": only rank 0 receives it (gather to one rank: each peer sends once on its own
+    link).  gloo (the CPU tests) has no int16 collectives and no streams: int32, synchronous."""
+
+    def __init__(self, obs_shape, device, mode="allgather"):
+        if mode not in ("allgather", "learner"):
+            raise ValueError("mode must be 'allgather' or 'learner'")
+        self.mode = mode
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        self.gloo = dist.get_backend() == "gloo"
+        self.transport = torch.int32 if self.gloo else torch.int16
+        shape = tuple(obs_shape)
+        self.send = [torch.empty(shape, dtype=self.transport, device=device) for _ in range(2)]
+        recv = mode == "allgather" or self.rank == 0
+        self.recv = [torch.empty((self.world,) + shape, dtype=self.transport, device=device) if recv else None
+                     for _ in range(2)]
+        cuda = device.type == "cuda" and not self.gloo
+        self.comm = torch.cuda.Stream(device) if cuda else None
+        self.done = [torch.cuda.Event() for _ in range(2)] if cuda else None
+        self.fired = [False, False]
+        self.i = 0
+
+    def _collective(self, b):
+        if self.mode == "allgather":
+            if self.gloo:
+                dist.all_gather(list(self.recv[b].unbind(0)), self.send[b])
+            else:
+                dist.all_gather_into_tensor(self.recv[b].view(-1), self.send[b].view(-1))
+        else:
+            dist.gather(self.send[b], gather_list=list(self.recv[b].unbind(0)) if self.rank == 0 else None, dst=0)
+
+    def push(self, obs):
+        """Call after the step that produced `obs`, on the compute stream.  Returns the receive
+        buffer of this step (None on non-learner ranks in "learner" mode); it is complete after
+        wait() or once the next-but-one push() returned."""
+        b = self.i & 1
+        self.i += 1
+        if self.comm is None:
+            self.send[b].copy_(obs)
+            self._collective(b)
+            return self.recv[b]
+        cur = torch.cuda.current_stream(obs.device)
+        if self.fired[b]:
+            cur.wait_event(self.done[b])  # buffer b still feeds the collective of two steps ago
+        self.send[b].copy_(obs)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ready)
+            self._collective(b)
+            self.done[b].record(self.comm)
+        self.fired[b] = True
+        return self.recv[b]
+
+    def wait(self):
+        """Make the current stream wait for every collective issued so far."""
+        if self.comm is not None:
+            cur = torch.cuda.current_stream(self.send[0].device)
+            for b in range(2):
+                if self.fired[b]:
+                    cur.wait_event(self.done[b])

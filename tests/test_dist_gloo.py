@@ -58,3 +58,53 @@ def test_two_rank_shards_equal_single_process():
     whole = _rollout(2 * G, 0)
     assert gathered.shape == (2, 2 * G) + whole.shape[1:]
     assert np.array_equal(gathered.reshape(whole.shape).astype(np.int32), whole)
+
+
+def _gather_worker(rank, world, port, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sh = mdist.shard(rank, G)
+    env = oracle_py.OracleVecClient(2 * G, 0, 2000, [MAP] * (2 * G), seed=11, slot_id_base=sh["slot_id_base"])
+    obs, _, _ = env.reset()
+    pipe = mdist.ObservationGather(obs.shape, torch.device("cpu"), mode=mode)
+    outs = []
+    for step in range(6):
+        m = env.get_masks(0)
+        acts = np.stack([oracle_py.policy(m[s], SEED, sh["slot_id_base"] + s, step, 0) for s in range(env.S)])
+        obs, _, _ = env.step(acts)
+        r = pipe.push(torch.from_numpy(obs))
+        outs.append(None if r is None else r.clone().numpy())
+    pipe.wait()
+    env.close()
+    q.put((rank, outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["allgather", "learner"])
+def test_observation_gather_pipeline(mode):
+    """The double-buffered per-step exchange (all-gather, or gather to the learner rank) delivers
+    every step's observations of both shards."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 1000 + (0 if mode == "allgather" else 50)
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    whole = oracle_py.OracleVecClient(4 * G, 0, 2000, [MAP] * (4 * G), seed=11)
+    whole.reset()
+    for step in range(6):
+        m = whole.get_masks(0)
+        acts = np.stack([oracle_py.policy(m[s], SEED, s, step, 0) for s in range(whole.S)])
+        o, _, _ = whole.step(acts)
+        for rank in (0, 1):
+            got = res[rank][step]
+            if mode == "learner" and rank == 1:
+                assert got is None
+                continue
+            assert np.array_equal(got.reshape(o.shape).astype(np.int32), o), f"rank {rank} step {step}"
+    whole.close()
