@@ -80,6 +80,10 @@ def cpu_baseline(map_path, threads, burnin):
 
 def main():
     a = parse()
+    # stdout carries exactly one JSON line (rank 0): everything else that writes to fd 1 — RCCL's
+    # version banner, library prints — goes to stderr
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -87,7 +91,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    use_pg = world > 1 or (a.gather_obs is not None and "RANK" in os.environ)  # 1-rank RCCL run: exercise the exchange
+    if use_pg:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from microrts_amd import DeviceVecEnv
@@ -101,7 +106,7 @@ def main():
     S, H, W, C, K = env.dims
     stream = torch.cuda.current_stream(env.device)
     gather_buf = None
-    if a.gather_obs and world > 1:
+    if a.gather_obs and use_pg:
         gather_buf = mdist.ObservationGather(env.obs.shape, env.device, mode=a.gather_obs)
 
     def one_step(k, ev=None):
@@ -258,9 +263,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin)
     if rank == 0:
-        print(json.dumps(out))
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     env.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -136,6 +136,14 @@ int mrts_policy_invalidate(mrts_env* env);
  * given, to read only the candidate cells' mask rows. */
 int mrts_set_source_output(mrts_env* env, uint32_t* d_source);
 
+/* MicroRTS-Py observation encoding (gym_microrts GridnetVecEnv `_encode_obs`, external to the
+ * reference: clip each plane to [0, n-1] and one-hot it, channels last) of an observation tensor as
+ * written above: uint8 [n_slots][H][W][F], plane sizes {5 hp, 5 resources, 3 owner, types+1, 6 action,
+ * 2 terrain} (+ 2 per partial-observability plane); F = mrts_onehot_features(env) (29 / 33).
+ * d_out 16-byte aligned. */
+int mrts_onehot_features(const mrts_env* env);
+int mrts_onehot_dev(mrts_env* env, const int32_t* d_obs, uint8_t* d_out, void* stream);
+
 /* Canonical state dump of the game behind `slot` (same format as the CPU oracle's dumpState):
  * [time, 2, res0, res1, n_units, (type, player, x, y, hp, resources)*, n_assignments,
  *  (unit index, action type, parameter, x, y, unit type or -1, issue time)*] — units in

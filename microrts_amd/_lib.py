@@ -19,7 +19,7 @@ ERR_BITS = {
 # every symbol include/mrts.h declares
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_step_rows", "mrts_get_masks_i32",
-    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
 ]
 
@@ -82,6 +82,8 @@ def load(path=LIB_PATH):
     L.mrts_get_masks_i32.argtypes = [P, I32, P]
     L.mrts_step_rows_dev.argtypes = [P, P, I32, P, P, P, P, P, I32, P]
     L.mrts_get_masks_i32_dev.argtypes = [P, I32, P, P]
+    L.mrts_onehot_features.argtypes = [P]
+    L.mrts_onehot_dev.argtypes = [P, P, P, P]
     L.mrts_reset_dev.argtypes = [P, P, P, P, P, P, I32, P]
     L.mrts_step_dev.argtypes = [P, P, P, P, P, P, P, I32, P]
     L.mrts_get_masks_dev.argtypes = [P, I32, P, P]

@@ -27,6 +27,7 @@ hipError_t phaseSpans(unsigned long long* out, int n);
 #endif
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream, bool* prevWritten);
 hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t stream);
+hipError_t launchOneHot(const int32_t* obs, uint8_t* out, int n_slots, int HW, int C, int ntypes, hipStream_t stream);
 hipError_t prepareLds(size_t bytes);
 }  // namespace mrts
 
@@ -611,6 +612,22 @@ int mrts_get_masks_i32_dev(mrts_env* env, int32_t player, int32_t* d_out, void* 
         int r = mrts_get_masks_dev(env, player, env->d_masks, stream);
         if (r) return r;
         HIPCHK(launchWiden(env->d_masks, d_out, (size_t)env->nSlots * env->HW * env->K, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_onehot_features(const mrts_env* env) {
+    const int base = 5 + 5 + 3 + (env->utt.ntypes + 1) + 6 + 2;
+    return base + 2 * (env->C - 6);
+}
+
+int mrts_onehot_dev(mrts_env* env, const int32_t* d_obs, uint8_t* d_out, void* stream) {
+    try {
+        if (!d_obs || !d_out) throw Fail{-EINVAL, "null buffer"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(launchOneHot(d_obs, d_out, env->nSlots, env->HW, env->C, env->utt.ntypes, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
         return fail(f);

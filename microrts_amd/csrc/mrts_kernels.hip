@@ -2440,6 +2440,60 @@ size_t ldsBytes(int HW, int W, int CAP, int po) {
            (po ? 4 * (size_t)HW : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
 }
+// MicroRTS-Py GridnetVecEnv observation encoding (gym_microrts `_encode_obs`: clip each plane to
+// [0, n_k - 1], one-hot, channels-last): int32 obs [S][C][H][W] -> uint8 [S][H][W][F] with plane sizes
+// n = {5 hp, 5 resources, 3 owner, ntypes + 1 type, 6 action, 2 terrain, 2 per PO visibility plane}.
+// One thread per cell over the flattened (slot, cell) index; a block's 256 cells x F bytes are
+// composed in LDS and leave as aligned 16-byte stores (256 * F is a multiple of 16 for any F).
+struct OneHotParams {
+    const int32_t* obs;
+    uint8_t* out;
+    int32_t n_cells, HW, C, F;
+    int32_t sizes[8], offs[8];
+};
+__global__ __launch_bounds__(256) void k_onehot(OneHotParams Q) {
+    __shared__ __align__(16) uint8_t buf[256 * 40];
+    const int t = (int)threadIdx.x;
+    const int64_t i0 = (int64_t)blockIdx.x * 256, i = i0 + t;
+    const int F = Q.F;
+    for (int k = t; k < 256 * F / 4; k += 256) ((uint32_t*)buf)[k] = 0u;
+    __syncthreads();
+    if (i < Q.n_cells) {
+        const int64_t slot = i / Q.HW;
+        const int c = (int)(i - slot * Q.HW);
+        const int32_t* o = Q.obs + slot * Q.C * Q.HW + c;
+        for (int p = 0; p < Q.C; p++) {
+            const int v = min(max(o[(int64_t)p * Q.HW], 0), Q.sizes[p] - 1);
+            buf[t * F + Q.offs[p] + v] = 1;
+        }
+    }
+    __syncthreads();
+    const int64_t ncell = min((int64_t)256, (int64_t)Q.n_cells - i0);
+    const int64_t nbytes = ncell * F, n16 = nbytes / 16;
+    uint8_t* dst = Q.out + i0 * F;
+    for (int64_t k = t; k < n16; k += 256) ((uint4*)dst)[k] = ((const uint4*)buf)[k];
+    for (int64_t k = 16 * n16 + t; k < nbytes; k += 256) dst[k] = buf[k];
+}
+hipError_t launchOneHot(const int32_t* obs, uint8_t* out, int n_slots, int HW, int C, int ntypes, hipStream_t stream) {
+    OneHotParams Q;
+    Q.obs = obs;
+    Q.out = out;
+    Q.n_cells = n_slots * HW;
+    Q.HW = HW;
+    Q.C = C;
+    const int base[6] = {5, 5, 3, ntypes + 1, 6, 2};
+    int f = 0;
+    for (int p = 0; p < 8; p++) {
+        Q.sizes[p] = p < 6 ? base[p] : 2;
+        Q.offs[p] = f;
+        if (p < C) f += Q.sizes[p];
+    }
+    Q.F = f;
+    if (C > 8 || f > 40 || ((uintptr_t)out & 15)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_onehot, dim3((unsigned)((Q.n_cells + 255) / 256)), dim3(256), 0, stream, Q);
+    return hipGetLastError();
+}
+
 // int32 copy of a uint8 mask buffer (the Java int[][][][] layout), 16 mask bytes per thread
 __global__ __launch_bounds__(256) void k_widen(const uint8_t* __restrict__ in, int32_t* __restrict__ out, size_t n) {
     const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 16;

@@ -31,9 +31,13 @@ def gather_observations(obs, out=None, transport=torch.int16):
         out = torch.empty((world,) + tuple(obs.shape), dtype=transport, device=obs.device)
     if dist.get_backend() == "gloo":
         dist.all_gather(list(out.unbind(0)), send)
-    else:
-        dist.all_gather_into_tensor(out.view(-1), send.view(-1))
+    else:  # RCCL/NCCL has no int16 type: move the same bytes as float16 (a gather does no arithmetic)
+        dist.all_gather_into_tensor(_wire(out.view(-1)), _wire(send.view(-1)))
     return out
+
+
+def _wire(t):
+    return t.view(torch.float16) if t.dtype == torch.int16 else t
 
 
 class ObservationGather:
@@ -66,13 +70,16 @@ class ObservationGather:
         self.i = 0
 
     def _collective(self, b):
+        # RCCL has no int16 collectives: the int16 buffers travel as float16 views (pure byte moves)
+        send = _wire(self.send[b])
         if self.mode == "allgather":
             if self.gloo:
                 dist.all_gather(list(self.recv[b].unbind(0)), self.send[b])
             else:
-                dist.all_gather_into_tensor(self.recv[b].view(-1), self.send[b].view(-1))
+                dist.all_gather_into_tensor(_wire(self.recv[b]).view(-1), send.view(-1))
         else:
-            dist.gather(self.send[b], gather_list=list(self.recv[b].unbind(0)) if self.rank == 0 else None, dst=0)
+            recv = [_wire(x) for x in self.recv[b].unbind(0)] if self.rank == 0 else None
+            dist.gather(send, gather_list=recv, dst=0)
 
     def push(self, obs):
         """Call after the step that produced `obs`, on the compute stream.  Returns the receive

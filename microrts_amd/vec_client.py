@@ -292,6 +292,17 @@ class DeviceVecEnv:
                                           self._p(self.masks) if self.masks is not None else None, self.mask_player,
                                           self._s(stream)))
 
+    def onehot_obs(self, obs=None, out=None, stream=None):
+        """MicroRTS-Py's encoding of the observation (gym_microrts `_encode_obs`: clip + one-hot,
+        channels last): uint8 [slots][H][W][F], F = 29 (33 with partial observability)."""
+        h = self._h
+        F = h.L.mrts_onehot_features(h.h)
+        src = self.obs if obs is None else obs
+        if out is None:
+            out = self.torch.empty((h.S, h.H, h.W, F), dtype=self.torch.uint8, device=self.device)
+        _lib.check(h.L.mrts_onehot_dev(h.h, self._p(src), self._p(out), self._s(stream)))
+        return out
+
     def get_masks(self, out=None, stream=None):
         h = self._h
         out = self.masks if out is None else out

@@ -448,3 +448,39 @@ def test_bot_only_reward_functions():
             er, ed = r.step(0)
             assert np.array_equal(rw[j], er) and np.array_equal(dn[j], ed), f"env {j} step {step}: {rw[j]} {er}"
     env.close()
+
+
+def _encode_obs_np(obs, ntypes=7):
+    """numpy restatement of MicroRTS-Py's GridnetVecEnv `_encode_obs` (gym_microrts, external to the
+    reference — parity unpinned): per env, planes clipped to [0, n-1] and one-hot encoded, channels
+    last, plane sizes [5, 5, 3, ntypes + 1, 6, 2] (+ [2] per extra partial-observability plane)."""
+    S, C, H, W = obs.shape
+    sizes = [5, 5, 3, ntypes + 1, 6, 2] + [2] * (C - 6)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    out = np.zeros((S, H * W, sum(sizes)), np.uint8)
+    flat = obs.reshape(S, C, H * W)
+    for p in range(C):
+        v = np.clip(flat[:, p], 0, sizes[p] - 1)
+        np.put_along_axis(out, (v + offs[p])[..., None], 1, axis=2)
+    return out.reshape(S, H, W, -1)
+
+
+@pytest.mark.parametrize("mp,po", [("maps/16x16/basesWorkers16x16.xml", False), ("maps/10x10/basesWorkers10x10.xml", True),
+                                   ("maps/4x4/base4x4.xml", False)])
+def test_onehot_encoder(mp, po):
+    """mrts_onehot_dev = MicroRTS-Py's observation encoding of the step's int32 observation."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    env = DeviceVecEnv(6, 0, 2000, [mp] * 6, seed=3, partial_obs=po)
+    env.reset()
+    for step in range(60):
+        env.random_policy(SEED, step)
+        env.step()
+        if step % 10 == 9:
+            got = env.onehot_obs()
+            env.synchronize()
+            ref = _encode_obs_np(env.obs.cpu().numpy())
+            assert got.shape == ref.shape and got.shape[-1] == (33 if po else 29)
+            assert np.array_equal(got.cpu().numpy(), ref), f"step {step}"
+    env.close()
