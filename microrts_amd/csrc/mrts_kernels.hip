@@ -144,7 +144,7 @@ static_assert(sizeof(DevUtt) % 4 == 0 && UTT_WORDS <= 192, "DevUtt copy: 3 words
 
 struct Game {
     const KStatic& P;
-    const KDyn D;
+    const KDyn& D;  // the kernel argument itself (kernarg memory): fields load on demand
     const DevUtt& U;
     int g, H, W, HW, CAP;
     bool po;
@@ -157,6 +157,7 @@ struct Game {
     int32_t* rseq;   // ready-list scratch (64)
     uint32_t* mprev; // previous mask row sets, [2][maskWords(HW)] (delta mask writes)
     int32_t* rwc;    // reward counters [player][RC_*] of the pairs issued this step
+    int32_t* hdr;    // [32]: header words 0..15 (H_*) + HX_* extras
     int16_t* hp;
     int16_t* res;
     int16_t* par;    // UnitAction.parameter (direction / NONE duration)
@@ -164,8 +165,9 @@ struct Game {
     uint16_t* rslot; // ready-list scratch (64)
     uint8_t* snap;   // PO snapshot bits
     // wave-uniform scalars (only ever modified in uniform control flow)
-    int time, nu, pres0, pres1, seq, steps, ccnt, deaths, kind;
-    int snapLimit0, snapLimit1;  // seq counter when player 0 / 1's snapshot was taken
+    int time, nu, pres0, pres1, seq, deaths;
+    // Cold per-game scalars live in LDS (`hdr`), not in SGPRs: the header words H_* (steps, error
+    // flags, cancel counter, kind, the three java.util.Random states) plus the HX_* extras below.
     // issue index (valid while ixValid): `bits` = target cells (+W) of present MOVE/PRODUCE
     // assignments, whether any exists, per player the largest present PRODUCE cost (-1 = none) and
     // the sum of present PRODUCE costs
@@ -179,14 +181,13 @@ struct Game {
     int curP;              // player whose pa is being issued
     // CloserToEnemyBase/Unit: each player's first Base before the step (x | y << 8, -1 = none) and
     // the smallest squared distance from the OTHER player's mobile units to it, before the step
-    int basePos0, basePos1, oldSq0, oldSq1;
     int readySlot;         // per lane: the unit slot of ready item lane_id() (-1 outside cycle)
     int maxProd0, maxProd1, sumProd0, sumProd1;
-    uint32_t err;
-    JRand rngCancel, rngDamage, rngSampler;
 
-    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem)
-        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(d.H), W(d.W), HW(d.HW), CAP(d.CAP),
+    // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
+    // array offset then folds to an immediate), else the kernel arguments
+    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem, int h, int w, int hw, int cap)
+        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap),
           po(p.partial_obs != 0) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
@@ -197,6 +198,7 @@ struct Game {
         rseq = (int32_t*)q; q += 4 * 64;
         mprev = (uint32_t*)q; q += 8 * maskWords(HW);
         rwc = (int32_t*)q; q += 4 * 16;
+        hdr = (int32_t*)q; q += 4 * 32;
         scell = (uint32_t*)q; q += po ? 4 * HW : 0;
         hp = (int16_t*)q; q += 2 * CAP;
         res = (int16_t*)q; q += 2 * CAP;
@@ -204,13 +206,25 @@ struct Game {
         cell = (uint16_t*)q; q += 2 * HW;
         rslot = (uint16_t*)q; q += 2 * 64;
         snap = (uint8_t*)q;
-        snapLimit0 = snapLimit1 = 0;
         ixValid = false;
         killedLanes = 0;
         readySlot = -1;
         curP = 0;
-        basePos0 = basePos1 = -1;
-        oldSq0 = oldSq1 = INF;
+    }
+    // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
+    enum { HX_SNAP = 16, HX_BASE = 18, HX_OLDSQ = 20 };
+    DEV int hget(int i) const { return uni(hdr[i]); }
+    DEV void hset(int i, int v) const {
+        if (lane_id() == 0) hdr[i] = v;
+    }
+    DEV void addErr(uint32_t bits) const {
+        if (lane_id() == 0) hdr[H_ERR] |= (int32_t)bits;
+    }
+    DEV uint32_t errFlags() const { return (uint32_t)hget(H_ERR); }
+    DEV JRand rngLoad(int i) const { return JRand{rng_of(hget(i), hget(i + 1))}; }
+    DEV void rngStore(int i, const JRand& r) const {
+        hset(i, (int)(uint32_t)r.s);
+        hset(i + 1, (int)(uint32_t)(r.s >> 32));
     }
     DEV int pres(int p) const { return p == 0 ? pres0 : pres1; }
     DEV void addPres(int p, int v) {
@@ -280,14 +294,10 @@ struct Game {
         pres0 = rl(hv, H_RES0);
         pres1 = rl(hv, H_RES1);
         seq = rl(hv, H_SEQ);
-        steps = rl(hv, H_STEPS);
-        err = (uint32_t)rl(hv, H_ERR);
-        ccnt = rl(hv, H_CANCEL_CNT);
-        kind = rl(hv, H_KIND);
-        rngCancel.s = rng_of(rl(hv, H_RNG_CANCEL), rl(hv, H_RNG_CANCEL + 1));
-        rngDamage.s = rng_of(rl(hv, H_RNG_DAMAGE), rl(hv, H_RNG_DAMAGE + 1));
-        rngSampler.s = rng_of(rl(hv, H_RNG_SAMPLER), rl(hv, H_RNG_SAMPLER + 1));
         deaths = 0;
+        const int l = lane_id();
+        if (l < H_WORDS) hdr[l] = hv;
+        else if (l < 32) hdr[l] = (l >= HX_BASE && l < HX_BASE + 2) ? -1 : (l >= HX_OLDSQ && l < HX_OLDSQ + 2) ? INF : 0;
     }
     // One global round trip: header, unit rows 0..63 (speculative — CAP >= 64), the terrain and the
     // previous mask row sets are all in flight before the first wait.
@@ -342,23 +352,13 @@ struct Game {
     DEV void store() {
         int32_t* s = st();
         const int l = lane_id();
-        int hv = 0;
+        int hv = l < H_WORDS ? hdr[l] : 0;
         switch (l) {
             case H_TIME: hv = time; break;
             case H_NU: hv = nu; break;
             case H_RES0: hv = pres0; break;
             case H_RES1: hv = pres1; break;
             case H_SEQ: hv = seq; break;
-            case H_STEPS: hv = steps; break;
-            case H_ERR: hv = (int)err; break;
-            case H_CANCEL_CNT: hv = ccnt; break;
-            case H_KIND: hv = kind; break;
-            case H_RNG_CANCEL: hv = (int)(uint32_t)rngCancel.s; break;
-            case H_RNG_CANCEL + 1: hv = (int)(uint32_t)(rngCancel.s >> 32); break;
-            case H_RNG_DAMAGE: hv = (int)(uint32_t)rngDamage.s; break;
-            case H_RNG_DAMAGE + 1: hv = (int)(uint32_t)(rngDamage.s >> 32); break;
-            case H_RNG_SAMPLER: hv = (int)(uint32_t)rngSampler.s; break;
-            case H_RNG_SAMPLER + 1: hv = (int)(uint32_t)(rngSampler.s >> 32); break;
         }
         if (l < H_WORDS) s[l] = hv;
         int32_t* arr = s + H_WORDS;
@@ -378,7 +378,7 @@ struct Game {
         const int nu_t = t[T_NU];
         time = 0;
         seq = 0;
-        steps = 0;
+        hset(H_STEPS, 0);
         deaths = 0;
         pres0 = t[T_RES0];
         pres1 = t[T_RES1];
@@ -433,7 +433,7 @@ struct Game {
             for (int k = 0; k < 7; k++) b[k] = r[k];
             bad_any |= decodeRow(o, b);
         }
-        if (ballot(bad_any)) err |= E_PRODUCE_TYPE;
+        if (ballot(bad_any)) addErr(E_PRODUCE_TYPE);
         wsync();
     }
     // UnitAction.fromVectorAction of row a for unit o; returns "produce type out of range"
@@ -520,7 +520,7 @@ struct Game {
             }
             npairs += __popcll(acc);
         }
-        if (ballot(badAny)) err |= E_PRODUCE_TYPE;
+        if (ballot(badAny)) addErr(E_PRODUCE_TYPE);
         __threadfence();  // the pairs are read back (by other lanes) in rowsIssue
         return npairs;
     }
@@ -827,12 +827,15 @@ struct Game {
                 if (uni(at[os]) == time) {  // same-cycle conflict: policy (GameState.java:266-297)
                     bool cold = false, cnew = false;
                     if (U.crs == 2) {
-                        if (rngCancel.nextInt(2) == 0) cnew = true;
+                        JRand rc = rngLoad(H_RNG_CANCEL);
+                        if (rc.nextInt(2) == 0) cnew = true;
                         else cold = true;
+                        rngStore(H_RNG_CANCEL, rc);
                     } else if (U.crs == 3) {
-                        if ((ccnt % 2) == 0) cnew = true;
+                        const int cc = hget(H_CANCEL_CNT);
+                        if ((cc % 2) == 0) cnew = true;
                         else cold = true;
-                        ccnt++;
+                        hset(H_CANCEL_CNT, cc + 1);
                     } else {
                         cold = cnew = true;
                     }
@@ -846,7 +849,7 @@ struct Game {
                             if (po) {  // the mutated UAA object is shared with the PO snapshots holding it
                                 uint32_t b = snap[os];
                                 for (int q = 0; q < 2; q++)
-                                    if (snap_in(b, q) && snap_act(b, q) && as[os] < (q == 0 ? snapLimit0 : snapLimit1))
+                                    if (snap_in(b, q) && snap_act(b, q) && as[os] < hdr[HX_SNAP + q])
                                         b = (b & ~(7u << (2 + 3 * q))) | ((uint32_t)(T_NONE + 1) << (2 + 3 * q));
                                 snap[os] = (uint8_t)b;
                             }
@@ -867,7 +870,7 @@ struct Game {
                         if (pc >= 0) rwc[curP * RC_N + pc] -= 1;
                     }
                     orig = false;
-                    err |= E_OLDER;
+                    addErr(E_OLDER);
                     t = T_NONE;
                     prm = -1;
                     tx = ty = ut = 0;
@@ -1157,7 +1160,9 @@ struct Game {
         double total = 0.0;
         for (int i = 0; i < n5; i++) total += 5.0;
         for (int i = 0; i < n1; i++) total += 1.0;
-        const double tmp = rngSampler.nextDouble() * total;
+        JRand rs = rngLoad(H_RNG_SAMPLER);
+        const double tmp = rs.nextDouble() * total;
+        rngStore(H_RNG_SAMPLER, rs);
         int idx = -1;
         double accum = 0.0;
         for (int i = 0; i < n5 + n1; i++) {
@@ -1301,8 +1306,7 @@ struct Game {
                 snap[o] = (uint8_t)b;
             }
         }
-        if (p == 0) snapLimit0 = seq;
-        else snapLimit1 = seq;
+        hset(HX_SNAP + p, seq);
         wsync();
     }
     DEV void clearSnap() {
@@ -1333,7 +1337,7 @@ struct Game {
             case T_MOVE: {
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
                 if (!dead) {
-                    if (uni(cell[ny * W + nx]) != EMPTY) err |= E_COLLISION;
+                    if (uni(cell[ny * W + nx]) != EMPTY) addErr(E_COLLISION);
                     if (lane_id() == 0) {
                         cell[y * W + x] = EMPTY;
                         cell[ny * W + nx] = (uint16_t)s;
@@ -1346,7 +1350,11 @@ struct Game {
                 const int n = uni(cell[ua_ty(a) * W + ua_tx(a)]);
                 if (n < CAP) {
                     int dmg = U.minD[typ];
-                    if (U.minD[typ] != U.maxD[typ]) dmg = U.minD[typ] + rngDamage.nextInt(1 + (U.maxD[typ] - U.minD[typ]));
+                    if (U.minD[typ] != U.maxD[typ]) {
+                        JRand rd = rngLoad(H_RNG_DAMAGE);
+                        dmg = U.minD[typ] + rd.nextInt(1 + (U.maxD[typ] - U.minD[typ]));
+                        rngStore(H_RNG_DAMAGE, rd);
+                    }
                     const int nhp = uni(hp[n]) - dmg;
                     if (lane_id() == 0) hp[n] = (int16_t)nhp;
                     wsync();
@@ -1385,9 +1393,9 @@ struct Game {
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
                 if (pres(pl) - U.cost[ut] >= 0) {
                     if (uni(cell[ny * W + nx]) != EMPTY) {
-                        err |= E_ADDUNIT;  // PhysicalGameState.addUnit throws (:190-195)
+                        addErr(E_ADDUNIT);  // PhysicalGameState.addUnit throws (:190-195)
                     } else if (nu >= CAP) {
-                        err |= E_CAPACITY;
+                        addErr(E_CAPACITY);
                     } else {
                         if (lane_id() == 0) {
                             uc[nu] = pack_uc(nx, ny, ut, pl);
@@ -1403,7 +1411,7 @@ struct Game {
                         wsync();
                     }
                 } else {
-                    err |= E_NEG_RES;
+                    addErr(E_NEG_RES);
                 }
             } break;
             default: break;
@@ -1555,12 +1563,16 @@ struct Game {
             if (b0 < 0 && m0) b0 = o0 + __builtin_ctzll(m0);
             if (b1 < 0 && m1) b1 = o0 + __builtin_ctzll(m1);
         }
-        basePos0 = b0 >= 0 ? (int)(uniu(uc[b0]) & 0xFFFFu) : -1;
-        basePos1 = b1 >= 0 ? (int)(uniu(uc[b1]) & 0xFFFFu) : -1;
-        closerMin(oldSq0, oldSq1);
+        hset(HX_BASE, b0 >= 0 ? (int)(uniu(uc[b0]) & 0xFFFFu) : -1);
+        hset(HX_BASE + 1, b1 >= 0 ? (int)(uniu(uc[b1]) & 0xFFFFu) : -1);
+        int o0, o1;
+        closerMin(o0, o1);
+        hset(HX_OLDSQ, o0);
+        hset(HX_OLDSQ + 1, o1);
     }
     // smallest squared distance of player p's mobile units to the other player's base (INF if none)
     DEV void closerMin(int& sq0, int& sq1) {
+        const int basePos0 = hget(HX_BASE), basePos1 = hget(HX_BASE + 1);
         int m0 = INF, m1 = INF;
         for (int o = lane_id(); o < nu; o += 64) {
             const uint32_t c = uc[o];
@@ -1616,8 +1628,8 @@ struct Game {
                 case RF_ATTACK: r = (double)rwc[p * RC_N + RC_ATTACK]; break;
                 case RF_CLOSER_TO_ENEMY_BASE:
                 case RF_CLOSER_TO_ENEMY_UNIT:
-                    if ((p == 0 ? basePos1 : basePos0) >= 0)
-                        r = closerDist(p == 0 ? oldSq0 : oldSq1) - closerDist(p == 0 ? newSq0 : newSq1);
+                    if (hdr[HX_BASE + 1 - p] >= 0)
+                        r = closerDist(hdr[HX_OLDSQ + p]) - closerDist(p == 0 ? newSq0 : newSq1);
                     break;
             }
             if (D.reward) D.reward[(size_t)(slot0 + i) * R + j] = r;
@@ -2012,11 +2024,12 @@ DEV void aiGetAction(Game& G, int kind, int p) {
     if (kind == GK_RANDOM_BIASED) G.randomBiased(p);
 }
 
-template <int MODE>
+// FIX = 16: specialised for 16x16 maps (the c3/c4 benchmark size; CAP = 320), 0: any size
+template <int MODE, int FIX>
 __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
-    Game G(P, D, smem);
+    Game G(P, D, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FIX * FIX + 64 : D.CAP);
     // games [0, n_sp_games) are self-play (mrts_create's layout): no load needed to place the slots
     const bool selfplay = G.g < D.n_sp_games;
     const int slot0 = selfplay ? 2 * G.g : 2 * D.n_sp_games + (G.g - D.n_sp_games);
@@ -2033,8 +2046,8 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     if (MODE == MODE_RESET) {
         G.copyUtt();
         G.loadHeader(G.st());
-        G.kind = P.game_kind[G.g];
-        G.err = 0;
+        G.hset(H_KIND, P.game_kind[G.g]);
+        G.hset(H_ERR, 0);
         G.initCells();
         G.storeTerrain();
         G.resetFromTemplate();
@@ -2046,7 +2059,7 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     } else {
         G.load(D.mask_delta && D.masks);
     }
-    const int kind = G.kind;
+    const int kind = G.hget(H_KIND);
     const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
     if (G.po) G.clearSnap();
     PHASE(0);
@@ -2109,9 +2122,10 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         G.outcome(gameover, winner);
         // reward functions + VecClient auto-reset on done[0] or max steps, keeping the terminal
         // reward/done and forcing done[0] (tests/JNIGridnetVecClient.java:214-287)
-        G.steps++;
+        const int steps = G.hget(H_STEPS) + 1;
+        G.hset(H_STEPS, steps);
         const bool done0 = G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner);
-        const bool reset = done0 || G.steps >= P.max_steps;
+        const bool reset = done0 || steps >= P.max_steps;
         if (reset && D.done && lane_id() < nslots) D.done[(size_t)(slot0 + lane_id()) * P.n_rewards] = 1;
         if (reset) {
             G.resetFromTemplate();
@@ -2436,7 +2450,7 @@ hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts then [n] 
 }
 #endif
 size_t ldsBytes(int HW, int W, int CAP, int po) {
-    return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 +
+    return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 + 128 +
            (po ? 4 * (size_t)HW : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
 }
@@ -2518,17 +2532,21 @@ hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t st
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
     const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);
     dim3 grid((unsigned)hs.n_games), block(64);
+    const bool fix16 = hs.H == 16 && hs.W == 16 && hs.CAP == 16 * 16 + 64;
     switch (mode) {
-        case MODE_STEP: hipLaunchKernelGGL(k_env<MODE_STEP>, grid, block, lds, stream, ds, D); break;
-        case MODE_RESET: hipLaunchKernelGGL(k_env<MODE_RESET>, grid, block, lds, stream, ds, D); break;
-        default: hipLaunchKernelGGL(k_env<MODE_MASKS>, grid, block, lds, stream, ds, D); break;
+        case MODE_STEP:
+            if (fix16) hipLaunchKernelGGL((k_env<MODE_STEP, 16>), grid, block, lds, stream, ds, D);
+            else hipLaunchKernelGGL((k_env<MODE_STEP, 0>), grid, block, lds, stream, ds, D);
+            break;
+        case MODE_RESET: hipLaunchKernelGGL((k_env<MODE_RESET, 0>), grid, block, lds, stream, ds, D); break;
+        default: hipLaunchKernelGGL((k_env<MODE_MASKS, 0>), grid, block, lds, stream, ds, D); break;
     }
     return hipGetLastError();
 }
 hipError_t prepareLds(size_t bytes) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_env<MODE_STEP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_RESET>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_MASKS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    hipError_t e = hipFuncSetAttribute((const void*)k_env<MODE_STEP, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_RESET, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_MASKS, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     return e;
 }
 // *prevWritten: the launch recorded its candidate set in Q.prev (a later call may use the delta form)
