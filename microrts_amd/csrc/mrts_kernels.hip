@@ -186,9 +186,8 @@ struct Game {
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
     // array offset then folds to an immediate), else the kernel arguments
-    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem, int h, int w, int hw, int cap)
-        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap),
-          po(p.partial_obs != 0) {
+    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem, int h, int w, int hw, int cap, bool partial)
+        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), po(partial) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
         ua = (uint32_t*)q; q += 4 * CAP;
@@ -199,17 +198,14 @@ struct Game {
         mprev = (uint32_t*)q; q += 8 * maskWords(HW);
         rwc = (int32_t*)q; q += 4 * 16;
         hdr = (int32_t*)q; q += 4 * 32;
-        scell = (uint32_t*)q; q += po ? 4 * HW : 0;
         hp = (int16_t*)q; q += 2 * CAP;
         res = (int16_t*)q; q += 2 * CAP;
         par = (int16_t*)q; q += 2 * CAP;
         cell = (uint16_t*)q; q += 2 * HW;
         rslot = (uint16_t*)q; q += 2 * 64;
-        snap = (uint8_t*)q;
+        snap = (uint8_t*)q; q += (CAP + 3) & ~3;
+        scell = (uint32_t*)q;  // PO only, last: the offsets above do not depend on it
         ixValid = false;
-        killedLanes = 0;
-        readySlot = -1;
-        curP = 0;
     }
     // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
     enum { HX_SNAP = 16, HX_BASE = 18, HX_OLDSQ = 20 };
@@ -2024,14 +2020,16 @@ DEV void aiGetAction(Game& G, int kind, int p) {
     if (kind == GK_RANDOM_BIASED) G.randomBiased(p);
 }
 
-// FIX = 16: specialised for 16x16 maps (the c3/c4 benchmark size; CAP = 320), 0: any size
+// FIX = 16: specialised for batches of self-play 16x16 games, full observability, grid action
+// layout (the c3/c4 benchmark: CAP = 320; no PO, bot or Java-row code), 0: anything
 template <int MODE, int FIX>
 __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
-    Game G(P, D, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FIX * FIX + 64 : D.CAP);
+    Game G(P, D, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FIX * FIX + 64 : D.CAP,
+           FIX ? false : P.partial_obs != 0);
     // games [0, n_sp_games) are self-play (mrts_create's layout): no load needed to place the slots
-    const bool selfplay = G.g < D.n_sp_games;
+    const bool selfplay = FIX ? true : G.g < D.n_sp_games;
     const int slot0 = selfplay ? 2 * G.g : 2 * D.n_sp_games + (G.g - D.n_sp_games);
     const int nslots = selfplay ? 2 : 1;
     // agent-vs-bot: the agent's side; bot-vs-bot: the side ai1 plays (JNIBotClient.gameStep(player))
@@ -2059,7 +2057,7 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     } else {
         G.load(D.mask_delta && D.masks);
     }
-    const int kind = G.hget(H_KIND);
+    const int kind = FIX ? GT_SELFPLAY : G.hget(H_KIND);
     const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
     if (G.po) G.clearSnap();
     PHASE(0);
@@ -2069,13 +2067,14 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         if (P.reward_need & RN_COUNTS)
             if (lane_id() < 2 * RC_N) G.rwc[lane_id()] = 0;
         if (P.reward_need & RN_CLOSER) G.closerBefore();
-        if (D.rows && gtype == GT_SELFPLAY) {
+        const bool rowsMode = FIX ? false : D.rows != nullptr;
+        if (rowsMode && gtype == GT_SELFPLAY) {
             for (int p = 0; p < 2; p++) {
                 if (G.po) G.snapshot(p);
                 const int np = G.rowsDecode(p, D.rows + (size_t)(slot0 + p) * D.n_rows * 8);
                 G.rowsIssue(p, np, 1);
             }
-        } else if (D.rows && gtype == GT_AGENT_VS_BOT) {
+        } else if (rowsMode && gtype == GT_AGENT_VS_BOT) {
             if (G.po) {
                 G.snapshot(side);
                 G.snapshot(1 - side);
@@ -2452,7 +2451,7 @@ hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts then [n] 
 size_t ldsBytes(int HW, int W, int CAP, int po) {
     return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 + 128 +
            (po ? 4 * (size_t)HW : 0) +
-           6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (size_t)CAP;
+           6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (((size_t)CAP + 3) & ~(size_t)3);
 }
 // MicroRTS-Py GridnetVecEnv observation encoding (gym_microrts `_encode_obs`: clip each plane to
 // [0, n_k - 1], one-hot, channels-last): int32 obs [S][C][H][W] -> uint8 [S][H][W][F] with plane sizes
@@ -2532,7 +2531,8 @@ hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t st
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
     const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);
     dim3 grid((unsigned)hs.n_games), block(64);
-    const bool fix16 = hs.H == 16 && hs.W == 16 && hs.CAP == 16 * 16 + 64;
+    const bool fix16 = hs.H == 16 && hs.W == 16 && hs.CAP == 16 * 16 + 64 && !hs.partial_obs &&
+                       hs.n_sp_games == hs.n_games && D.rows == nullptr;
     switch (mode) {
         case MODE_STEP:
             if (fix16) hipLaunchKernelGGL((k_env<MODE_STEP, 16>), grid, block, lds, stream, ds, D);
