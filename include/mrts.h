@@ -79,6 +79,9 @@ typedef struct {
                                    reward / done become [n_slots][n_rewards]; the auto-reset follows done
                                    of the FIRST function (rs.done[0], :247,272) */
     int32_t n_rewards;          /* 0..8 */
+    int32_t forward_model;      /* 1 (with ai1_kinds): a batched forward model for search AIs instead of the
+                                   bot-only client: games advance only through mrts_playout*, never
+                                   auto-reset; ai1_kinds / bot_kinds are players 0 / 1's playout policies */
 } mrts_config;
 
 typedef struct {               /* ai/jni/Responses.java:12-30 */
@@ -143,6 +146,26 @@ int mrts_set_source_output(mrts_env* env, uint32_t* d_source);
  * d_out 16-byte aligned. */
 int mrts_onehot_features(const mrts_env* env);
 int mrts_onehot_dev(mrts_env* env, const int32_t* d_obs, uint8_t* d_out, void* stream);
+
+/* Batched forward model for search AIs: GameState.clone() + playouts + evaluation,
+ * as NaiveMCTS / ModelledEvaluationMCTS use the engine.  Games of a forward-model handle are its slots
+ * (one per game); a self-play handle's game g holds its slots 2g and 2g+1. */
+#define MRTS_MAX_HORIZON 65536
+/* GameState.clone() (rts/GameState.java:591-610) for pairs [n][2] = (dst game, src game): dst games of
+ * the forward-model handle `dst`, src games of `src` (any handle with the same map size and unit-type
+ * table on the same device; NULL = dst).  A dst game keeps its own random streams and playout
+ * policies.  No game may be both a source and a destination, nor a destination twice (the host form
+ * checks; the device form skips out-of-range pairs and is stream-ordered on `stream` only). */
+int mrts_copy_games(mrts_env* dst, const mrts_env* src, const int32_t* pairs, int32_t n);
+int mrts_copy_games_dev(mrts_env* dst, const mrts_env* src, const int32_t* d_pairs, int32_t n, void* stream);
+/* NaiveMCTS.simulate(gs, gs.getTime() + horizon) (ai/mcts/naivemcts/NaiveMCTS.java:297-308) on every
+ * game of a forward-model handle, each with its own policies; |horizon| <= MRTS_MAX_HORIZON. */
+int mrts_playout(mrts_env* env, int32_t horizon);
+int mrts_playout_dev(mrts_env* env, int32_t horizon, void* stream);
+/* SimpleSqrtEvaluationFunction3.evaluate(maxplayer, 1 - maxplayer, gs)
+ * (ai/evaluation/SimpleSqrtEvaluationFunction3.java:24-44) of every game: float [n_games] */
+int mrts_evaluate(mrts_env* env, int32_t maxplayer, float* out);
+int mrts_evaluate_dev(mrts_env* env, int32_t maxplayer, float* d_out, void* stream);
 
 /* Canonical state dump of the game behind `slot` (same format as the CPU oracle's dumpState):
  * [time, 2, res0, res1, n_units, (type, player, x, y, hp, resources)*, n_assignments,

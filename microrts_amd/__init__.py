@@ -2,6 +2,6 @@
 
 Drop-in for tests.JNIGridnetVecClient of the reference (src/tests/JNIGridnetVecClient.java).
 """
-from .vec_client import JNIGridnetVecClient, UnitTypeTable, DeviceVecEnv  # noqa: F401
+from .vec_client import JNIGridnetVecClient, UnitTypeTable, DeviceVecEnv, ForwardModel  # noqa: F401
 
-__all__ = ["JNIGridnetVecClient", "UnitTypeTable", "DeviceVecEnv"]
+__all__ = ["JNIGridnetVecClient", "UnitTypeTable", "DeviceVecEnv", "ForwardModel"]

@@ -7,6 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmrts.so")
 
 MRTS_BOT_PASSIVE, MRTS_BOT_RANDOM_BIASED = 0, 1
+MRTS_MAX_HORIZON = 65536
 # a_rfs names (src/ai/reward/*.java) -> MRTS_RF_* ids
 REWARD_FUNCTIONS = {"WinLossRewardFunction": 0, "ResourceGatherRewardFunction": 1, "ProduceWorkerRewardFunction": 2,
                     "ProduceBuildingRewardFunction": 3, "AttackRewardFunction": 4, "ProduceCombatUnitRewardFunction": 5,
@@ -19,7 +20,8 @@ ERR_BITS = {
 # every symbol include/mrts.h declares
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_step_rows", "mrts_get_masks_i32",
-    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_copy_games", "mrts_copy_games_dev", "mrts_playout", "mrts_playout_dev",
+    "mrts_evaluate", "mrts_evaluate_dev", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
 ]
 
@@ -41,6 +43,7 @@ class MrtsConfig(ctypes.Structure):
         ("mask_delta", ctypes.c_int32),
         ("reward_kinds", ctypes.POINTER(ctypes.c_int32)),
         ("n_rewards", ctypes.c_int32),
+        ("forward_model", ctypes.c_int32),
     ]
 
 
@@ -90,6 +93,12 @@ def load(path=LIB_PATH):
     L.mrts_policy_dev.argtypes = [P, P, P, U64, U32, P, P]
     L.mrts_policy_invalidate.argtypes = [P]
     L.mrts_set_source_output.argtypes = [P, P]
+    L.mrts_copy_games.argtypes = [P, P, P, I32]
+    L.mrts_copy_games_dev.argtypes = [P, P, P, I32, P]
+    L.mrts_playout.argtypes = [P, I32]
+    L.mrts_playout_dev.argtypes = [P, I32, P]
+    L.mrts_evaluate.argtypes = [P, I32, P]
+    L.mrts_evaluate_dev.argtypes = [P, I32, P, P]
     L.mrts_get_state.argtypes = [P, I32, P, I32]
     L.mrts_error_flags.argtypes = [P, P]
     L.mrts_env_steps.argtypes = [P, P]

@@ -29,6 +29,9 @@ hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream, bool* prevWri
 hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t stream);
 hipError_t launchOneHot(const int32_t* obs, uint8_t* out, int n_slots, int HW, int C, int ntypes, hipStream_t stream);
 hipError_t prepareLds(size_t bytes);
+hipError_t launchCopyGames(int32_t* dst, const int32_t* src, const int32_t* pairs, int n, int n_dst, int n_src,
+                           int CAP, int HW, hipStream_t stream);
+hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, float* out, hipStream_t stream);
 }  // namespace mrts
 
 static thread_local std::string g_err;
@@ -254,6 +257,7 @@ struct mrts_env {
     hipStream_t stream = nullptr;
     int H = 0, W = 0, HW = 0, CAP = 0, C = 6, K = 79;
     int nSlots = 0, nGames = 0, nSpGames = 0, maxSteps = 0, partialObs = 0;
+    int forwardModel = 0;  // games advance through mrts_playout* only (GT_PLAYOUT)
     uint32_t slotIdBase = 0;
     DevUtt utt;
     std::vector<int> tmplOffHost;
@@ -289,6 +293,9 @@ struct mrts_env {
     int32_t* d_rowsStage = nullptr;
     size_t rowsStageInts = 0;
     int32_t* d_masks32 = nullptr;
+    int32_t* d_copyPairs = nullptr;  // mrts_copy_games staging
+    int copyPairsCap = 0;
+    float* d_eval = nullptr;         // mrts_evaluate staging
     std::vector<int32_t> rewardKinds{RF_WINLOSS};  // a_rfs
     const int32_t* lastPolicyActions = nullptr;
     bool polValid = false;
@@ -404,12 +411,16 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
                 if (k < 0 || k >= RF_COUNT) throw Fail{-EINVAL, "unknown reward function"};
         }
         if (cfg->ai1_kinds && cfg->n_selfplay_slots) throw Fail{-EINVAL, "the bot-only client has no self-play slots"};
+        env->forwardModel = cfg->forward_model ? 1 : 0;
+        if (env->forwardModel && !cfg->ai1_kinds) throw Fail{-EINVAL, "a forward model needs ai1_kinds (player 0's playout policy)"};
+        if (env->forwardModel && cfg->partial_obs) throw Fail{-EINVAL, "a forward model plays on the full state (partial_obs must be 0)"};
         env->gameKindHost.assign((size_t)env->nGames, 0);  // self-play = 0
         for (int j = 0; j < cfg->n_bot_envs; j++) {
             const int k2 = cfg->bot_kinds ? cfg->bot_kinds[j] : MRTS_BOT_PASSIVE;
             const int k1 = cfg->ai1_kinds ? cfg->ai1_kinds[j] : MRTS_BOT_PASSIVE;
             if (k1 < 0 || k1 > 1 || k2 < 0 || k2 > 1) throw Fail{-ENOTSUP, "only PassiveAI / RandomBiasedAI are native"};
-            env->gameKindHost[(size_t)(env->nSpGames + j)] = (cfg->ai1_kinds ? 2 : 1) | (k1 << 4) | (k2 << 8);
+            const int type = env->forwardModel ? 3 : (cfg->ai1_kinds ? 2 : 1);  // GT_PLAYOUT / BOT_VS_BOT / AGENT_VS_BOT
+            env->gameKindHost[(size_t)(env->nSpGames + j)] = type | (k1 << 4) | (k2 << 8);
         }
         // maps: one template per distinct path
         std::map<std::string, int> tmplIndex;
@@ -554,6 +565,7 @@ int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, doub
 int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                   uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream) {
     try {
+        if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
         if (!d_actions) throw Fail{-EINVAL, "actions is null"};
         HIPCHK(hipSetDevice(env->device));
         KDyn D;
@@ -576,6 +588,7 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
 int mrts_step_rows_dev(mrts_env* env, const int32_t* d_rows, int32_t n_rows, const int32_t* d_players, int32_t* d_obs,
                        double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream) {
     try {
+        if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
         if (!d_rows && n_rows > 0) throw Fail{-EINVAL, "rows is null"};
         if (n_rows < 0 || (size_t)n_rows * env->nSlots * 8 >= ((size_t)1 << 31)) throw Fail{-EINVAL, "bad n_rows"};
         HIPCHK(hipSetDevice(env->device));
@@ -890,6 +903,8 @@ void mrts_destroy(mrts_env* env) {
     (void)hipFree(env->d_pairs);
     (void)hipFree(env->d_rowsStage);
     (void)hipFree(env->d_masks32);
+    (void)hipFree(env->d_copyPairs);
+    (void)hipFree(env->d_eval);
     (void)hipFree(env->d_tmpl);
     (void)hipFree(env->d_tmplOff);
     (void)hipFree(env->d_gameKind);
@@ -904,6 +919,118 @@ void mrts_destroy(mrts_env* env) {
     (void)hipHostFree(env->h_done);
     if (env->stream) (void)hipStreamDestroy(env->stream);
     delete env;
+}
+
+// ---------------------------------------------------------------- forward model
+static void checkCopy(const mrts_env* dst, const mrts_env* src) {
+    if (!dst || !src) throw Fail{-EINVAL, "null handle"};
+    if (!dst->forwardModel) throw Fail{-EINVAL, "copy destination must be a forward-model handle"};
+    if (src->H != dst->H || src->W != dst->W || src->CAP != dst->CAP) throw Fail{-EINVAL, "handles differ in map size"};
+    if (std::memcmp(&src->utt, &dst->utt, sizeof(DevUtt)) != 0) throw Fail{-EINVAL, "handles differ in unit-type table"};
+    if (src->device != dst->device) throw Fail{-EINVAL, "handles live on different devices"};
+}
+
+int mrts_copy_games_dev(mrts_env* dst, const mrts_env* src, const int32_t* d_pairs, int32_t n, void* stream) {
+    try {
+        if (!src) src = dst;
+        checkCopy(dst, src);
+        if (n < 0 || (n > 0 && !d_pairs)) throw Fail{-EINVAL, "bad pairs"};
+        HIPCHK(hipSetDevice(dst->device));
+        HIPCHK(launchCopyGames(dst->d_state, src->d_state, d_pairs, n, dst->nGames, src->nGames, dst->CAP, dst->HW,
+                               pickStream(dst, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_copy_games(mrts_env* dst, const mrts_env* src, const int32_t* pairs, int32_t n) {
+    try {
+        if (!src) src = dst;
+        checkCopy(dst, src);
+        if (n < 0 || (n > 0 && !pairs)) throw Fail{-EINVAL, "bad pairs"};
+        std::vector<char> isDst((size_t)dst->nGames, 0), isSrc((size_t)src->nGames, 0);
+        for (int i = 0; i < n; i++) {
+            const int d = pairs[2 * i], s = pairs[2 * i + 1];
+            if (d < 0 || d >= dst->nGames || s < 0 || s >= src->nGames) throw Fail{-EINVAL, "game index out of range"};
+            if (isDst[(size_t)d]) throw Fail{-EINVAL, "a destination game appears twice"};
+            isDst[(size_t)d] = 1;
+            isSrc[(size_t)s] = 1;
+        }
+        if (src == dst)
+            for (int g = 0; g < dst->nGames; g++)
+                if (isDst[(size_t)g] && isSrc[(size_t)g]) throw Fail{-EINVAL, "a game is both a source and a destination"};
+        if (n == 0) return 0;
+        HIPCHK(hipSetDevice(dst->device));
+        HIPCHK(hipStreamSynchronize(src->stream));
+        if (n > dst->copyPairsCap) {
+            HIPCHK(hipStreamSynchronize(dst->stream));
+            (void)hipFree(dst->d_copyPairs);
+            dst->d_copyPairs = nullptr;
+            HIPCHK(hipMalloc(&dst->d_copyPairs, (size_t)n * 2 * 4));
+            dst->copyPairsCap = n;
+        }
+        HIPCHK(hipMemcpyAsync(dst->d_copyPairs, pairs, (size_t)n * 2 * 4, hipMemcpyHostToDevice, dst->stream));
+        HIPCHK(launchCopyGames(dst->d_state, src->d_state, dst->d_copyPairs, n, dst->nGames, src->nGames, dst->CAP,
+                               dst->HW, dst->stream));
+        HIPCHK(hipStreamSynchronize(dst->stream));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_playout_dev(mrts_env* env, int32_t horizon, void* stream) {
+    try {
+        if (!env || !env->forwardModel) throw Fail{-EINVAL, "not a forward-model handle"};
+        if (horizon < -MRTS_MAX_HORIZON || horizon > MRTS_MAX_HORIZON) throw Fail{-EINVAL, "horizon out of range"};
+        HIPCHK(hipSetDevice(env->device));
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.horizon = horizon;
+        HIPCHK(env->launch(3, D, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_playout(mrts_env* env, int32_t horizon) {
+    try {
+        int r = mrts_playout_dev(env, horizon, env ? env->stream : nullptr);
+        if (r) return r;
+        HIPCHK(hipStreamSynchronize(env->stream));
+        checkFlagsAfter(env);
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_evaluate_dev(mrts_env* env, int32_t maxplayer, float* d_out, void* stream) {
+    try {
+        if (!env || !d_out) throw Fail{-EINVAL, "null argument"};
+        if (maxplayer != 0 && maxplayer != 1) throw Fail{-EINVAL, "maxplayer must be 0 or 1"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(launchEvaluate(env->hstatic, env->d_static, maxplayer, d_out, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_evaluate(mrts_env* env, int32_t maxplayer, float* out) {
+    try {
+        if (!env || !out) throw Fail{-EINVAL, "null argument"};
+        if (!env->d_eval) HIPCHK(hipMalloc(&env->d_eval, (size_t)env->nGames * 4));
+        int r = mrts_evaluate_dev(env, maxplayer, env->d_eval, env->stream);
+        if (r) return r;
+        HIPCHK(hipMemcpyAsync(out, env->d_eval, (size_t)env->nGames * 4, hipMemcpyDeviceToHost, env->stream));
+        HIPCHK(hipStreamSynchronize(env->stream));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
 }
 
 #ifdef MRTS_PHASE_TIMING

@@ -101,6 +101,7 @@ struct KDyn {
     const int32_t* rows;           // Java row layout [n_slots][n_rows][8] (replaces `actions`) or null
     int32_t n_rows;
     uint32_t* pairs;               // rows mode: per game [n_rows][2] accepted-pair scratch
+    int32_t horizon;               // playout mode: NaiveMCTS.simulate(gs, gs.getTime() + horizon)
 };
 
 struct PolicyParams {

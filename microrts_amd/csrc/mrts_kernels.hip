@@ -27,7 +27,7 @@ namespace {
 constexpr uint16_t EMPTY = 0xFFFF, WALL = 0xFFFE;
 constexpr int INF = 0x7FFFFFFF;
 enum { T_NONE = 0, T_MOVE = 1, T_HARVEST = 2, T_RETURN = 3, T_PRODUCE = 4, T_ATTACK = 5 };
-enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2 };
+enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2, MODE_PLAYOUT = 3 };
 
 // Diagnostic build only (-DMRTS_PHASE_TIMING, tools/phase_timing.py): per-phase shader-clock cycles
 // summed over games; not compiled into libmrts.so.
@@ -51,7 +51,7 @@ __device__ unsigned long long g_span[2 * PH_GAMES];    // last launch: [game] st
     do {          \
     } while (0)
 #endif
-enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2 };  // game_kind & 15
+enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2, GT_PLAYOUT = 3 };  // game_kind & 15
 // per-player counters of this step's issued pairs, as the TraceEntry holds them (after issueSafe's
 // legality rewrite, before issue()'s conflict cancellations): HARVEST, RETURN, ATTACK, and PRODUCE
 // of a Worker / a Base or Barracks / a Light, Heavy or Ranged
@@ -1503,6 +1503,18 @@ struct Game {
         gameover = (c0 + c1 == 0) || ((c0 > 0) != (c1 > 0));
         winner = (c0 > 0 && c1 == 0) ? 0 : ((c1 > 0 && c0 == 0) ? 1 : -1);
     }
+    // GameState.isComplete (rts/GameState.java:148-157): every owned unit has an assignment
+    DEV bool complete() const {
+        bool idle = false;
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            if (o < nu) {
+                const uint32_t c = uc[o];
+                idle |= !(c & UC_DEAD) && uplay(c) >= 0 && !(ua[o] & UA_PRESENT);
+            }
+        }
+        return ballot(idle) == 0;
+    }
     // order-preserving removal of dead slots (LinkedList.remove, PhysicalGameState.java:208-210)
     DEV void compact() {
         int base = 0;
@@ -2062,6 +2074,39 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     if (G.po) G.clearSnap();
     PHASE(0);
 
+    if (MODE == MODE_PLAYOUT) {
+        // NaiveMCTS.simulate (ai/mcts/naivemcts/NaiveMCTS.java:297-308, the same loop as
+        // ai/AALL/mcts/ModelledEvaluationMCTS.java:313-324): do { if (isComplete()) gameover = cycle();
+        // else { issue(policy.getAction(0)); issue(policy.getAction(1)); } } while (!gameover &&
+        // time < until).  The policies give every idle unit an action, so after an issue pass the
+        // state is complete: one pass below = [issue pass if incomplete] + cycle.  The state stays in
+        // LDS for the whole playout; time grows by one per pass, so every wave reaches the exit.
+        const int until = G.time + D.horizon;
+        bool first = true;
+        for (;;) {
+            if (!G.complete()) {
+                aiGetAction(G, ai1, 0);
+                G.issuePlayer(0, 10, true);
+                aiGetAction(G, ai2, 1);
+                G.issuePlayer(1, 10, true);
+                if (first && G.time >= until) break;  // the do-while's first test follows the issue pass
+            }
+            first = false;
+            G.cycle();
+            bool over;
+            int winner;
+            G.outcome(over, winner);
+            if (G.deaths) {
+                G.compact();
+                G.deaths = 0;
+            }
+            if (over || G.time >= until) break;
+        }
+        wsync();
+        G.store();
+        return;
+    }
+
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
         if (P.reward_need & RN_COUNTS)
@@ -2528,6 +2573,87 @@ hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t st
     hipLaunchKernelGGL(k_widen, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, in, out, n);
     return hipGetLastError();
 }
+// ---------------------------------------------------------------- forward model
+// GameState.clone() (rts/GameState.java:591-610) of pairs (dst game, src game): units, players,
+// time, the cancel counter and the assignments (LinkedHashMap order = the sequence numbers) travel;
+// the dst game keeps its own random streams (Sampler.generator / GameState.r / UnitAction.r are
+// JVM-global, not part of a GameState), its kind (playout policies), and its mask row sets (they
+// describe the dst handle's mask buffer).  One block of 256 threads per pair.
+__global__ __launch_bounds__(256) void k_copy_games(int32_t* __restrict__ dst, const int32_t* __restrict__ src,
+                                                    const int32_t* __restrict__ pairs, int n_dst, int n_src,
+                                                    int words, int maskLo, int maskHi) {
+    const int d = pairs[2 * blockIdx.x], s = pairs[2 * blockIdx.x + 1];
+    if (d < 0 || d >= n_dst || s < 0 || s >= n_src) return;
+    int32_t* o = dst + (size_t)d * words;
+    const int32_t* i = src + (size_t)s * words;
+    for (int w = threadIdx.x; w < words; w += 256) {
+        const bool keep = (w >= H_RNG_CANCEL && w <= H_KIND) || (w >= maskLo && w < maskHi);
+        if (!keep) o[w] = w == H_STEPS ? 0 : i[w];
+    }
+}
+hipError_t launchCopyGames(int32_t* dst, const int32_t* src, const int32_t* pairs, int n, int n_dst, int n_src,
+                           int CAP, int HW, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const int lo = H_WORDS + N_ARRAYS * CAP;
+    hipLaunchKernelGGL(k_copy_games, dim3((unsigned)n), dim3(256), 0, stream, dst, src, pairs, n_dst, n_src,
+                       stateWords(CAP, HW), lo, lo + 2 * maskWords(HW));
+    return hipGetLastError();
+}
+
+// SimpleSqrtEvaluationFunction3.evaluate(maxplayer, 1 - maxplayer, gs)
+// (ai/evaluation/SimpleSqrtEvaluationFunction3.java:24-44), Java float semantics: the unit loop runs
+// in list order, `score += res * 10f` is a float add, `score += 40f * cost * Math.sqrt(hp / maxHp)`
+// (integer division) is a double add rounded back to float; no contraction into FMAs.  One wave per
+// game: lanes load 64 units at a time, every lane runs the same ordered sum over readlane values.
+__global__ __launch_bounds__(64) void k_evaluate(const KStatic* __restrict__ PS, const int32_t* __restrict__ state,
+                                                 int words, int CAP, int maxplayer, float* __restrict__ out) {
+#pragma clang fp contract(off)
+    const KStatic& P = *PS;
+    const int32_t* s = state + (size_t)blockIdx.x * words;
+    const int nu = uni(s[H_NU]);
+    const int l = lane_id();
+    float score[2];
+    bool any[2] = {false, false};
+    score[0] = __fmul_rn((float)uni(s[H_RES0]), 20.0f);
+    score[1] = __fmul_rn((float)uni(s[H_RES1]), 20.0f);
+    for (int o0 = 0; o0 < nu; o0 += 64) {
+        const int o = o0 + l;
+        uint32_t c = UC_DEAD;
+        int hpv = 0, rv = 0;
+        if (o < nu) {
+            c = (uint32_t)s[H_WORDS + A_UC * CAP + o];
+            hpv = s[H_WORDS + A_HP * CAP + o];
+            rv = s[H_WORDS + A_RES * CAP + o];
+        }
+        const int n = min(64, nu - o0);
+        for (int k = 0; k < n; k++) {
+            const uint32_t ck = (uint32_t)rl((int)c, k);
+            if (ck & UC_DEAD) continue;
+            const int p = uplay(ck);
+            if (p != 0 && p != 1) continue;
+            const int typ = utyp(ck);
+            const int h = rl(hpv, k), r = rl(rv, k);
+            float sc = score[p];
+            sc = __fadd_rn(sc, __fmul_rn((float)r, 10.0f));
+            const double bonus = __dmul_rn((double)__fmul_rn(40.0f, (float)P.utt.cost[typ]),
+                                           __builtin_sqrt((double)(h / P.utt.hp[typ])));
+            sc = (float)__dadd_rn((double)sc, bonus);
+            score[p] = sc;
+            any[p] = true;
+        }
+    }
+    const float s1 = any[maxplayer] ? score[maxplayer] : 0.0f;
+    const float s2 = any[1 - maxplayer] ? score[1 - maxplayer] : 0.0f;
+    const float tot = __fadd_rn(s1, s2);
+    const float v = tot == 0.0f ? 0.5f : __fsub_rn(__fdiv_rn(__fmul_rn(2.0f, s1), tot), 1.0f);
+    if (l == 0) out[blockIdx.x] = v;
+}
+hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, float* out, hipStream_t stream) {
+    hipLaunchKernelGGL(k_evaluate, dim3((unsigned)hs.n_games), dim3(64), 0, stream, ds, hs.state,
+                       stateWords(hs.CAP, hs.HW), hs.CAP, maxplayer, out);
+    return hipGetLastError();
+}
+
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
     const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);
     dim3 grid((unsigned)hs.n_games), block(64);
@@ -2539,7 +2665,8 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
             else hipLaunchKernelGGL((k_env<MODE_STEP, 0>), grid, block, lds, stream, ds, D);
             break;
         case MODE_RESET: hipLaunchKernelGGL((k_env<MODE_RESET, 0>), grid, block, lds, stream, ds, D); break;
-        default: hipLaunchKernelGGL((k_env<MODE_MASKS, 0>), grid, block, lds, stream, ds, D); break;
+        case MODE_PLAYOUT: hipLaunchKernelGGL((k_env<MODE_PLAYOUT, 0>), grid, block, lds, stream, ds, D); break;
+        default:hipLaunchKernelGGL((k_env<MODE_MASKS, 0>), grid, block, lds, stream, ds, D); break;
     }
     return hipGetLastError();
 }
@@ -2547,6 +2674,7 @@ hipError_t prepareLds(size_t bytes) {
     hipError_t e = hipFuncSetAttribute((const void*)k_env<MODE_STEP, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_RESET, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_MASKS, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_PLAYOUT, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     return e;
 }
 // *prevWritten: the launch recorded its candidate set in Q.prev (a later call may use the delta form)

@@ -80,7 +80,7 @@ def _kinds(ais, n):
 
 class _Handle:
     def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base,
-                 ai1s=None, mask_delta=False, rewards=None):
+                 ai1s=None, mask_delta=False, rewards=None, forward_model=False):
         L = _lib.load()
         self.L = L
         self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
@@ -94,7 +94,7 @@ class _Handle:
                               ctypes.cast(self._kinds, P32),
                               ctypes.cast(self._ai1, P32) if self._ai1 is not None else None,
                               ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base,
-                              int(bool(mask_delta)), ctypes.cast(self._rk, P32), self.R)
+                              int(bool(mask_delta)), ctypes.cast(self._rk, P32), self.R, int(bool(forward_model)))
         h = ctypes.c_void_p()
         _lib.check(L.mrts_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -337,6 +337,85 @@ class DeviceVecEnv:
     def dims(self):
         h = self._h
         return h.S, h.H, h.W, h.C, h.K
+
+    def close(self):
+        self.synchronize()
+        self._h.close()
+
+
+class ForwardModel:
+    """Batched forward model for search AIs: n games kept in HBM, each advanced by
+    NaiveMCTS.simulate (ai/mcts/naivemcts/NaiveMCTS.java:297-308) with its own playout policies
+    (RandomBiasedAI / PassiveAI for players 0 and 1), cloned from any handle's games with
+    GameState.clone() semantics (rts/GameState.java:591-610), and scored with
+    SimpleSqrtEvaluationFunction3.  Game j's java.util.Random streams are seeded from seed + j (see
+    DESIGN.md).  Device calls are ordered on torch's current stream of the device."""
+
+    def __init__(self, n_games, map_path, policies=("RandomBiasedAI", "RandomBiasedAI"), utt=None, device=0, seed=0):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("ForwardModel needs an MI355X (torch.cuda is unavailable); there is no CPU fallback")
+        self.torch = torch
+        utt = utt or UnitTypeTable()
+        p0, p1 = policies
+        p0 = p0 if isinstance(p0, (list, tuple)) else [p0] * n_games
+        p1 = p1 if isinstance(p1, (list, tuple)) else [p1] * n_games
+        self._h = _Handle(0, n_games, 1 << 30, [_resolve("", map_path)] * n_games, p1, utt, False, device, seed, 0,
+                          ai1s=p0, forward_model=True)
+        self.n = n_games
+        self.device = torch.device("cuda", device)
+        self.value = torch.zeros(n_games, dtype=torch.float32, device=self.device)
+        torch.cuda.synchronize(self.device)
+
+    def _s(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self):
+        """Every game back to its map's initial state (random streams continue)."""
+        h = self._h
+        _lib.check(h.L.mrts_reset_dev(h.h, None, None, None, None, None, 0, self._s()))
+
+    def copy_from(self, pairs, src=None):
+        """gs[dst] = src_games[src_game].clone() for (dst, src_game) rows of `pairs` (int32 [n, 2]: a
+        torch tensor on this device, or anything numpy accepts).  src: a DeviceVecEnv,
+        JNIGridnetVecClient or ForwardModel with the same map size (None = self)."""
+        h = self._h
+        sh = h.h if src is None else src._h.h
+        if isinstance(pairs, self.torch.Tensor) and pairs.is_cuda:
+            assert pairs.dtype == self.torch.int32 and pairs.is_contiguous() and pairs.dim() == 2 and pairs.shape[1] == 2
+            if src is not None and hasattr(src, "synchronize"):
+                src.synchronize()
+            _lib.check(h.L.mrts_copy_games_dev(h.h, sh, ctypes.c_void_p(pairs.data_ptr()), pairs.shape[0], self._s()))
+        else:
+            pr = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32).reshape(-1, 2))
+            self.synchronize()
+            _lib.check(h.L.mrts_copy_games(h.h, sh, pr.ctypes.data_as(ctypes.c_void_p), pr.shape[0]))
+
+    def playout(self, horizon):
+        """NaiveMCTS.simulate(gs, gs.getTime() + horizon) on every game (one launch)."""
+        if not -_lib.MRTS_MAX_HORIZON <= horizon <= _lib.MRTS_MAX_HORIZON:
+            raise ValueError("horizon out of range")
+        h = self._h
+        _lib.check(h.L.mrts_playout_dev(h.h, int(horizon), self._s()))
+
+    def evaluate(self, maxplayer=0, out=None):
+        """SimpleSqrtEvaluationFunction3.evaluate(maxplayer, 1 - maxplayer, gs): float32 [n] on device."""
+        h = self._h
+        out = self.value if out is None else out
+        _lib.check(h.L.mrts_evaluate_dev(h.h, int(maxplayer), ctypes.c_void_p(out.data_ptr()), self._s()))
+        return out
+
+    def synchronize(self):
+        self.torch.cuda.current_stream(self.device).synchronize()
+
+    def dump_state(self, game):
+        self.synchronize()
+        return self._h.dump(game)
+
+    def error_flags(self):
+        self.synchronize()
+        return self._h.error_flags()
 
     def close(self):
         self.synchronize()

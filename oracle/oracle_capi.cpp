@@ -627,6 +627,105 @@ int oref_botclient_dump(void* h, int32_t* buf, int cap) {
     return (int)d.size();
 }
 
+// ------------------------------------------------ batched forward model
+// GameState.clone() (rts/GameState.java:591-610) + NaiveMCTS.simulate (ai/mcts/naivemcts/
+// NaiveMCTS.java:297-308) + SimpleSqrtEvaluationFunction3, one GameState per game.  Game j's random
+// streams are seeded like bot env j of oref_create (seed + j): one JVM running that playout with
+// Sampler.generator (shared by both policies), GameState.r and UnitAction.r seeded so.
+struct FwdModel {
+    std::unique_ptr<World> world;
+    MapTemplate map;
+    struct Game {
+        GSP gs;
+        JavaRandom gen, cancelGen, damageGen;
+        std::unique_ptr<AI> ai[2];
+    };
+    std::vector<std::unique_ptr<Game>> games;
+    void attach(Game& g) {
+        g.gs->cancelRandom = &g.cancelGen;
+        g.gs->damageRandom = &g.damageGen;
+    }
+};
+
+void* oref_fm_create(const char* map_path, int n, const int32_t* ai1, const int32_t* ai2, int utt_version, int crs,
+                     int64_t seed) {
+    try {
+        auto f = new FwdModel();
+        f->world.reset(new World(utt_version, crs));
+        f->map = loadMapFile(map_path);
+        f->world->H = f->map.height;
+        f->world->W = f->map.width;
+        for (int j = 0; j < n; j++) {
+            auto g = std::make_unique<FwdModel::Game>();
+            const int64_t es = seed + j;
+            g->gen.setSeed(es);
+            g->cancelGen.setSeed((int64_t)((uint64_t)es ^ 0x9E3779B97F4A7C15ULL));
+            g->damageGen.setSeed((int64_t)((uint64_t)es ^ 0xC2B2AE3D27D4EB4FULL));
+            const int k[2] = {ai1[j], ai2[j]};
+            for (int p = 0; p < 2; p++)
+                g->ai[p].reset(k[p] == BOT_PASSIVE ? (AI*)new PassiveAI() : (AI*)new RandomBiasedAI(&g->gen));
+            g->gs = std::make_shared<GameState>(instantiate(f->map, f->world->utt), &f->world->utt);
+            f->attach(*g);
+            f->games.push_back(std::move(g));
+        }
+        return f;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return nullptr;
+    }
+}
+void oref_fm_destroy(void* h) { delete (FwdModel*)h; }
+// gs[dst] = gs[src].clone()
+int oref_fm_copy(void* h, int dst, int src) {
+    auto f = (FwdModel*)h;
+    auto& g = *f->games.at((size_t)dst);
+    g.gs = f->games.at((size_t)src)->gs->clone();
+    f->attach(g);
+    return 0;
+}
+// gs[dst] = (the game behind slot `slot` of VecClient `vec`).clone()
+int oref_fm_copy_from_vec(void* h, int dst, void* vec, int slot) {
+    auto f = (FwdModel*)h;
+    int p;
+    auto& g = *f->games.at((size_t)dst);
+    g.gs = ((VecClient*)vec)->slotEnv(slot, &p)->gs->clone();
+    f->attach(g);
+    return 0;
+}
+// NaiveMCTS.simulate(gs, gs.getTime() + horizon) (NaiveMCTS.java:297-308)
+int oref_fm_playout(void* h, int game, int horizon) {
+    try {
+        auto& g = *((FwdModel*)h)->games.at((size_t)game);
+        GameState& gs = *g.gs;
+        const int time = gs.time + horizon;
+        bool gameover = false;
+        do {
+            if (gs.isComplete()) {
+                gameover = gs.cycle();
+            } else {
+                PlayerAction pa0 = g.ai[0]->getAction(0, gs);
+                gs.issue(pa0);
+                PlayerAction pa1 = g.ai[1]->getAction(1, gs);
+                gs.issue(pa1);
+            }
+        } while (!gameover && gs.time < time);
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -22;
+    }
+}
+float oref_fm_evaluate(void* h, int game, int maxplayer) {
+    return simpleSqrtEvaluation3(maxplayer, 1 - maxplayer, *((FwdModel*)h)->games.at((size_t)game)->gs);
+}
+int oref_fm_dump(void* h, int game, int32_t* buf, int cap) {
+    auto d = dumpState(*((FwdModel*)h)->games.at((size_t)game)->gs);
+    if ((int)d.size() > cap) return -(int)d.size();
+    std::memcpy(buf, d.data(), d.size() * sizeof(int32_t));
+    return (int)d.size();
+}
+int oref_fm_errors(void* h, int game) { return ((FwdModel*)h)->games.at((size_t)game)->gs->errors; }
+
 // ------------------------------------------------ strict trace replay
 // Fixture text (tests/golden/make_trace_fixtures.py): see that script's docstring.
 // Replays like TestTracesIntegrity.testTrace and additionally compares the full

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <cmath>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -662,6 +663,31 @@ bool GameState::canExecuteAnyAction(int pID) const {  // :416-423
     return false;
 }
 
+bool GameState::isComplete() const {  // :148-157
+    for (auto& u : pgs->units) {
+        if (u->player != -1) {
+            UAAP uaa = unitActions.get(u.get());
+            if (!uaa || !uaa->action) return false;
+        }
+    }
+    return true;
+}
+
+std::shared_ptr<GameState> GameState::clone() const {  // :591-610
+    auto gs = std::make_shared<GameState>(pgs->clone(), utt);
+    gs->time = time;
+    gs->unitCancelationCounter = unitCancelationCounter;
+    for (auto& uaa : unitActions.order) {
+        size_t idx = 0;
+        while (idx < pgs->units.size() && pgs->units[idx].get() != uaa->unit.get()) idx++;
+        if (idx == pgs->units.size()) throw std::runtime_error("Inconsistent game state during cloning...");
+        const UnitP& u2 = gs->pgs->units[idx];
+        // a new assignment sharing the UnitAction object, as the Java does
+        gs->unitActions.put(u2, std::make_shared<UnitActionAssignment>(UnitActionAssignment{u2, uaa->action, uaa->time}));
+    }
+    return gs;
+}
+
 bool GameState::cycle() {  // :553-571
     time++;
     std::vector<UAAP> ready;
@@ -962,6 +988,33 @@ PGSP instantiate(const MapTemplate& t, const UnitTypeTable& utt) {
 }
 
 // ---------------------------------------------------------------- state dump
+// ai/evaluation/SimpleSqrtEvaluationFunction3.java:31-44.  `score += i * 10f` is a float add; the
+// sqrt term is a double (40f * cost is a float, times Math.sqrt of an int quotient) added to the
+// float score and rounded back (compound assignment); x86-64 SSE float / double with no FMA contraction
+// (the Makefile builds without -mfma) is exactly Java's strictfp arithmetic.
+static float baseScoreSqrt3(int player, const GameState& gs) {
+    const float RESOURCE = 20, RESOURCE_IN_WORKER = 10, UNIT_BONUS_MULTIPLIER = 40.0f;
+    float score = gs.getPlayer(player).resources * RESOURCE;
+    bool anyunit = false;
+    for (auto& up : gs.pgs->units) {
+        const Unit& u = *up;
+        if (u.player == player) {
+            anyunit = true;
+            score += u.resources * RESOURCE_IN_WORKER;
+            const float f = UNIT_BONUS_MULTIPLIER * u.type->cost;
+            score = (float)((double)score + (double)f * std::sqrt((double)(u.hitpoints / u.type->hp)));
+        }
+    }
+    if (!anyunit) return 0;
+    return score;
+}
+float simpleSqrtEvaluation3(int maxplayer, int minplayer, const GameState& gs) {  // :24-29
+    float s1 = baseScoreSqrt3(maxplayer, gs);
+    float s2 = baseScoreSqrt3(minplayer, gs);
+    if (s1 + s2 == 0) return 0.5f;
+    return (2 * s1 / (s1 + s2)) - 1;
+}
+
 std::vector<int32_t> dumpState(const GameState& gs) {
     std::vector<int32_t> d;
     const PhysicalGameState& p = *gs.pgs;

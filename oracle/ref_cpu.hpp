@@ -219,6 +219,8 @@ struct GameState {
     bool issue(PlayerAction& pa);      // :249-328
     bool issueSafe(PlayerAction& pa);  // :338-408
     bool canExecuteAnyAction(int pID) const;  // :416-423
+    bool isComplete() const;           // :148-157
+    std::shared_ptr<GameState> clone() const;  // :591-610 (random-stream pointers are the caller's)
     bool cycle();                      // :553-571
     bool integrityCheck() const;       // :703-719
     bool gameover() const { return pgs->gameover(); }
@@ -274,6 +276,9 @@ struct RandomBiasedAI : AI {  // ai/RandomBiasedAI.java:51-107 + util/Sampler.ja
     explicit RandomBiasedAI(JavaRandom* g) : generator(g) {}
     PlayerAction getAction(int player, GameState& gs) override;
 };
+
+// ai/evaluation/SimpleSqrtEvaluationFunction3.java:24-44 (Java float / double arithmetic)
+float simpleSqrtEvaluation3(int maxplayer, int minplayer, const GameState& gs);
 
 // masks: JNIGridnetClient.getMasks (tests/JNIGridnetClient.java:210-223); out = u8[H][W][K]
 void computeMasks(const GameState& gs, const UnitTypeTable& utt, int player, uint8_t* out);

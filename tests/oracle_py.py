@@ -50,6 +50,16 @@ def load():
         L.oref_botclient_destroy.argtypes = [P]
         L.oref_botclient_step.argtypes = [P, I, P, P]
         L.oref_botclient_dump.argtypes = [P, P, I]
+        L.oref_fm_create.restype = P
+        L.oref_fm_create.argtypes = [ctypes.c_char_p, I, P, P, I, I, ctypes.c_int64]
+        L.oref_fm_destroy.argtypes = [P]
+        L.oref_fm_copy.argtypes = [P, I, I]
+        L.oref_fm_copy_from_vec.argtypes = [P, I, P, I]
+        L.oref_fm_playout.argtypes = [P, I, I]
+        L.oref_fm_evaluate.restype = ctypes.c_float
+        L.oref_fm_evaluate.argtypes = [P, I, I]
+        L.oref_fm_dump.argtypes = [P, I, P, I]
+        L.oref_fm_errors.argtypes = [P, I]
         L.oref_bench.restype = ctypes.c_double
         L.oref_bench.argtypes = [ctypes.c_char_p, I, I, I, U64, I]
         _lib = L
@@ -186,3 +196,48 @@ class OracleBotClient:
         if self.h:
             self.L.oref_botclient_destroy(self.h)
             self.h = None
+
+
+class OracleForwardModel:
+    """Batched forward model (GameState.clone + NaiveMCTS.simulate + SimpleSqrtEvaluationFunction3)
+    on the CPU oracle; game j's random streams are seeded from seed + j like the GPU ForwardModel."""
+
+    def __init__(self, n, map_path, ai1, ai2, utt_version=1, crs=1, seed=0):
+        L = load()
+        self.L = L
+        a1 = np.asarray(ai1 if isinstance(ai1, (list, tuple, np.ndarray)) else [ai1] * n, np.int32)
+        a2 = np.asarray(ai2 if isinstance(ai2, (list, tuple, np.ndarray)) else [ai2] * n, np.int32)
+        self.h = L.oref_fm_create(os.path.join(ROOT, map_path).encode(), n, _ptr(a1), _ptr(a2), utt_version, crs, seed)
+        if not self.h:
+            raise RuntimeError(L.oref_last_error().decode())
+        self.n = n
+
+    def copy(self, dst, src):
+        self.L.oref_fm_copy(self.h, dst, src)
+
+    def copy_from_vec(self, dst, vec, slot):
+        self.L.oref_fm_copy_from_vec(self.h, dst, vec.h, slot)
+
+    def playout(self, game, horizon):
+        if self.L.oref_fm_playout(self.h, game, horizon) != 0:
+            raise RuntimeError(self.L.oref_last_error().decode())
+
+    def evaluate(self, game, maxplayer=0):
+        return np.float32(self.L.oref_fm_evaluate(self.h, game, maxplayer))
+
+    def dump(self, game):
+        buf = np.zeros(1 << 16, np.int32)
+        n = self.L.oref_fm_dump(self.h, game, _ptr(buf), buf.size)
+        assert n >= 0
+        return buf[:n].copy()
+
+    def errors(self, game):
+        return self.L.oref_fm_errors(self.h, game)
+
+    def close(self):
+        if self.h:
+            self.L.oref_fm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()

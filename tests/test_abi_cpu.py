@@ -35,6 +35,7 @@ def test_config_struct_layout():
     assert _lib.MrtsConfig.seed.offset == 56
     assert _lib.MrtsConfig.mask_delta.offset == 68
     assert _lib.MrtsConfig.reward_kinds.offset == 72 and _lib.MrtsConfig.n_rewards.offset == 80
+    assert _lib.MrtsConfig.forward_model.offset == 84
 
 
 def test_argument_validation():
