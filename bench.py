@@ -58,6 +58,54 @@ def parse():
     return ap.parse_args()
 
 
+class _FenceFreeEvent:
+    """A HIP timing event created with hipEventDisableSystemFence: recording it does not add a
+    system-scope release fence (cache write-back) in front of the bracketed kernel, so an event pair
+    around one launch measures that kernel plus only its dispatch.  Bound with ctypes to the HIP
+    runtime torch already loaded (one runtime per process); torch.cuda.Event is the fallback."""
+
+    _hip = None
+
+    @classmethod
+    def runtime(cls):
+        if cls._hip is None:
+            import ctypes
+
+            path = None
+            with open("/proc/self/maps") as f:
+                for line in f:
+                    if "libamdhip64.so" in line:
+                        path = line.split()[-1]
+                        break
+            if path is None:
+                raise OSError("libamdhip64 not loaded")
+            hip = ctypes.CDLL(path)
+            hip.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+            hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+            hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
+            hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            cls._hip = hip
+        return cls._hip
+
+    def __init__(self):
+        import ctypes
+
+        self.ctypes = ctypes
+        self.h = ctypes.c_void_p()
+        if self.runtime().hipEventCreateWithFlags(ctypes.byref(self.h), 0x20000000) != 0:  # hipEventDisableSystemFence
+            raise OSError("hipEventCreateWithFlags failed")
+
+    def record(self, stream):
+        if self._hip.hipEventRecord(self.h, self.ctypes.c_void_p(stream.cuda_stream)) != 0:
+            raise OSError("hipEventRecord failed")
+
+    def elapsed_time(self, end):
+        ms = self.ctypes.c_float()
+        if self._hip.hipEventElapsedTime(self.ctypes.byref(ms), self.h, end.h) != 0:
+            raise OSError("hipEventElapsedTime failed")
+        return ms.value
+
+
 def cpu_baseline(map_path, threads, burnin):
     """The CPU oracle (C++ restatement of the Java engine; the JVM is not available) running the
     same workload: VecClient self-play + getMasks + the same Philox policy, std::thread shards."""
@@ -149,7 +197,13 @@ def main():
         except Exception as ex:  # capture unsupported here: time eagerly instead
             print(f"bench: hipGraph capture failed ({ex!r}); eager launches", file=sys.stderr)
             graph = None
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    try:
+        evs = [(_FenceFreeEvent(), _FenceFreeEvent()) for _ in range(a.steps)]
+        event_kind = "hipEventDisableSystemFence events"
+    except (OSError, AttributeError) as ex:
+        print(f"bench: fence-free events unavailable ({ex!r}); torch.cuda.Event", file=sys.stderr)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+        event_kind = "torch.cuda.Event"
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(env.device)
@@ -168,6 +222,12 @@ def main():
         dist.barrier()
     t = time.perf_counter() - t0
     if graph is not None:  # kernel-duration pass (untimed for `value`)
+        # hold the stream in a GPU spin while the host enqueues the K eager steps, so each event
+        # pair brackets back-to-back kernels instead of the host's launch latency
+        try:
+            torch.cuda._sleep(int(150_000 * a.steps))
+        except (AttributeError, RuntimeError):
+            pass
         for k in range(a.steps):
             one_step(base + a.steps + k, evs[k])
         torch.cuda.synchronize(env.device)
@@ -235,8 +295,8 @@ def main():
             "burnin_steps": a.burnin,
             "mask_mode": a.mask_mode,
             "launch": "hipGraph replay of the K timed steps" if graph is not None else "eager",
-            "kernel_timing": ("HIP events around each step-kernel launch, eager pass over the next K steps"
-                              if graph is not None else "HIP events around each step-kernel launch in the timed window"),
+            "kernel_timing": (f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
+                              if graph is not None else f"{event_kind} around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (
                 f", per-step RCCL int16 observation {a.gather_obs} overlapped on a comm stream" if gather_buf is not None
                 else ", no collective in the step"),

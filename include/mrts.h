@@ -82,6 +82,8 @@ typedef struct {
     int32_t forward_model;      /* 1 (with ai1_kinds): a batched forward model for search AIs instead of the
                                    bot-only client: games advance only through mrts_playout*, never
                                    auto-reset; ai1_kinds / bot_kinds are players 0 / 1's playout policies */
+    const char* utt_json;       /* non-NULL: UnitTypeTable.fromJSON(utt_json) (UnitTypeTable.java:414-433)
+                                   replaces utt_version / conflict_policy (the JSON names its own policy) */
 } mrts_config;
 
 typedef struct {               /* ai/jni/Responses.java:12-30 */
@@ -173,6 +175,11 @@ int mrts_evaluate_dev(mrts_env* env, int32_t maxplayer, float* d_out, void* stre
  * PhysicalGameState list order, assignments in LinkedHashMap insertion order.  Synchronous.
  * Returns the number of int32 written, or -(needed) when cap is too small. */
 int mrts_get_state(mrts_env* env, int32_t slot, int32_t* buf, int32_t cap);
+/* The unit-type table a config names (utt_json, else utt_version + conflict_policy) as
+ * UnitTypeTable.toJSON writes it (UnitTypeTable.java:372-383) — what the clients' sendUTT() returns
+ * (JNIGridnetClient.java:225-233).  NUL-terminated; returns the length, or -(length + 1) when cap
+ * is too small, or a negative errno for an invalid table. */
+int mrts_utt_json(int32_t utt_version, int32_t conflict_policy, const char* utt_json, char* buf, int32_t cap);
 /* per-game error flags (MRTS_ERR_*), one uint32 per slot; synchronous */
 int mrts_error_flags(mrts_env* env, uint32_t* flags);
 /* per-slot envSteps (JNIGridnetVecClient.envSteps, :27); synchronous */

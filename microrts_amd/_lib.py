@@ -21,7 +21,7 @@ ERR_BITS = {
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_step_rows", "mrts_get_masks_i32",
     "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_copy_games", "mrts_copy_games_dev", "mrts_playout", "mrts_playout_dev",
-    "mrts_evaluate", "mrts_evaluate_dev", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_evaluate", "mrts_evaluate_dev", "mrts_utt_json", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
 ]
 
@@ -44,6 +44,7 @@ class MrtsConfig(ctypes.Structure):
         ("reward_kinds", ctypes.POINTER(ctypes.c_int32)),
         ("n_rewards", ctypes.c_int32),
         ("forward_model", ctypes.c_int32),
+        ("utt_json", ctypes.c_char_p),
     ]
 
 
@@ -99,6 +100,7 @@ def load(path=LIB_PATH):
     L.mrts_playout_dev.argtypes = [P, I32, P]
     L.mrts_evaluate.argtypes = [P, I32, P]
     L.mrts_evaluate_dev.argtypes = [P, I32, P, P]
+    L.mrts_utt_json.argtypes = [I32, I32, ctypes.c_char_p, ctypes.c_char_p, I32]
     L.mrts_get_state.argtypes = [P, I32, P, I32]
     L.mrts_error_flags.argtypes = [P, P]
     L.mrts_env_steps.argtypes = [P, P]

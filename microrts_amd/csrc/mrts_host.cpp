@@ -15,6 +15,7 @@
 
 #include "../../include/mrts.h"
 #include "mrts_internal.h"
+#include "mrts_json.hpp"
 
 using namespace mrts;
 
@@ -49,10 +50,41 @@ struct Fail {
     } while (0)
 
 // ------------------------------------------------------------------ unit type tables
-// new UnitTypeTable(version, crs) — reference src/rts/units/UnitTypeTable.java:104-289
+// The device table (DevUtt) plus what only the host needs: names (map loading, toJSON),
+// returnTime and producedBy (toJSON only; RETURN lasts moveTime, UnitAction.java:321-322).
+struct UttInfo {
+    DevUtt dev;
+    std::vector<std::string> names;
+    std::vector<int> returnT;
+    std::vector<std::vector<int>> producedBy;
+    int typeOf(const std::string& n) const {
+        for (size_t t = 0; t < names.size(); t++)
+            if (names[t] == n) return (int)t;
+        return -1;
+    }
+};
+
 static const char* kTypeNames[7] = {"Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"};
 
-DevUtt makeUtt(int version, int crs) {
+// the reward functions' type-name tests as flag bits; K and the attack radius from the table
+static void finishUtt(UttInfo& I) {
+    DevUtt& u = I.dev;
+    for (int t = 0; t < u.ntypes; t++) {
+        const std::string& n = I.names[(size_t)t];
+        if (n == "Resource") u.flags[t] |= N_RESOURCE;
+        if (n == "Base") u.flags[t] |= N_BASE | N_BUILDING;
+        if (n == "Barracks") u.flags[t] |= N_BUILDING;
+        if (n == "Worker") u.flags[t] |= N_WORKER;
+        if (n == "Light" || n == "Heavy" || n == "Ranged") u.flags[t] |= N_COMBAT;
+    }
+    int maxRange = 0;  // UnitTypeTable.getMaxAttackRange (:341-349)
+    for (int t = 0; t < u.ntypes; t++) maxRange = std::max(maxRange, u.range[t]);
+    u.maxAttackRadius = 2 * maxRange + 1;
+    u.K = 1 + 6 + 4 + 4 + 4 + 4 + u.ntypes + u.maxAttackRadius * u.maxAttackRadius;
+}
+
+// new UnitTypeTable(version, crs) — reference src/rts/units/UnitTypeTable.java:104-289
+UttInfo makeUtt(int version, int crs) {
     if (version < 1 || version > 3) throw Fail{-EINVAL, "utt_version must be 1, 2 or 3"};
     if (crs < 1 || crs > 3) throw Fail{-EINVAL, "conflict_policy must be 1, 2 or 3"};
     DevUtt u;
@@ -113,11 +145,124 @@ DevUtt makeUtt(int version, int crs) {
     u.nprod[2] = 3; u.prod[2][0] = 4; u.prod[2][1] = 5; u.prod[2][2] = 6;
     u.nprod[3] = 2; u.prod[3][0] = 1; u.prod[3][1] = 2;
     u.crs = crs;
-    int maxRange = 0;
-    for (int t = 0; t < 7; t++) maxRange = std::max(maxRange, u.range[t]);
-    u.maxAttackRadius = 2 * maxRange + 1;
-    u.K = 1 + 6 + 4 + 4 + 4 + 4 + u.ntypes + u.maxAttackRadius * u.maxAttackRadius;
-    return u;
+    UttInfo I;
+    I.dev = u;
+    I.names.assign(kTypeNames, kTypeNames + 7);
+    I.returnT.assign(7, 10);
+    // producedBy in the order of the produces() calls (:283-288): type order here
+    I.producedBy.assign(7, {});
+    for (int t = 0; t < 7; t++)
+        for (int i = 0; i < u.nprod[t]; i++) I.producedBy[(size_t)u.prod[t][i]].push_back(t);
+    finishUtt(I);
+    return I;
+}
+
+// UnitTypeTable.fromJSON (:414-433) + UnitType.createStub / updateFromJSON (UnitType.java:156-161,
+// 217-248), including its quirks: harvestTime is read from "produceTime", returnTime is not read,
+// and absent members take updateFromJSON's defaults (harvestAmount and sightRadius default to 10,
+// canMove / canAttack to false).  Limits of this build: <= 8 types, type IDs equal to their list
+// positions, <= 4 produced types, attack range <= 3 (K <= 80 mask slots: an idle unit's mask is
+// parked as 80 bits in its free assignment words), hp in int16, positive durations; every produced /
+// producedBy name must exist.
+UttInfo uttFromJson(const std::string& text) {
+    mjson::Value o;
+    try {
+        o = mjson::parse(text);
+    } catch (const std::exception& e) {
+        throw Fail{-EINVAL, std::string("utt_json: ") + e.what()};
+    }
+    try {
+        if (o.kind != mjson::Value::OBJ) throw Fail{-EINVAL, "utt_json: not an object"};
+        const int crs = o.getInt("moveConflictResolutionStrategy", 1);
+        if (crs < 1 || crs > 3) throw Fail{-ENOTSUP, "utt_json: moveConflictResolutionStrategy must be 1, 2 or 3"};
+        const mjson::Value& a = o.at("unitTypes");
+        if (a.kind != mjson::Value::ARR) throw Fail{-EINVAL, "utt_json: unitTypes is not an array"};
+        const int n = (int)a.arr.size();
+        if (n < 1 || n > MAX_TYPES) throw Fail{-ENOTSUP, "utt_json: 1..8 unit types supported"};
+        UttInfo I;
+        DevUtt& u = I.dev;
+        std::memset(&u, 0, sizeof(u));
+        u.ntypes = n;
+        u.crs = crs;
+        for (int t = 0; t < n; t++) {  // createStub: ID and name
+            const mjson::Value& ut = a.arr[(size_t)t];
+            if (ut.getInt("ID", -1) != t) throw Fail{-ENOTSUP, "utt_json: type IDs must equal their list positions"};
+            I.names.push_back(ut.getString("name", ""));
+        }
+        I.returnT.assign((size_t)n, 10);
+        I.producedBy.assign((size_t)n, {});
+        auto lookup = [&](const mjson::Value& v) {
+            if (v.kind != mjson::Value::STR) throw Fail{-EINVAL, "utt_json: type names must be strings"};
+            const int k = I.typeOf(v.s);
+            if (k < 0) throw Fail{-EINVAL, "utt_json: unknown unit type " + v.s};
+            return k;
+        };
+        for (int t = 0; t < n; t++) {  // updateFromJSON
+            const mjson::Value& ut = a.arr[(size_t)t];
+            u.cost[t] = ut.getInt("cost", 1);
+            u.hp[t] = ut.getInt("hp", 1);
+            u.minD[t] = ut.getInt("minDamage", 1);
+            u.maxD[t] = ut.getInt("maxDamage", 1);
+            u.range[t] = ut.getInt("attackRange", 1);
+            u.produceT[t] = ut.getInt("produceTime", 10);
+            u.moveT[t] = ut.getInt("moveTime", 10);
+            u.attackT[t] = ut.getInt("attackTime", 10);
+            u.harvestT[t] = ut.getInt("produceTime", 10);  // sic (UnitType.java:227)
+            u.harvestAmt[t] = ut.getInt("harvestAmount", 10);
+            u.sight[t] = ut.getInt("sightRadius", 10);
+            uint32_t f = 0;
+            if (ut.getBool("isResource", false)) f |= F_RESOURCE;
+            if (ut.getBool("isStockpile", false)) f |= F_STOCKPILE;
+            if (ut.getBool("canHarvest", false)) f |= F_HARVEST;
+            if (ut.getBool("canMove", false)) f |= F_MOVE;
+            if (ut.getBool("canAttack", false)) f |= F_ATTACK;
+            u.flags[t] = f;
+            const mjson::Value& pr = ut.at("produces");
+            if (pr.kind != mjson::Value::ARR || pr.arr.size() > (size_t)MAX_PRODUCES)
+                throw Fail{-ENOTSUP, "utt_json: at most 4 produced types per type"};
+            u.nprod[t] = (int)pr.arr.size();
+            for (size_t i = 0; i < pr.arr.size(); i++) u.prod[t][i] = lookup(pr.arr[i]);
+            const mjson::Value& pb = ut.at("producedBy");
+            if (pb.kind != mjson::Value::ARR) throw Fail{-EINVAL, "utt_json: producedBy is not an array"};
+            for (auto& v : pb.arr) I.producedBy[(size_t)t].push_back(lookup(v));
+            if (u.hp[t] < 1 || u.hp[t] > 32767 || u.cost[t] < 0 || u.cost[t] > 32767 || u.minD[t] < 0 ||
+                u.maxD[t] < u.minD[t] || u.maxD[t] > 32767 || u.range[t] < 1 || u.range[t] > 3 ||
+                u.produceT[t] < 1 || u.moveT[t] < 1 || u.attackT[t] < 1 || u.harvestT[t] < 1 ||
+                u.harvestAmt[t] < 0 || u.harvestAmt[t] > 32767 || u.sight[t] < 0 || u.sight[t] > 64)
+                throw Fail{-ENOTSUP, "utt_json: a value of type " + I.names[(size_t)t] + " is outside this build's limits"};
+        }
+        finishUtt(I);
+        return I;
+    } catch (const std::runtime_error& e) {
+        throw Fail{-EINVAL, std::string("utt_json: ") + e.what()};
+    }
+}
+
+// UnitTypeTable.toJSON (:372-383) + UnitType.toJSON (UnitType.java:299-343), byte for byte
+std::string uttToJson(const UttInfo& I) {
+    const DevUtt& u = I.dev;
+    auto b = [](bool v) { return v ? "true" : "false"; };
+    std::ostringstream w;
+    w << "{\"moveConflictResolutionStrategy\":" << u.crs << ",\"unitTypes\":[";
+    for (int t = 0; t < u.ntypes; t++) {
+        if (t) w << ", ";
+        const uint32_t f = u.flags[t];
+        w << "{\"ID\":" << t << ", \"name\":\"" << I.names[(size_t)t] << "\", \"cost\":" << u.cost[t] << ", \"hp\":" << u.hp[t]
+          << ", \"minDamage\":" << u.minD[t] << ", \"maxDamage\":" << u.maxD[t] << ", \"attackRange\":" << u.range[t]
+          << ", \"produceTime\":" << u.produceT[t] << ", \"moveTime\":" << u.moveT[t] << ", \"attackTime\":" << u.attackT[t]
+          << ", \"harvestTime\":" << u.harvestT[t] << ", \"returnTime\":" << I.returnT[(size_t)t]
+          << ", \"harvestAmount\":" << u.harvestAmt[t] << ", \"sightRadius\":" << u.sight[t]
+          << ", \"isResource\":" << b(f & F_RESOURCE) << ", \"isStockpile\":" << b(f & F_STOCKPILE)
+          << ", \"canHarvest\":" << b(f & F_HARVEST) << ", \"canMove\":" << b(f & F_MOVE)
+          << ", \"canAttack\":" << b(f & F_ATTACK) << ", \"produces\":[";
+        for (int i = 0; i < u.nprod[t]; i++) w << (i ? ", " : "") << "\"" << I.names[(size_t)u.prod[t][i]] << "\"";
+        w << "], \"producedBy\":[";
+        for (size_t i = 0; i < I.producedBy[(size_t)t].size(); i++)
+            w << (i ? ", " : "") << "\"" << I.names[(size_t)I.producedBy[(size_t)t][i]] << "\"";
+        w << "]}";
+    }
+    w << "]}";
+    return w.str();
 }
 
 // ------------------------------------------------------------------ XML map reader
@@ -159,7 +304,7 @@ int toInt(const std::string& s) {
     }
 }
 
-MapDef parseMap(const std::string& path) {
+MapDef parseMap(const std::string& path, const UttInfo& utt) {
     std::ifstream f(path);
     if (!f) throw Fail{-ENOENT, "cannot open map " + path};
     std::stringstream ss;
@@ -227,9 +372,7 @@ MapDef parseMap(const std::string& path) {
         const std::string ut = x.substr(a, b - a);
         MapDef::U u;
         const std::string tn = attrOf(ut, "type");
-        u.type = -1;
-        for (int t = 0; t < 7; t++)
-            if (tn == kTypeNames[t]) u.type = t;
+        u.type = utt.typeOf(tn);  // utt.getUnitType(name) (Unit.java:608)
         if (u.type < 0) throw Fail{-EINVAL, "map: unknown unit type " + tn};
         u.id = std::stoll(attrOf(ut, "ID"));
         u.player = toInt(attrOf(ut, "player"));
@@ -260,6 +403,7 @@ struct mrts_env {
     int forwardModel = 0;  // games advance through mrts_playout* only (GT_PLAYOUT)
     uint32_t slotIdBase = 0;
     DevUtt utt;
+    UttInfo uttInfo;
     std::vector<int> tmplOffHost;
     int32_t* d_state = nullptr;
     int32_t* d_tmpl = nullptr;
@@ -393,7 +537,8 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         env->device = cfg->device;
         HIPCHK(hipSetDevice(cfg->device));
         HIPCHK(hipStreamCreateWithFlags(&env->stream, hipStreamNonBlocking));
-        env->utt = makeUtt(cfg->utt_version, cfg->conflict_policy);
+        env->uttInfo = cfg->utt_json ? uttFromJson(cfg->utt_json) : makeUtt(cfg->utt_version, cfg->conflict_policy);
+        env->utt = env->uttInfo.dev;
         env->K = env->utt.K;
         env->C = cfg->partial_obs ? 8 : 6;
         env->partialObs = cfg->partial_obs;
@@ -432,7 +577,7 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
             if (!p) throw Fail{-EINVAL, "null map path"};
             auto it = tmplIndex.find(p);
             if (it == tmplIndex.end()) {
-                maps.push_back(parseMap(p));
+                maps.push_back(parseMap(p, env->uttInfo));
                 it = tmplIndex.emplace(p, (int)maps.size() - 1).first;
             }
             gameTmpl[(size_t)g] = it->second;
@@ -860,6 +1005,17 @@ int mrts_get_state(mrts_env* env, int32_t slot, int32_t* buf, int32_t cap) {
         if ((int)d.size() > cap) return -(int)d.size();
         std::memcpy(buf, d.data(), d.size() * 4);
         return (int)d.size();
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_utt_json(int32_t utt_version, int32_t conflict_policy, const char* utt_json, char* buf, int32_t cap) {
+    try {
+        const std::string j = uttToJson(utt_json ? uttFromJson(utt_json) : makeUtt(utt_version, conflict_policy));
+        if (!buf || cap < (int32_t)j.size() + 1) return -((int)j.size() + 1);
+        std::memcpy(buf, j.c_str(), j.size() + 1);
+        return (int)j.size();
     } catch (const Fail& f) {
         return fail(f);
     }

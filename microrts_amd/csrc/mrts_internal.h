@@ -25,7 +25,13 @@ struct DevUtt {
     int32_t maxAttackRadius;    // 2 * max attack range + 1 (JNIGridnetClient.java:125)
     int32_t K;                  // mask slots per cell (JNIGridnetClient.java:138)
 };
-enum : uint32_t { F_RESOURCE = 1, F_STOCKPILE = 2, F_HARVEST = 4, F_MOVE = 8, F_ATTACK = 16 };
+enum : uint32_t { F_RESOURCE = 1, F_STOCKPILE = 2, F_HARVEST = 4, F_MOVE = 8, F_ATTACK = 16,
+                  // the type-name tests of the reward functions (src/ai/reward/*.java), set from the names
+                  N_RESOURCE = 1u << 8,   // "Resource"
+                  N_BASE = 1u << 9,       // "Base"
+                  N_WORKER = 1u << 10,    // "Worker"
+                  N_BUILDING = 1u << 11,  // "Base" or "Barracks"
+                  N_COMBAT = 1u << 12 };  // "Light", "Heavy" or "Ranged"
 
 // ---- per-game state block in HBM (int32 words) -------------------------------------------------
 // header

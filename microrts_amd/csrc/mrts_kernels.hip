@@ -56,8 +56,9 @@ enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2, GT_PLAYOUT = 3 }
 // legality rewrite, before issue()'s conflict cancellations): HARVEST, RETURN, ATTACK, and PRODUCE
 // of a Worker / a Base or Barracks / a Light, Heavy or Ranged
 enum { RC_HARVEST = 0, RC_RETURN = 1, RC_ATTACK = 2, RC_PROD_WORKER = 3, RC_PROD_BUILDING = 4, RC_PROD_COMBAT = 5, RC_N = 6 };
-DEV int prodCategory(int ut) {  // type ids: Resource 0, Base 1, Barracks 2, Worker 3, Light 4, Heavy 5, Ranged 6
-    return ut == 3 ? RC_PROD_WORKER : (ut == 1 || ut == 2) ? RC_PROD_BUILDING : (ut >= 4 && ut <= 6) ? RC_PROD_COMBAT : -1;
+DEV int prodCategory(uint32_t typeFlags) {  // the reward functions' name tests (DevUtt.flags N_*)
+    return (typeFlags & N_WORKER) ? RC_PROD_WORKER : (typeFlags & N_BUILDING) ? RC_PROD_BUILDING
+                                                   : (typeFlags & N_COMBAT) ? RC_PROD_COMBAT : -1;
 }
 enum { GK_PASSIVE = 0, GK_RANDOM_BIASED = 1 };                    // AI kinds (bits 4-7 ai1, 8-11 ai2)
 enum : uint32_t {
@@ -862,7 +863,7 @@ struct Game {
                     // p.m_b = NONE mutates pa's own Pair unless a cancel already replaced p: the
                     // TraceEntry (pa.clone() after issueSafe) then records NONE, not the PRODUCE
                     if (orig && tIn == T_PRODUCE && (P.reward_need & RN_COUNTS) && lane_id() == 0) {
-                        const int pc = prodCategory(utIn);
+                        const int pc = prodCategory(U.flags[utIn]);
                         if (pc >= 0) rwc[curP * RC_N + pc] -= 1;
                     }
                     orig = false;
@@ -936,7 +937,7 @@ struct Game {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
         if (P.reward_need & RN_COUNTS) {  // the pairs as the TraceEntry records them (legality applied)
-            const int pc = np ? prodCategory(ut) : -1;
+            const int pc = np ? prodCategory(U.flags[ut]) : -1;
             auto cnt = [](bool b) { return (int)__popcll(ballot(b)); };
             const int c[RC_N] = {cnt(act && t == T_HARVEST), cnt(act && t == T_RETURN), cnt(act && t == T_ATTACK),
                                  cnt(pc == RC_PROD_WORKER), cnt(pc == RC_PROD_BUILDING), cnt(pc == RC_PROD_COMBAT)};
@@ -1560,13 +1561,13 @@ struct Game {
     // Base is the first unit of minplayer named "Base" in the pre-cycle list; distances are from
     // maxplayer's Light/Heavy/Ranged/Worker units.  Squared distances are exact integers and sqrt is
     // monotone, so min(sqrt) = sqrt(min).
-    static DEV bool mobileType(int t) { return t == 3 || t == 4 || t == 5 || t == 6; }
+    DEV bool mobileType(int t) const { return (U.flags[t] & (N_WORKER | N_COMBAT)) != 0; }  // Light/Heavy/Ranged/Worker
     DEV void closerBefore() {
         int b0 = -1, b1 = -1;
         for (int o0 = 0; o0 < nu; o0 += 64) {
             const int o = o0 + lane_id();
             const uint32_t c = o < nu ? uc[o] : UC_DEAD;
-            const bool base = !(c & UC_DEAD) && utyp(c) == 1;
+            const bool base = !(c & UC_DEAD) && (U.flags[utyp(c)] & N_BASE);
             const uint64_t m0 = ballot(base && uplay(c) == 0), m1 = ballot(base && uplay(c) == 1);
             if (b0 < 0 && m0) b0 = o0 + __builtin_ctzll(m0);
             if (b1 < 0 && m1) b1 = o0 + __builtin_ctzll(m1);
@@ -1610,7 +1611,7 @@ struct Game {
         if (P.reward_need & RN_RESOURCES)
             for (int o0 = 0; o0 < nu; o0 += 64) {
                 const int o = o0 + lane_id();
-                resLeft |= ballot(o < nu && !(uc[o] & UC_DEAD) && utyp(uc[o]) == 0 && res[o] > 0) != 0;
+                resLeft |= ballot(o < nu && !(uc[o] & UC_DEAD) && (U.flags[utyp(uc[o])] & N_RESOURCE) && res[o] > 0) != 0;
             }
         const int k0 = P.reward_kinds[0];
         const bool done0 = k0 == RF_WINLOSS ? gameover : (k0 == RF_RESOURCE_GATHER ? !resLeft : false);

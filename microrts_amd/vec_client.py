@@ -29,15 +29,65 @@ class UnitTypeTable:
     MOVE_CONFLICT_RESOLUTION_CANCEL_BOTH = 1
     MOVE_CONFLICT_RESOLUTION_CANCEL_RANDOM = 2
     MOVE_CONFLICT_RESOLUTION_CANCEL_ALTERNATING = 3
-    TYPES = ["Resource", "Base", "Barracks", "Worker", "Light", "Heavy", "Ranged"]
 
     def __init__(self, version=VERSION_ORIGINAL, crs=MOVE_CONFLICT_RESOLUTION_CANCEL_BOTH):
         if version not in (1, 2, 3) or crs not in (1, 2, 3):
             raise ValueError("unsupported UnitTypeTable version / conflict policy")
         self.version, self.crs = version, crs
+        self.json = None  # set by fromJSON: the table is then the JSON's (version / crs unused)
+        self._desc = None
+
+    @classmethod
+    def fromJSON(cls, text):
+        """UnitTypeTable.fromJSON (UnitTypeTable.java:414-433), validated by the native parser (its
+        quirks included: harvestTime is read from "produceTime", returnTime is not read)."""
+        utt = cls()
+        utt.json = text if isinstance(text, str) else text.decode()
+        utt.toJSON()  # raises on a table this build cannot run
+        return utt
+
+    def toJSON(self):
+        """UnitTypeTable.toJSON (UnitTypeTable.java:372-383), byte for byte."""
+        L = _lib.load()
+        j = self.json.encode() if self.json else None
+        n = L.mrts_utt_json(self.version, self.crs, j, None, 0)
+        if n >= 0 or n == -22 or n == -95:
+            raise ValueError(L.mrts_last_error().decode() or "invalid unit-type table")
+        buf = ctypes.create_string_buffer(-n)
+        _lib.check(0 if L.mrts_utt_json(self.version, self.crs, j, buf, -n) >= 0 else -1)
+        return buf.value.decode()
+
+    def _table(self):
+        if self._desc is None:
+            import json
+
+            self._desc = json.loads(self.toJSON())
+        return self._desc
+
+    @property
+    def TYPES(self):
+        return [t["name"] for t in self._table()["unitTypes"]]
+
+    def getUnitTypes(self):
+        return self._table()["unitTypes"]
+
+    def getMoveConflictResolutionStrategy(self):
+        return self._table()["moveConflictResolutionStrategy"]
 
     def getMaxAttackRange(self):
-        return 3
+        """UnitTypeTable.getMaxAttackRange (:341-349)."""
+        return max(t["attackRange"] for t in self._table()["unitTypes"])
+
+
+class _ClientView:
+    """The per-env client objects the Java VecClient exposes (clients / selfPlayClients); only
+    sendUTT() (JNIGridnetClient.java:225-233) is meaningful on this build."""
+
+    def __init__(self, utt):
+        self._utt = utt
+
+    def sendUTT(self):
+        return self._utt.toJSON()
 
 
 class Responses:
@@ -94,7 +144,8 @@ class _Handle:
                               ctypes.cast(self._kinds, P32),
                               ctypes.cast(self._ai1, P32) if self._ai1 is not None else None,
                               ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base,
-                              int(bool(mask_delta)), ctypes.cast(self._rk, P32), self.R, int(bool(forward_model)))
+                              int(bool(mask_delta)), ctypes.cast(self._rk, P32), self.R, int(bool(forward_model)),
+                              utt.json.encode() if utt.json else None)
         h = ctypes.c_void_p()
         _lib.check(L.mrts_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -149,6 +200,13 @@ class JNIGridnetVecClient:
         h = self._h
         self.num_slots, self.height, self.width, self.num_planes, self.mask_slots = h.S, h.H, h.W, h.C, h.K
         self._resp = _lib.MrtsResponses()
+        # the Java fields of per-env clients (:22-26); each offers sendUTT()
+        self.selfPlayClients = [_ClientView(utt)] * (a_num_selfplayenvs // 2)
+        self.clients = [_ClientView(utt)] * a_num_envs
+
+    def sendUTT(self):
+        """The unit-type table as JSON (JNIGridnetClient.sendUTT, :225-233)."""
+        return self.utt.toJSON()
 
     @classmethod
     def bots(cls, a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai1s, a_ai2s, a_utt=None, partial_obs=False, device=0,

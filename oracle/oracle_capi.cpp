@@ -142,7 +142,8 @@ struct World {
     bool partialObs = false;
     uint64_t seed = 0;
     std::vector<int> rfs{RF_WINLOSS};  // a_rfs (JNIGridnetVecClient.java:106)
-    World(int ver, int crs) : utt(ver, crs) {
+    World(int ver, int crs, const char* uttJson = nullptr)
+        : utt(uttJson ? UnitTypeTable::fromJSON(uttJson) : UnitTypeTable(ver, crs)) {
         maxAttackRadius = utt.getMaxAttackRange() * 2 + 1;
         K = maskSlotsPerCell(utt);
     }
@@ -423,11 +424,11 @@ const char* oref_last_error() { return g_err.c_str(); }
 
 // map_paths: one per slot (self-play games use map_paths[2i], like :119); bot_kinds: per bot env
 void* oref_create(int n_selfplay_slots, int n_bot_envs, const int32_t* bot_kinds, int max_steps, int partial_obs,
-                  int utt_version, int crs, const char** map_paths, uint64_t seed) {
+                  int utt_version, int crs, const char** map_paths, uint64_t seed, const char* utt_json) {
     try {
         if (n_selfplay_slots % 2) throw std::runtime_error("n_selfplay_slots must be even");
         auto v = new VecClient();
-        v->world.reset(new World(utt_version, crs));
+        v->world.reset(new World(utt_version, crs, utt_json));
         v->world->partialObs = partial_obs != 0;
         v->world->C = partial_obs ? 8 : 6;
         v->world->seed = seed;
@@ -565,10 +566,11 @@ struct BotVec {
     std::vector<int> rfs{RF_WINLOSS};
 };
 
-void* oref_botclient_create(const char* map_path, int ai1, int ai2, int max_steps, int utt_version, int crs, int64_t seed) {
+void* oref_botclient_create(const char* map_path, int ai1, int ai2, int max_steps, int utt_version, int crs, int64_t seed,
+                            const char* utt_json) {
     try {
         auto b = new BotVec();
-        b->world.reset(new World(utt_version, crs));
+        b->world.reset(new World(utt_version, crs, utt_json));
         b->map = loadMapFile(map_path);
         b->world->H = b->map.height;
         b->world->W = b->map.width;
@@ -648,10 +650,10 @@ struct FwdModel {
 };
 
 void* oref_fm_create(const char* map_path, int n, const int32_t* ai1, const int32_t* ai2, int utt_version, int crs,
-                     int64_t seed) {
+                     int64_t seed, const char* utt_json) {
     try {
         auto f = new FwdModel();
-        f->world.reset(new World(utt_version, crs));
+        f->world.reset(new World(utt_version, crs, utt_json));
         f->map = loadMapFile(map_path);
         f->world->H = f->map.height;
         f->world->W = f->map.width;
@@ -839,7 +841,7 @@ double oref_bench(const char* map_path, int n_games, int steps, int threads, uin
     for (int t = 0; t < threads; t++) {
         per[(size_t)t] = n_games / threads + (t < n_games % threads ? 1 : 0);
         std::vector<const char*> paths((size_t)per[(size_t)t] * 2, map_path);
-        hs[(size_t)t] = oref_create(per[(size_t)t] * 2, 0, nullptr, 2000, 0, 1, 1, paths.data(), seed + (uint64_t)t * 1000003ULL);
+        hs[(size_t)t] = oref_create(per[(size_t)t] * 2, 0, nullptr, 2000, 0, 1, 1, paths.data(), seed + (uint64_t)t * 1000003ULL, nullptr);
         oref_reset(hs[(size_t)t], nullptr, nullptr, nullptr, nullptr);
     }
     auto worker = [&](int t) {

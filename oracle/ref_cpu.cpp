@@ -3,6 +3,7 @@
 // PlayerAction,PartiallyObservableGameState}.java, rts/units/{Unit,UnitTypeTable}.java,
 // ai/{PassiveAI,RandomBiasedAI}.java, util/Sampler.java.
 #include "ref_cpu.hpp"
+#include "../microrts_amd/csrc/mrts_json.hpp"  // a plain JSON reader (minimal-json's role)
 
 #include <algorithm>
 #include <array>
@@ -140,6 +141,46 @@ UnitTypeTable::UnitTypeTable(int ver, int crs) : moveConflictResolutionStrategy(
     barracks->produces.push_back(ranged);
     worker->produces.push_back(base);
     worker->produces.push_back(barracks);
+}
+
+// UnitTypeTable.fromJSON (:414-433): EMPTY table, the policy (default CANCEL_BOTH), then createStub
+// for every entry (UnitType.java:156-161) and updateFromJSON by name (UnitType.java:217-248) —
+// harvestTime from "produceTime", returnTime untouched, minimal-json defaults for absent members.
+UnitTypeTable UnitTypeTable::fromJSON(const std::string& json) {
+    const mjson::Value o = mjson::parse(json);
+    UnitTypeTable utt(1, 1);
+    utt.unitTypes.clear();
+    utt.version = 0;  // EMPTY_TYPE_TABLE
+    utt.moveConflictResolutionStrategy = o.getInt("moveConflictResolutionStrategy", 1);
+    const mjson::Value& a = o.at("unitTypes");
+    for (auto& v : a.arr) {
+        auto* ut = new UnitType();
+        ut->ID = v.getInt("ID", -1);
+        ut->name = v.getString("name", "");
+        utt.unitTypes.emplace_back(ut);
+    }
+    for (auto& v : a.arr) {
+        UnitType* ut = utt.getUnitType(v.getString("name", ""));
+        ut->cost = v.getInt("cost", 1);
+        ut->hp = v.getInt("hp", 1);
+        ut->minDamage = v.getInt("minDamage", 1);
+        ut->maxDamage = v.getInt("maxDamage", 1);
+        ut->attackRange = v.getInt("attackRange", 1);
+        ut->produceTime = v.getInt("produceTime", 10);
+        ut->moveTime = v.getInt("moveTime", 10);
+        ut->attackTime = v.getInt("attackTime", 10);
+        ut->harvestTime = v.getInt("produceTime", 10);
+        ut->produceTime = v.getInt("produceTime", 10);
+        ut->harvestAmount = v.getInt("harvestAmount", 10);
+        ut->sightRadius = v.getInt("sightRadius", 10);
+        ut->isResource = v.getBool("isResource", false);
+        ut->isStockpile = v.getBool("isStockpile", false);
+        ut->canHarvest = v.getBool("canHarvest", false);
+        ut->canMove = v.getBool("canMove", false);
+        ut->canAttack = v.getBool("canAttack", false);
+        for (auto& p : v.at("produces").arr) ut->produces.push_back(utt.getUnitType(p.s));
+    }
+    return utt;
 }
 
 UnitType* UnitTypeTable::getUnitType(int ID) const {

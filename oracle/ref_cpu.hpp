@@ -68,6 +68,7 @@ struct UnitTypeTable {
     int moveConflictResolutionStrategy = 1;
     int version = 1;
     UnitTypeTable(int version = 1, int crs = 1);
+    static UnitTypeTable fromJSON(const std::string& json);  // :414-433
     UnitType* getUnitType(int ID) const;  // ArrayList.get: throws on bad index (:305-307)
     UnitType* getUnitType(const std::string& name) const;  // :314-319
     int getMaxAttackRange() const;  // :341-349

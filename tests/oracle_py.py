@@ -17,6 +17,7 @@ BOT_PASSIVE, BOT_RANDOM_BIASED = 0, 1
 
 def build():
     srcs = [os.path.join(ROOT, "oracle", f) for f in ("ref_cpu.cpp", "ref_cpu.hpp", "oracle_capi.cpp", "Makefile")]
+    srcs.append(os.path.join(ROOT, "microrts_amd", "csrc", "mrts_json.hpp"))
     if os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in srcs):
         return LIB
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
@@ -30,7 +31,7 @@ def load():
         L = ctypes.CDLL(LIB)
         P, I, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
         L.oref_create.restype = P
-        L.oref_create.argtypes = [I, I, P, I, I, I, I, P, U64]
+        L.oref_create.argtypes = [I, I, P, I, I, I, I, P, U64, ctypes.c_char_p]
         L.oref_destroy.argtypes = [P]
         L.oref_dims.argtypes = [P, P, P, P, P, P]
         L.oref_reset.argtypes = [P, P, P, P, P]
@@ -46,12 +47,12 @@ def load():
         L.oref_trace_replay.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, I]
         L.oref_policy.argtypes = [P, I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P]
         L.oref_botclient_create.restype = P
-        L.oref_botclient_create.argtypes = [ctypes.c_char_p, I, I, I, I, I, ctypes.c_int64]
+        L.oref_botclient_create.argtypes = [ctypes.c_char_p, I, I, I, I, I, ctypes.c_int64, ctypes.c_char_p]
         L.oref_botclient_destroy.argtypes = [P]
         L.oref_botclient_step.argtypes = [P, I, P, P]
         L.oref_botclient_dump.argtypes = [P, P, I]
         L.oref_fm_create.restype = P
-        L.oref_fm_create.argtypes = [ctypes.c_char_p, I, P, P, I, I, ctypes.c_int64]
+        L.oref_fm_create.argtypes = [ctypes.c_char_p, I, P, P, I, I, ctypes.c_int64, ctypes.c_char_p]
         L.oref_fm_destroy.argtypes = [P]
         L.oref_fm_copy.argtypes = [P, I, I]
         L.oref_fm_copy_from_vec.argtypes = [P, I, P, I]
@@ -74,7 +75,7 @@ class OracleVecClient:
     """Mirror of tests.JNIGridnetVecClient (src/tests/JNIGridnetVecClient.java) on the CPU oracle."""
 
     def __init__(self, n_selfplay_slots, n_bot_envs, max_steps, map_paths, partial_obs=False, utt_version=1, crs=1,
-                 bot_kinds=None, seed=0, slot_id_base=0, rewards=None):
+                 bot_kinds=None, seed=0, slot_id_base=0, rewards=None, utt_json=None):
         """rewards: reward function ids (REWARD_IDS); None = [WinLoss].  reward / done are [S] for one
         reward function, [S][R] otherwise."""
         L = load()
@@ -82,7 +83,8 @@ class OracleVecClient:
         paths = (ctypes.c_char_p * len(map_paths))(*[os.path.join(ROOT, p).encode() for p in map_paths])
         bk = np.asarray(bot_kinds if bot_kinds is not None else [0] * n_bot_envs, dtype=np.int32)
         self.h = L.oref_create(n_selfplay_slots, n_bot_envs, _ptr(bk) if n_bot_envs else None, max_steps, int(partial_obs),
-                               utt_version, crs, ctypes.cast(paths, ctypes.c_void_p), seed + slot_id_base)
+                               utt_version, crs, ctypes.cast(paths, ctypes.c_void_p), seed + slot_id_base,
+                               utt_json.encode() if utt_json else None)
         if not self.h:
             raise RuntimeError(L.oref_last_error().decode())
         d = [ctypes.c_int32() for _ in range(5)]
@@ -164,10 +166,11 @@ def policy(mask, seed, env_id, step, player, n_types=7):
 class OracleBotClient:
     """tests.JNIBotClient (src/tests/JNIBotClient.java) + the bot-only VecClient auto-reset, one game."""
 
-    def __init__(self, map_path, ai1, ai2, max_steps=2000, utt_version=1, crs=1, seed=0, rewards=None):
+    def __init__(self, map_path, ai1, ai2, max_steps=2000, utt_version=1, crs=1, seed=0, rewards=None, utt_json=None):
         L = load()
         self.L = L
-        self.h = L.oref_botclient_create(os.path.join(ROOT, map_path).encode(), ai1, ai2, max_steps, utt_version, crs, seed)
+        self.h = L.oref_botclient_create(os.path.join(ROOT, map_path).encode(), ai1, ai2, max_steps, utt_version, crs, seed,
+                                         utt_json.encode() if utt_json else None)
         if not self.h:
             raise RuntimeError(L.oref_last_error().decode())
         self.R = 1
@@ -202,12 +205,13 @@ class OracleForwardModel:
     """Batched forward model (GameState.clone + NaiveMCTS.simulate + SimpleSqrtEvaluationFunction3)
     on the CPU oracle; game j's random streams are seeded from seed + j like the GPU ForwardModel."""
 
-    def __init__(self, n, map_path, ai1, ai2, utt_version=1, crs=1, seed=0):
+    def __init__(self, n, map_path, ai1, ai2, utt_version=1, crs=1, seed=0, utt_json=None):
         L = load()
         self.L = L
         a1 = np.asarray(ai1 if isinstance(ai1, (list, tuple, np.ndarray)) else [ai1] * n, np.int32)
         a2 = np.asarray(ai2 if isinstance(ai2, (list, tuple, np.ndarray)) else [ai2] * n, np.int32)
-        self.h = L.oref_fm_create(os.path.join(ROOT, map_path).encode(), n, _ptr(a1), _ptr(a2), utt_version, crs, seed)
+        self.h = L.oref_fm_create(os.path.join(ROOT, map_path).encode(), n, _ptr(a1), _ptr(a2), utt_version, crs, seed,
+                                  utt_json.encode() if utt_json else None)
         if not self.h:
             raise RuntimeError(L.oref_last_error().decode())
         self.n = n

@@ -31,11 +31,31 @@ def test_library_loads_and_exports_every_symbol():
 
 def test_config_struct_layout():
     # mrts_config: 6 int32, pointer, pointer, int32, uint64, int32 (natural alignment)
-    assert ctypes.sizeof(_lib.MrtsConfig) == 88
+    assert ctypes.sizeof(_lib.MrtsConfig) == 96
     assert _lib.MrtsConfig.seed.offset == 56
     assert _lib.MrtsConfig.mask_delta.offset == 68
     assert _lib.MrtsConfig.reward_kinds.offset == 72 and _lib.MrtsConfig.n_rewards.offset == 80
-    assert _lib.MrtsConfig.forward_model.offset == 84
+    assert _lib.MrtsConfig.forward_model.offset == 84 and _lib.MrtsConfig.utt_json.offset == 88
+
+
+def test_config_struct_matches_the_c_header(tmp_path):
+    """offsetof / sizeof of every mrts_config member as the C compiler lays out include/mrts.h"""
+    import shutil
+    import subprocess
+
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    names = [f[0] for f in _lib.MrtsConfig._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mrts.h"\nint main(void) {\n'
+                   + "".join(f'  printf("%zu\\n", offsetof(mrts_config, {n}));\n' for n in names)
+                   + '  printf("%zu\\n", sizeof(mrts_config));\n  return 0;\n}\n')
+    exe = tmp_path / "layout"
+    subprocess.check_call([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    want = [getattr(_lib.MrtsConfig, n).offset for n in names] + [ctypes.sizeof(_lib.MrtsConfig)]
+    assert got == want
 
 
 def test_argument_validation():

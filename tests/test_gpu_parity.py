@@ -42,16 +42,18 @@ def _compare_step(env, ref, step, dump_every, tag=""):
 
 
 def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, policy="masked", dump_every=10, seed=3,
-             players=None, partial_obs=False, bots=None, rfs=None):
+             players=None, partial_obs=False, bots=None, rfs=None, utt_json=None):
     torch = _torch()
     from microrts_amd import DeviceVecEnv, UnitTypeTable
 
-    env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=UnitTypeTable(utt, crs), seed=seed, partial_obs=partial_obs,
+    table = UnitTypeTable.fromJSON(utt_json) if utt_json else UnitTypeTable(utt, crs)
+    ntypes = len(table.TYPES)
+    env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=table, seed=seed, partial_obs=partial_obs,
                        ai2s=bots, rfs=rfs)
     kinds = [1 if b == "RandomBiasedAI" else 0 for b in bots] if bots else None
     ref = oracle_py.OracleVecClient(n_sp, n_bot, max_steps, maps, utt_version=utt, crs=crs, seed=seed,
                                     partial_obs=partial_obs, bot_kinds=kinds,
-                                    rewards=[oracle_py.REWARD_IDS[r] for r in rfs] if rfs else None)
+                                    rewards=[oracle_py.REWARD_IDS[r] for r in rfs] if rfs else None, utt_json=utt_json)
     S = ref.S
     if players is not None:
         env.players.copy_(torch.as_tensor(players, dtype=torch.int32))
@@ -73,11 +75,11 @@ def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, polic
             acts = env.actions.cpu().numpy()
             if step < 20 or step % 10 == 0:  # the GPU policy kernel is bit-identical to the oracle's Philox policy
                 for s in range(min(S, 8)):
-                    assert np.array_equal(acts[s], oracle_py.policy(m_ref[s], SEED, s, step, 0))
+                    assert np.array_equal(acts[s], oracle_py.policy(m_ref[s], SEED, s, step, 0, ntypes))
         else:  # unmasked uniform components (exercises every illegal → NONE path)
             acts = np.stack([rng.integers(0, 6, (S, HW)), rng.integers(0, 4, (S, HW)), rng.integers(0, 4, (S, HW)),
-                             rng.integers(0, 4, (S, HW)), rng.integers(0, 4, (S, HW)), rng.integers(0, 7, (S, HW)),
-                             rng.integers(0, 49, (S, HW))], axis=-1).astype(np.int32)
+                             rng.integers(0, 4, (S, HW)), rng.integers(0, 4, (S, HW)), rng.integers(0, ntypes, (S, HW)),
+                             rng.integers(0, ref.K - 23 - ntypes, (S, HW))], axis=-1).astype(np.int32)
             env.actions.copy_(torch.as_tensor(acts))
         env.step()
         ref.step(acts, players)
@@ -484,3 +486,43 @@ def test_onehot_encoder(mp, po):
             assert got.shape == ref.shape and got.shape[-1] == (33 if po else 29)
             assert np.array_equal(got.cpu().numpy(), ref), f"step {step}"
     env.close()
+
+
+# ------------------------------------------------------------------ JSON unit-type tables
+def _fixture_utt():
+    import os
+
+    return open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "utts", "TestUnitTypeTable.json")).read()
+
+
+@pytest.mark.parametrize("mp,n_sp,n_bot,po,policy", [
+    ("maps/8x8/basesWorkers8x8.xml", 8, 4, False, "masked"),
+    ("maps/16x16/basesWorkers16x16.xml", 4, 2, True, "uniform"),
+])
+def test_utt_from_json_fixture(mp, n_sp, n_bot, po, policy):
+    """The reference's utts/TestUnitTypeTable.json (Base hp 50, Barracks hp 25, harvestTime taken
+    from produceTime by UnitType.updateFromJSON) with every reward function."""
+    S = n_sp + n_bot
+    _rollout.nonzero = np.zeros(len(ALL_RFS), bool)
+    assert not _rollout([mp] * S, n_sp, n_bot, steps=300, policy=policy, partial_obs=po, bots=["RandomBiasedAI"] * n_bot,
+                        rfs=ALL_RFS, utt_json=_fixture_utt(), dump_every=25).any()
+    assert _rollout.nonzero[[6, 7]].all()
+
+
+def test_utt_from_json_eight_types():
+    """A table unlike any built-in one: an 8th type (produced by Workers, defaults for absent
+    members, attack range 2) -> K = 1+6+16+8+49 = 80 mask slots, this build's maximum."""
+    from microrts_amd.vec_client import UnitTypeTable
+    import json
+
+    t = json.loads(UnitTypeTable(2, 3).toJSON())
+    t["unitTypes"][3]["produces"].append("Tower")
+    t["unitTypes"].append({"ID": 7, "name": "Tower", "cost": 3, "hp": 6, "attackRange": 2, "minDamage": 1,
+                           "maxDamage": 3, "canAttack": True, "sightRadius": 4, "produces": [],
+                           "producedBy": ["Worker"]})
+    js = json.dumps(t)
+    mp = "maps/8x8/basesWorkers8x8.xml"
+    _rollout.nonzero = np.zeros(len(ALL_RFS), bool)
+    assert not _rollout([mp] * 8, 6, 2, steps=300, policy="masked", bots=["RandomBiasedAI"] * 2, rfs=ALL_RFS,
+                        utt_json=js, dump_every=25, seed=12).any()
+    assert _rollout.nonzero[[1, 2, 4, 6, 7]].all()
