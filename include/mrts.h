@@ -184,6 +184,21 @@ int mrts_utt_json(int32_t utt_version, int32_t conflict_policy, const char* utt_
 int mrts_error_flags(mrts_env* env, uint32_t* flags);
 /* per-slot envSteps (JNIGridnetVecClient.envSteps, :27); synchronous */
 int mrts_env_steps(mrts_env* env, int32_t* out);
+/* GameState.toJSON (rts/GameState.java:819-837; includeConstants, raw terrain) of the game behind
+ * `slot`; unit IDs are list positions (Java's come from a JVM-global counter).  NUL-terminated;
+ * returns the length, or -(length + 1) when cap is too small.  Synchronous. */
+int mrts_get_state_json(mrts_env* env, int32_t slot, char* buf, int32_t cap);
+/* GameState.fromJSON (rts/GameState.java:889-915) into the game behind `slot` (both slots of a
+ * self-play game): time, players, units, terrain and assignments from the JSON; envSteps and the
+ * cancel counter restart at 0; the game's random streams are kept.  The next mask / policy write of
+ * the handle is a full one.  Synchronous. */
+int mrts_set_state_json(mrts_env* env, int32_t slot, const char* json);
+/* Whole-handle checkpoint / resume: every game's state block (including the random streams, envSteps
+ * and error flags) behind a small header.  mrts_restore accepts only a checkpoint of an identically
+ * configured handle (map size, games, unit-type table).  Synchronous. */
+int64_t mrts_checkpoint_size(const mrts_env* env);
+int mrts_checkpoint(mrts_env* env, void* buf, int64_t cap);
+int mrts_restore(mrts_env* env, const void* buf, int64_t size);
 /* the handle's hipStream_t */
 void* mrts_stream(mrts_env* env);
 /* close() (:318-334) + free */

@@ -21,7 +21,8 @@ ERR_BITS = {
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_step_rows", "mrts_get_masks_i32",
     "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_policy_invalidate", "mrts_set_source_output", "mrts_copy_games", "mrts_copy_games_dev", "mrts_playout", "mrts_playout_dev",
-    "mrts_evaluate", "mrts_evaluate_dev", "mrts_utt_json", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
+    "mrts_evaluate", "mrts_evaluate_dev", "mrts_utt_json", "mrts_get_state_json",
+    "mrts_set_state_json", "mrts_checkpoint_size", "mrts_checkpoint", "mrts_restore", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
 ]
 
@@ -102,6 +103,12 @@ def load(path=LIB_PATH):
     L.mrts_evaluate_dev.argtypes = [P, I32, P, P]
     L.mrts_utt_json.argtypes = [I32, I32, ctypes.c_char_p, ctypes.c_char_p, I32]
     L.mrts_get_state.argtypes = [P, I32, P, I32]
+    L.mrts_get_state_json.argtypes = [P, I32, ctypes.c_char_p, I32]
+    L.mrts_set_state_json.argtypes = [P, I32, ctypes.c_char_p]
+    L.mrts_checkpoint_size.argtypes = [P]
+    L.mrts_checkpoint_size.restype = ctypes.c_int64
+    L.mrts_checkpoint.argtypes = [P, P, ctypes.c_int64]
+    L.mrts_restore.argtypes = [P, P, ctypes.c_int64]
     L.mrts_error_flags.argtypes = [P, P]
     L.mrts_env_steps.argtypes = [P, P]
     L.mrts_stream.argtypes = [P]

@@ -304,6 +304,37 @@ int toInt(const std::string& s) {
     }
 }
 
+// terrain text, raw digits or the A/B run-length form (PhysicalGameState.java:577-607,765-777)
+std::vector<int> decodeTerrain(const std::string& ts, int HW) {
+    std::vector<int> terr;
+    if (ts.find('A') != std::string::npos || ts.find('B') != std::string::npos) {
+        std::string counter;
+        for (char ch : ts) {
+            if (ch == 'A' || ch == 'B') {
+                if (!counter.empty()) {
+                    const int n = toInt(counter);
+                    if (terr.empty() || n < 1 || n > HW) throw Fail{-EINVAL, "terrain: bad run length"};
+                    for (int i = 0; i < n - 1; i++) terr.push_back(terr.back());
+                    counter.clear();
+                }
+                terr.push_back(ch == 'A' ? 0 : 1);
+            } else if (!isspace((unsigned char)ch)) {
+                counter.push_back(ch);
+            }
+        }
+        if (!counter.empty()) {
+            const int n = toInt(counter);
+            if (terr.empty() || n < 1 || n > HW) throw Fail{-EINVAL, "terrain: bad run length"};
+            for (int i = 0; i < n - 1; i++) terr.push_back(terr.back());
+        }
+    } else {
+        for (char ch : ts)
+            if (!isspace((unsigned char)ch)) terr.push_back(ch - '0');
+    }
+    if ((int)terr.size() < HW) throw Fail{-EINVAL, "terrain too short"};
+    return terr;
+}
+
 MapDef parseMap(const std::string& path, const UttInfo& utt) {
     std::ifstream f(path);
     if (!f) throw Fail{-ENOENT, "cannot open map " + path};
@@ -322,30 +353,7 @@ MapDef parseMap(const std::string& path, const UttInfo& utt) {
     if (t0 == std::string::npos || t1 == std::string::npos) throw Fail{-EINVAL, "map: no terrain"};
     const std::string ts = x.substr(t0 + 9, t1 - t0 - 9);
     const int HW = m.W * m.H;
-    std::vector<int> terr;
-    if (ts.find('A') != std::string::npos || ts.find('B') != std::string::npos) {
-        std::string counter;
-        for (char ch : ts) {
-            if (ch == 'A' || ch == 'B') {
-                if (!counter.empty()) {
-                    const int n = toInt(counter);
-                    for (int i = 0; i < n - 1; i++) terr.push_back(terr.back());
-                    counter.clear();
-                }
-                terr.push_back(ch == 'A' ? 0 : 1);
-            } else if (!isspace((unsigned char)ch)) {
-                counter.push_back(ch);
-            }
-        }
-        if (!counter.empty()) {
-            const int n = toInt(counter);
-            for (int i = 0; i < n - 1; i++) terr.push_back(terr.back());
-        }
-    } else {
-        for (char ch : ts)
-            if (!isspace((unsigned char)ch)) terr.push_back(ch - '0');
-    }
-    if ((int)terr.size() < HW) throw Fail{-EINVAL, "map: terrain too short"};
+    const std::vector<int> terr = decodeTerrain(ts, HW);
     m.terrain.resize((size_t)HW);
     for (int i = 0; i < HW; i++) m.terrain[(size_t)i] = terr[(size_t)i] != 0;
     const size_t end = x.find("</rts.PhysicalGameState>", t1);
@@ -1075,6 +1083,255 @@ void mrts_destroy(mrts_env* env) {
     (void)hipHostFree(env->h_done);
     if (env->stream) (void)hipStreamDestroy(env->stream);
     delete env;
+}
+
+// ---------------------------------------------------------------- state serialisation (checkpoint / interop)
+static void readBlock(mrts_env* env, int g, std::vector<int32_t>& s) {
+    const size_t sw = (size_t)stateWords(env->CAP, env->HW);
+    s.resize(sw);
+    HIPCHK(hipStreamSynchronize(env->stream));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(s.data(), env->d_state + (size_t)g * sw, sw * 4, hipMemcpyDeviceToHost));
+}
+
+// GameState.toJSON(w, true, false) (rts/GameState.java:819-837) with PhysicalGameState.toJSON
+// (:658-691), Player.toJSON (Player.java:86-88), Unit.toJSON (Unit.java:577-588) and
+// UnitAction.toJSON (UnitAction.java:569-582).  Unit IDs are list positions: Java's IDs come from a
+// JVM-global counter and are not part of a game's reproducible state.
+static std::string gameToJson(const mrts_env* env, const std::vector<int32_t>& s) {
+    const int CAP = env->CAP, HW = env->HW;
+    const int32_t* A = s.data() + H_WORDS;
+    const uint8_t* terr = (const uint8_t*)(s.data() + stateTerrOff(CAP, HW));
+    const int nu = s[H_NU];
+    std::ostringstream w;
+    w << "{\"time\":" << s[H_TIME] << ",\"pgs\":{\"width\":" << env->W << ",\"height\":" << env->H << ",\"terrain\":\"";
+    for (int i = 0; i < HW; i++) w << (int)terr[i];
+    w << "\",\"players\":[{\"ID\":0, \"resources\":" << s[H_RES0] << "},{\"ID\":1, \"resources\":" << s[H_RES1]
+      << "}],\"units\":[";
+    struct Asg { int seq, unit; };
+    std::vector<Asg> asg;
+    for (int i = 0; i < nu; i++) {
+        const uint32_t c = (uint32_t)A[A_UC * CAP + i];
+        if (i) w << ",";
+        w << "{\"type\":\"" << env->uttInfo.names[(c >> 16) & 0xF] << "\", \"ID\":" << i << ", \"player\":"
+          << (int)((c >> 20) & 3) - 1 << ", \"x\":" << (c & 0xFF) << ", \"y\":" << ((c >> 8) & 0xFF)
+          << ", \"resources\":" << A[A_RES * CAP + i] << ", \"hitpoints\":" << A[A_HP * CAP + i] << "}";
+        if ((uint32_t)A[A_UA * CAP + i] & UA_PRESENT) asg.push_back({A[A_AS * CAP + i], i});
+    }
+    w << "]},\"actions\":[";
+    std::sort(asg.begin(), asg.end(), [](const Asg& a, const Asg& b) { return a.seq < b.seq; });
+    for (size_t k = 0; k < asg.size(); k++) {
+        const int i = asg[k].unit;
+        const uint32_t a = (uint32_t)A[A_UA * CAP + i];
+        const int t = (int)(a & 0xF), prm = (int16_t)A[A_PAR * CAP + i];
+        if (k) w << ",";
+        w << "{\"ID\":" << i << ", \"time\":" << A[A_AT * CAP + i] << ", \"action\":{\"type\":" << t;
+        if (t == 5) {
+            w << ", \"x\":" << ((a >> 8) & 0xFF) << ",\"y\":" << ((a >> 16) & 0xFF);
+        } else {
+            if (prm != -1) w << ", \"parameter\":" << prm;
+            if (t == 4) w << ", \"unitType\":\"" << env->uttInfo.names[(a >> 4) & 0xF] << "\"";
+        }
+        w << "}}";
+    }
+    w << "]}";
+    return w.str();
+}
+
+// GameState.fromJSON (rts/GameState.java:889-915): PhysicalGameState.fromJSON (:735-756, terrain raw
+// or A/B), Player.fromJSON, Unit.fromJSON (Unit.java:629-642: hitpoints default 1), the actions by
+// unit ID in array order (UnitAction.fromJSON, UnitAction.java:647-658).  A new GameState: time from
+// the JSON, unitCancelationCounter 0.  Writes the words of block `s` it describes; everything else
+// (random streams, kind, mask row sets) is kept.  Rejects what Java would throw on (unknown type or
+// ID, two units in a cell) and what this build cannot hold.
+static void jsonToBlock(const mrts_env* env, const std::string& text, std::vector<int32_t>& s) {
+    mjson::Value o;
+    try {
+        o = mjson::parse(text);
+    } catch (const std::exception& e) {
+        throw Fail{-EINVAL, std::string("state json: ") + e.what()};
+    }
+    try {
+        const int CAP = env->CAP, HW = env->HW, W = env->W, H = env->H;
+        const mjson::Value& pg = o.at("pgs");
+        if (pg.getInt("width", 8) != W || pg.getInt("height", 8) != H) throw Fail{-EINVAL, "state json: map size differs from the handle's"};
+        const std::vector<int> terr = decodeTerrain(pg.getString("terrain", ""), HW);
+        const mjson::Value& pl = pg.at("players");
+        if (pl.arr.size() != 2 || pl.arr[0].getInt("ID", -1) != 0 || pl.arr[1].getInt("ID", -1) != 1)
+            throw Fail{-ENOTSUP, "state json: players must be 0 and 1"};
+        const mjson::Value& us = pg.at("units");
+        const int nu = (int)us.arr.size();
+        if (nu > CAP - 64) throw Fail{-ENOSPC, "state json: too many units"};
+        int32_t* A = s.data() + H_WORDS;
+        std::vector<int64_t> ids((size_t)nu);
+        std::vector<char> occ((size_t)HW, 0);
+        for (int a = 0; a < N_ARRAYS; a++)
+            for (int i = 0; i < CAP; i++) A[a * CAP + i] = 0;
+        for (int i = 0; i < nu; i++) {
+            const mjson::Value& u = us.arr[(size_t)i];
+            const int type = env->uttInfo.typeOf(u.getString("type", ""));
+            const int p = u.getInt("player", -1), x = u.getInt("x", 0), y = u.getInt("y", 0);
+            const int r = u.getInt("resources", 0), hp = u.getInt("hitpoints", 1);
+            ids[(size_t)i] = u.getLong("ID", -1);
+            if (type < 0) throw Fail{-EINVAL, "state json: unknown unit type"};
+            if (p < -1 || p > 1 || x < 0 || y < 0 || x >= W || y >= H) throw Fail{-EINVAL, "state json: unit out of range"};
+            if (r < -32768 || r > 32767 || hp < -32768 || hp > 32767) throw Fail{-EINVAL, "state json: value exceeds int16"};
+            if (occ[(size_t)(y * W + x)]) throw Fail{-EINVAL, "state json: two units in one position (addUnit)"};
+            for (int j = 0; j < i; j++)
+                if (ids[(size_t)j] == ids[(size_t)i]) throw Fail{-EINVAL, "state json: repeated unit ID"};
+            occ[(size_t)(y * W + x)] = 1;
+            A[A_UC * CAP + i] = (int32_t)((uint32_t)x | ((uint32_t)y << 8) | ((uint32_t)type << 16) | ((uint32_t)(p + 1) << 20));
+            A[A_HP * CAP + i] = hp;
+            A[A_RES * CAP + i] = r;
+            A[A_PAR * CAP + i] = -1;
+        }
+        const mjson::Value& acts = o.at("actions");
+        int seq = 0;
+        for (auto& av : acts.arr) {
+            const int64_t id = av.getLong("ID", -1);
+            int i = 0;
+            while (i < nu && ids[(size_t)i] != id) i++;
+            if (i == nu) throw Fail{-EINVAL, "state json: action for an unknown unit ID"};
+            const uint32_t c = (uint32_t)A[A_UC * CAP + i];
+            if ((int)((c >> 20) & 3) - 1 < 0) throw Fail{-EINVAL, "state json: action for a neutral unit"};
+            const mjson::Value& ua = av.at("action");
+            const int t = ua.getInt("type", 0), prm = ua.getInt("parameter", -1);
+            const int tx = ua.getInt("x", -1), ty = ua.getInt("y", -1);
+            const std::string utn = ua.getString("unitType", "");
+            int ut = 0;
+            if (t < 0 || t > 5) throw Fail{-EINVAL, "state json: bad action type"};
+            if (t == 5 && (tx < 0 || ty < 0 || tx >= W || ty >= H)) throw Fail{-ENOTSUP, "state json: attack target off the map"};
+            if (t >= 1 && t <= 4 && (prm < 0 || prm > 3)) throw Fail{-ENOTSUP, "state json: bad direction"};
+            if (t == 0 && (prm < -1 || prm > 32767)) throw Fail{-ENOTSUP, "state json: bad NONE duration"};
+            if (t == 4) {
+                ut = env->uttInfo.typeOf(utn);
+                if (ut < 0) throw Fail{-EINVAL, "state json: unknown produced type"};
+            }
+            const bool again = (uint32_t)A[A_UA * CAP + i] & UA_PRESENT;  // put() on a present key keeps its place
+            A[A_UA * CAP + i] = (int32_t)((uint32_t)t | ((uint32_t)ut << 4) |
+                                          (t == 5 ? ((uint32_t)tx << 8) | ((uint32_t)ty << 16) : 0u) | UA_PRESENT);
+            A[A_PAR * CAP + i] = t == 5 ? -1 : prm;
+            A[A_AT * CAP + i] = av.getInt("time", 0);
+            if (!again) A[A_AS * CAP + i] = seq++;
+        }
+        const mjson::Value& p0 = pl.arr[0];
+        const mjson::Value& p1 = pl.arr[1];
+        s[H_TIME] = o.getInt("time", 0);
+        s[H_NU] = nu;
+        s[H_RES0] = p0.getInt("resources", 0);
+        s[H_RES1] = p1.getInt("resources", 0);
+        s[H_SEQ] = seq;
+        s[H_STEPS] = 0;
+        s[H_ERR] = 0;
+        s[H_CANCEL_CNT] = 0;
+        uint8_t* tb = (uint8_t*)(s.data() + stateTerrOff(CAP, HW));
+        for (int i = 0; i < HW; i++) tb[i] = terr[(size_t)i] != 0;
+        for (int i = HW; i < 4 * ((HW + 3) / 4); i++) tb[i] = 0;
+        for (int i = 0; i < nu; i++) {  // units may not stand on walls (the cell map has one owner per cell)
+            const uint32_t c = (uint32_t)A[A_UC * CAP + i];
+            if (tb[(c & 0xFF) + ((c >> 8) & 0xFF) * W]) throw Fail{-ENOTSUP, "state json: unit on a wall"};
+        }
+    } catch (const std::runtime_error& e) {
+        throw Fail{-EINVAL, std::string("state json: ") + e.what()};
+    }
+}
+
+int mrts_get_state_json(mrts_env* env, int32_t slot, char* buf, int32_t cap) {
+    try {
+        if (!env || slot < 0 || slot >= env->nSlots) throw Fail{-EINVAL, "slot out of range"};
+        int pl;
+        std::vector<int32_t> s;
+        readBlock(env, env->gameOfSlot(slot, &pl), s);
+        const std::string j = gameToJson(env, s);
+        if (!buf || cap < (int32_t)j.size() + 1) return -((int)j.size() + 1);
+        std::memcpy(buf, j.c_str(), j.size() + 1);
+        return (int)j.size();
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_set_state_json(mrts_env* env, int32_t slot, const char* json) {
+    try {
+        if (!env || !json || slot < 0 || slot >= env->nSlots) throw Fail{-EINVAL, "bad argument"};
+        int pl;
+        const int g = env->gameOfSlot(slot, &pl);
+        std::vector<int32_t> s;
+        readBlock(env, g, s);
+        jsonToBlock(env, json, s);
+        const size_t sw = s.size();
+        HIPCHK(hipMemcpy(env->d_state + (size_t)g * sw, s.data(), sw * 4, hipMemcpyHostToDevice));
+        env->lastMaskPtr = nullptr;  // the next mask write is a full one
+        env->polValid = false;
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+// whole-handle checkpoint: a header + every game's state block (random streams, envSteps, kind included)
+namespace {
+struct CkptHeader {
+    char magic[8];
+    int32_t version, H, W, CAP, nGames, nSpGames, words;
+    uint32_t uttHash;
+};
+uint32_t uttHash(const DevUtt& u) {
+    uint32_t h = 2166136261u;
+    const uint8_t* p = (const uint8_t*)&u;
+    for (size_t i = 0; i < sizeof(DevUtt); i++) h = (h ^ p[i]) * 16777619u;
+    return h;
+}
+}  // namespace
+
+int64_t mrts_checkpoint_size(const mrts_env* env) {
+    if (!env) return -EINVAL;
+    return (int64_t)sizeof(CkptHeader) + (int64_t)stateWords(env->CAP, env->HW) * env->nGames * 4;
+}
+
+int mrts_checkpoint(mrts_env* env, void* buf, int64_t cap) {
+    try {
+        if (!env || !buf) throw Fail{-EINVAL, "null argument"};
+        if (cap < mrts_checkpoint_size(env)) throw Fail{-ENOSPC, "buffer too small"};
+        CkptHeader h;
+        std::memset(&h, 0, sizeof(h));
+        std::memcpy(h.magic, "MRTSCKP1", 8);
+        h.version = 1;
+        h.H = env->H;
+        h.W = env->W;
+        h.CAP = env->CAP;
+        h.nGames = env->nGames;
+        h.nSpGames = env->nSpGames;
+        h.words = stateWords(env->CAP, env->HW);
+        h.uttHash = uttHash(env->utt);
+        std::memcpy(buf, &h, sizeof(h));
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy((char*)buf + sizeof(h), env->d_state, (size_t)h.words * h.nGames * 4, hipMemcpyDeviceToHost));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_restore(mrts_env* env, const void* buf, int64_t size) {
+    try {
+        if (!env || !buf) throw Fail{-EINVAL, "null argument"};
+        CkptHeader h;
+        if (size < (int64_t)sizeof(h)) throw Fail{-EINVAL, "checkpoint too short"};
+        std::memcpy(&h, buf, sizeof(h));
+        if (std::memcmp(h.magic, "MRTSCKP1", 8) != 0 || h.version != 1) throw Fail{-EINVAL, "not a checkpoint"};
+        if (h.H != env->H || h.W != env->W || h.CAP != env->CAP || h.nGames != env->nGames || h.nSpGames != env->nSpGames ||
+            h.words != stateWords(env->CAP, env->HW) || h.uttHash != uttHash(env->utt))
+            throw Fail{-EINVAL, "checkpoint of a different configuration"};
+        if (size != mrts_checkpoint_size(env)) throw Fail{-EINVAL, "checkpoint size mismatch"};
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(env->d_state, (const char*)buf + sizeof(h), (size_t)h.words * h.nGames * 4, hipMemcpyHostToDevice));
+        env->lastMaskPtr = nullptr;
+        env->polValid = false;
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
 }
 
 // ---------------------------------------------------------------- forward model

@@ -170,6 +170,27 @@ class _Handle:
         _lib.check(self.L.mrts_error_flags(self.h, f.ctypes.data_as(ctypes.c_void_p)))
         return f
 
+    def state_json(self, slot):
+        n = self.L.mrts_get_state_json(self.h, slot, None, 0)  # -(length + 1), or an errno
+        if n > -64:
+            _lib.check(n if n < 0 else -22)
+        buf = ctypes.create_string_buffer(-n)
+        n = self.L.mrts_get_state_json(self.h, slot, buf, -n)
+        _lib.check(0 if n >= 0 else n)
+        return buf.value.decode()
+
+    def set_state_json(self, slot, text):
+        _lib.check(self.L.mrts_set_state_json(self.h, slot, text.encode() if isinstance(text, str) else text))
+
+    def checkpoint(self):
+        n = self.L.mrts_checkpoint_size(self.h)
+        buf = ctypes.create_string_buffer(n)
+        _lib.check(self.L.mrts_checkpoint(self.h, buf, n))
+        return buf.raw
+
+    def restore(self, data):
+        _lib.check(self.L.mrts_restore(self.h, ctypes.c_char_p(bytes(data)), len(data)))
+
     def env_steps(self):
         f = np.zeros(self.S, np.int32)
         _lib.check(self.L.mrts_env_steps(self.h, f.ctypes.data_as(ctypes.c_void_p)))
@@ -207,6 +228,21 @@ class JNIGridnetVecClient:
     def sendUTT(self):
         """The unit-type table as JSON (JNIGridnetClient.sendUTT, :225-233)."""
         return self.utt.toJSON()
+
+    def getGameStateJSON(self, slot):
+        """GameState.toJSON of the game behind `slot` (unit IDs = list positions)."""
+        return self._h.state_json(slot)
+
+    def setGameStateJSON(self, slot, text):
+        """GameState.fromJSON into the game behind `slot` (envSteps restarts at 0)."""
+        self._h.set_state_json(slot, text)
+
+    def checkpoint(self):
+        """bytes holding every game's state (random streams and envSteps included)."""
+        return self._h.checkpoint()
+
+    def restore(self, data):
+        self._h.restore(data)
 
     @classmethod
     def bots(cls, a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai1s, a_ai2s, a_utt=None, partial_obs=False, device=0,
@@ -391,6 +427,27 @@ class DeviceVecEnv:
         self.synchronize()
         return self._h.error_flags()
 
+    def state_json(self, slot):
+        """GameState.toJSON of the game behind `slot` (unit IDs = list positions)."""
+        self.synchronize()
+        return self._h.state_json(slot)
+
+    def set_state_json(self, slot, text):
+        """GameState.fromJSON into the game behind `slot`; call get_masks() before a policy reads masks."""
+        self.synchronize()
+        self._h.set_state_json(slot, text)
+        self._policy_out = None
+
+    def checkpoint(self):
+        self.synchronize()
+        return self._h.checkpoint()
+
+    def restore(self, data):
+        """Every game's state from checkpoint(); call get_masks() before a policy reads masks."""
+        self.synchronize()
+        self._h.restore(data)
+        self._policy_out = None
+
     @property
     def dims(self):
         h = self._h
@@ -474,6 +531,14 @@ class ForwardModel:
     def error_flags(self):
         self.synchronize()
         return self._h.error_flags()
+
+    def state_json(self, game):
+        self.synchronize()
+        return self._h.state_json(game)
+
+    def set_state_json(self, game, text):
+        self.synchronize()
+        self._h.set_state_json(game, text)
 
     def close(self):
         self.synchronize()

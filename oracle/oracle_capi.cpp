@@ -544,6 +544,36 @@ int oref_dump_state(void* h, int slot, int32_t* buf, int cap) {
 }
 
 int oref_env_steps(void* h, int slot) { return ((VecClient*)h)->envSteps[(size_t)slot]; }
+// GameState.toJSON of the game behind `slot`; returns the length or -(length + 1)
+int oref_state_json(void* h, int slot, char* buf, int cap) {
+    int p;
+    const std::string j = gameStateToJSON(*((VecClient*)h)->slotEnv(slot, &p)->gs);
+    if (!buf || cap < (int)j.size() + 1) return -((int)j.size() + 1);
+    std::memcpy(buf, j.c_str(), j.size() + 1);
+    return (int)j.size();
+}
+// GameState.fromJSON into the game behind `slot` (its random streams kept, envSteps restarts at 0)
+int oref_set_state_json(void* h, int slot, const char* json) {
+    try {
+        auto v = (VecClient*)h;
+        int p;
+        Env* e = v->slotEnv(slot, &p);
+        e->gs = gameStateFromJSON(json, v->world->utt);
+        e->gs->cancelRandom = &e->cancelGen;
+        e->gs->damageRandom = &e->damageGen;
+        const int nsp = (int)v->selfPlay.size() * 2;
+        if (slot < nsp) {
+            v->envSteps[(size_t)(slot & ~1)] = 0;
+            v->envSteps[(size_t)(slot | 1)] = 0;
+        } else {
+            v->envSteps[(size_t)slot] = 0;
+        }
+        return 0;
+    } catch (std::exception& ex) {
+        g_err = ex.what();
+        return -22;
+    }
+}
 int oref_errors(void* h, int slot) {
     int p;
     return ((VecClient*)h)->slotEnv(slot, &p)->gs->errors;

@@ -1088,3 +1088,103 @@ std::vector<int32_t> dumpState(const GameState& gs) {
 }
 
 }  // namespace oref
+
+namespace oref {
+// GameState.toJSON (rts/GameState.java:819-837) + PhysicalGameState.toJSON (:658-691) + Player /
+// Unit / UnitAction.toJSON (Player.java:86-88, Unit.java:577-588, UnitAction.java:569-582)
+std::string gameStateToJSON(const GameState& gs) {
+    const PhysicalGameState& p = *gs.pgs;
+    std::ostringstream w;
+    w << "{\"time\":" << gs.time << ",\"pgs\":";
+    w << "{\"width\":" << p.width << ",\"height\":" << p.height << ",\"terrain\":\"";
+    for (int i = 0; i < p.height * p.width; i++) w << (*p.terrain)[(size_t)i];
+    w << "\",\"players\":[";
+    for (size_t i = 0; i < p.players.size(); i++) {
+        w << "{\"ID\":" << p.players[i]->ID << ", \"resources\":" << p.players[i]->resources << "}";
+        if (i + 1 < p.players.size()) w << ",";
+    }
+    w << "],\"units\":[";
+    for (size_t i = 0; i < p.units.size(); i++) {
+        const Unit& u = *p.units[i];
+        w << "{\"type\":\"" << u.type->name << "\", \"ID\":" << u.ID << ", \"player\":" << u.player << ", \"x\":" << u.x
+          << ", \"y\":" << u.y << ", \"resources\":" << u.resources << ", \"hitpoints\":" << u.hitpoints << "}";
+        if (i + 1 < p.units.size()) w << ",";
+    }
+    w << "]}";
+    w << ",\"actions\":[";
+    bool first = true;
+    for (auto& uaa : gs.unitActions.order) {
+        if (!first) w << ",";
+        first = false;
+        const UnitAction& a = *uaa->action;
+        w << "{\"ID\":" << uaa->unit->ID << ", \"time\":" << uaa->time << ", \"action\":";
+        w << "{\"type\":" << a.type;
+        if (a.type == UnitAction::TYPE_ATTACK_LOCATION) {
+            w << ", \"x\":" << a.x << ",\"y\":" << a.y;
+        } else {
+            if (a.parameter != UnitAction::DIRECTION_NONE) w << ", \"parameter\":" << a.parameter;
+            if (a.unitType) w << ", \"unitType\":\"" << a.unitType->name << "\"";
+        }
+        w << "}}";
+    }
+    w << "]";
+    w << "}";
+    return w.str();
+}
+
+// GameState.fromJSON (:889-915): PhysicalGameState.fromJSON (:735-756), Player.fromJSON
+// (Player.java:106-110), Unit.fromJSON (Unit.java:629-642), UnitAction.fromJSON (UnitAction.java:647-658)
+GSP gameStateFromJSON(const std::string& json, const UnitTypeTable& utt) {
+    const mjson::Value o = mjson::parse(json);
+    const mjson::Value& po = o.at("pgs");
+    auto p = std::make_shared<PhysicalGameState>();
+    p->width = po.getInt("width", 8);
+    p->height = po.getInt("height", 8);
+    const std::string ts = po.getString("terrain", "");
+    std::vector<int> terr((size_t)(p->width * p->height), 0);
+    if (ts.find('A') != std::string::npos || ts.find('B') != std::string::npos) {
+        MapTemplate t = parseMapXML("<rts.PhysicalGameState width=\"" + std::to_string(p->width) + "\" height=\"" +
+                                    std::to_string(p->height) + "\"><terrain>" + ts +
+                                    "</terrain><players></players><units></units></rts.PhysicalGameState>");
+        terr = t.terrain;
+    } else {
+        for (size_t i = 0; i < terr.size(); i++) terr[i] = ts.at(i) - '0';
+    }
+    p->terrain = std::make_shared<std::vector<int>>(terr);
+    for (auto& v : po.at("players").arr) p->players.push_back(std::make_shared<Player>(Player{v.getInt("ID", -1), v.getInt("resources", 0)}));
+    for (auto& v : po.at("units").arr) {
+        auto u = std::make_shared<Unit>();
+        u->ID = v.getLong("ID", -1);
+        if (u->ID >= g_next_ID) g_next_ID = u->ID + 1;
+        u->player = v.getInt("player", -1);
+        u->type = utt.getUnitType(v.getString("type", ""));
+        if (!u->type) throw std::runtime_error("unknown unit type");
+        u->x = v.getInt("x", 0);
+        u->y = v.getInt("y", 0);
+        u->resources = v.getInt("resources", 0);
+        u->hitpoints = v.getInt("hitpoints", 1);
+        p->addUnit(u);
+    }
+    auto gs = std::make_shared<GameState>(p, &utt);
+    gs->time = o.getInt("time", 0);
+    for (auto& v : o.at("actions").arr) {
+        const int64_t id = v.getLong("ID", -1);
+        UnitP u;
+        for (auto& x : p->units)
+            if (x->ID == id) {
+                u = x;
+                break;
+            }
+        if (!u) throw std::runtime_error("action for an unknown unit");
+        const mjson::Value& ao = v.at("action");
+        auto a = std::make_shared<UnitAction>(ao.getInt("type", UnitAction::TYPE_NONE));
+        a->parameter = ao.getInt("parameter", UnitAction::DIRECTION_NONE);
+        a->x = ao.getInt("x", UnitAction::DIRECTION_NONE);
+        a->y = ao.getInt("y", UnitAction::DIRECTION_NONE);
+        const std::string ut = ao.getString("unitType", "");
+        if (!ut.empty()) a->unitType = utt.getUnitType(ut);
+        gs->unitActions.put(u, std::make_shared<UnitActionAssignment>(UnitActionAssignment{u, a, v.getInt("time", 0)}));
+    }
+    return gs;
+}
+}  // namespace oref

@@ -287,4 +287,8 @@ void computeMasks(const GameState& gs, const UnitTypeTable& utt, int player, uin
 // Canonical state dump shared with the GPU build (see DESIGN.md §State dump)
 std::vector<int32_t> dumpState(const GameState& gs);
 
+// rts/GameState.java:819-837 toJSON(w, true, false) and :889-915 fromJSON (Java's own unit IDs)
+std::string gameStateToJSON(const GameState& gs);
+GSP gameStateFromJSON(const std::string& json, const UnitTypeTable& utt);
+
 }  // namespace oref

@@ -51,6 +51,8 @@ def load():
         L.oref_botclient_destroy.argtypes = [P]
         L.oref_botclient_step.argtypes = [P, I, P, P]
         L.oref_botclient_dump.argtypes = [P, P, I]
+        L.oref_state_json.argtypes = [P, I, ctypes.c_char_p, I]
+        L.oref_set_state_json.argtypes = [P, I, ctypes.c_char_p]
         L.oref_fm_create.restype = P
         L.oref_fm_create.argtypes = [ctypes.c_char_p, I, P, P, I, I, ctypes.c_int64, ctypes.c_char_p]
         L.oref_fm_destroy.argtypes = [P]
@@ -137,6 +139,16 @@ class OracleVecClient:
 
     def env_steps(self, slot):
         return self.L.oref_env_steps(self.h, slot)
+
+    def state_json(self, slot):
+        """GameState.toJSON of the game behind `slot` (Java's unit IDs)."""
+        n = self.L.oref_state_json(self.h, slot, None, 0)
+        buf = ctypes.create_string_buffer(-n)
+        self.L.oref_state_json(self.h, slot, buf, -n)
+        return buf.value.decode()
+
+    def set_state_json(self, slot, text):
+        self._chk(self.L.oref_set_state_json(self.h, slot, text.encode()))
 
     def close(self):
         if self.h:
