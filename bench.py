@@ -34,6 +34,14 @@ SEED = 0x5EEDC0DE
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
+# BASELINE.json configs: (map, self-play games per GPU, partial observability)
+CONFIGS = {
+    "c2": ("maps/8x8/basesWorkers8x8.xml", 1024, False),
+    "c3": (MAP, 4096, False),
+    "c5": ("maps/BWDistantResources32x32.xml", 2048, True),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -41,8 +49,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--burnin", type=int, default=1000,
                     help="untimed steps from reset before warmup: the timed window sees mid-episode unit counts")
-    ap.add_argument("--envs", type=int, default=4096, help="self-play games per GPU")
-    ap.add_argument("--map", default=MAP)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
+                    help="BASELINE.json workload preset (c3 = the headline; c2 / c5 = the other single-GPU configs)")
+    ap.add_argument("--envs", type=int, default=None, help="self-play games per GPU (default: the preset's)")
+    ap.add_argument("--map", default=None)
     ap.add_argument("--mask-mode", choices=["delta", "full"], default="delta",
                     help="delta: the persistent mask tensor is updated in place (only changed rows written); "
                          "full: every mask byte is rewritten each step")
@@ -55,7 +65,12 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per step-kernel launch from a rocprofv3 --pmc pass (profiles/), for roofline.traffic")
-    return ap.parse_args()
+    a = ap.parse_args()
+    m, e, po = CONFIGS[a.config]
+    a.map = a.map or m
+    a.envs = a.envs or e
+    a.po = po
+    return a
 
 
 class _FenceFreeEvent:
@@ -149,6 +164,7 @@ def main():
     E = a.envs
     sh = mdist.shard(rank, E)
     env = DeviceVecEnv(sh["n_slots"], 0, 2000, [os.path.join(ROOT, a.map)] * sh["n_slots"], device=local, seed=SEED,
+                       partial_obs=a.po,
                        slot_id_base=sh["slot_id_base"], mask_delta=a.mask_mode == "delta",
                        source_bits=a.mask_mode == "delta")
     S, H, W, C, K = env.dims
@@ -288,7 +304,8 @@ def main():
         "dtype": "int32",
         "data": "synthetic (masked uniform random policy, Philox seed 0x5EEDC0DE)",
         "config": {
-            "workload": f"c3/c4: {a.map} self-play, {E} games/GPU ({2 * E} player slots), masks+obs every step",
+            "workload": f"{a.config}: {a.map} self-play, {E} games/GPU ({2 * E} player slots), masks+obs every step"
+                        + (", partial observability" if a.po else ""),
             "envs_per_gpu": E,
             "utt": "VERSION_ORIGINAL, CANCEL_BOTH",
             "max_steps": 2000,
@@ -320,7 +337,7 @@ def main():
             "survey_8d_equivalent_GBps": survey / (kern_ms * 1e-3) / 1e9,
         },
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.po:
         out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin)
     if rank == 0:
         sys.stdout.flush()

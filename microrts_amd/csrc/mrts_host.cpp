@@ -452,7 +452,14 @@ struct mrts_env {
     const int32_t* lastPolicyActions = nullptr;
     bool polValid = false;
     int polParity = 0;
+    // the kernels store observations and mask chunks as 16-byte vectors
+    static void checkAlign(const KDyn& D) {
+        if (((uintptr_t)D.obs & 15) || ((uintptr_t)D.masks & 15)) throw Fail{-EINVAL, "obs / masks buffers must be 16-byte aligned"};
+        if (((uintptr_t)D.reward & 7) || ((uintptr_t)D.actions & 3) || ((uintptr_t)D.rows & 3) || ((uintptr_t)D.players & 3))
+            throw Fail{-EINVAL, "misaligned buffer"};
+    }
     void prepMasks(KDyn& D) {
+        checkAlign(D);
         D.source = D.masks ? d_source : nullptr;
         D.mask_delta = (maskDelta && D.masks && D.masks == lastMaskPtr && D.mask_player == lastMaskPlayer) ? 1 : 0;
         if (D.masks) {

@@ -155,6 +155,7 @@ struct Game {
     int32_t* as;     // assignment insertion sequence number (LinkedHashMap order)
     uint32_t* bits;  // running ResourceUsage positions, indices [-W, HW+W)
     uint32_t* scell; // PO: last snapshot unit per cell (slot+1, 0 = none)
+    uint32_t* vis;   // PO: 2 x H rows x ceil(W/32) words of sight-disk bitmaps (after scell)
     int32_t* rseq;   // ready-list scratch (64)
     uint32_t* mprev; // previous mask row sets, [2][maskWords(HW)] (delta mask writes)
     int32_t* rwc;    // reward counters [player][RC_*] of the pairs issued this step
@@ -206,6 +207,7 @@ struct Game {
         rslot = (uint16_t*)q; q += 2 * 64;
         snap = (uint8_t*)q; q += (CAP + 3) & ~3;
         scell = (uint32_t*)q;  // PO only, last: the offsets above do not depend on it
+        vis = scell + HW;
         ixValid = false;
     }
     // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
@@ -919,10 +921,15 @@ struct Game {
             }
         }
         anyMP = ballot(mp) != 0;
-        maxProd0 = -wave_min(-mc0);
-        maxProd1 = -wave_min(-mc1);
-        sumProd0 = wave_sum(s0);
-        sumProd1 = wave_sum(s1);
+        if (ballot(mc0 >= 0 || mc1 >= 0)) {  // any present PRODUCE (rare)
+            maxProd0 = -wave_min(-mc0);
+            maxProd1 = -wave_min(-mc1);
+            sumProd0 = wave_sum(s0);
+            sumProd1 = wave_sum(s1);
+        } else {
+            maxProd0 = maxProd1 = -1;
+            sumProd0 = sumProd1 = 0;
+        }
         ixValid = true;
         wsync();
     }
@@ -993,10 +1000,12 @@ struct Game {
             seq += n;
             if (mpm) {
                 anyMP = true;
-                maxProd0 = max(maxProd0, -wave_min(np && pl == 0 ? -ncost : 1));
-                maxProd1 = max(maxProd1, -wave_min(np && pl == 1 ? -ncost : 1));
-                sumProd0 += wave_sum(np && pl == 0 ? ncost : 0);
-                sumProd1 += wave_sum(np && pl == 1 ? ncost : 0);
+                if (ballot(np)) {  // PRODUCE is rare: skip the four reductions otherwise
+                    maxProd0 = max(maxProd0, -wave_min(np && pl == 0 ? -ncost : 1));
+                    maxProd1 = max(maxProd1, -wave_min(np && pl == 1 ? -ncost : 1));
+                    sumProd0 += wave_sum(np && pl == 0 ? ncost : 0);
+                    sumProd1 += wave_sum(np && pl == 1 ? ncost : 0);
+                }
             }
             wsync();
         } else {
@@ -1268,8 +1277,34 @@ struct Game {
     // new PartiallyObservableGameState(gs, p) (rts/PartiallyObservableGameState.java:90-109):
     // the list keeps p's units and every other unit whose cell p observes (:116-126); the
     // assignment map is the live one at this moment (UAA objects shared).
+    // Sight disks (dx^2 + dy^2 <= sightRadius^2 of the seeing unit's type) painted into per-row bitmaps:
+    // lane = seeing unit, one atomicOr per covered row word; a cell is seen iff its bit is set.
+    DEV void paintDisk(uint32_t* rows, uint32_t u) const {
+        const int WPR = (W + 31) >> 5;
+        const int sr = U.sight[utyp(u)], x = ux(u), y = uy(u);
+        for (int dy = -sr; dy <= sr; dy++) {
+            const int yy = y + dy;
+            if (yy < 0 || yy >= H) continue;
+            const int lim = sr * sr - dy * dy;
+            int w = (int)__builtin_sqrtf((float)lim);
+            while (w * w > lim) w--;
+            while ((w + 1) * (w + 1) <= lim) w++;
+            const int x0 = max(0, x - w), x1 = min(W - 1, x + w);
+            for (int k = x0 >> 5; k <= (x1 >> 5); k++) {
+                const int lo = max(x0, 32 * k) - 32 * k, hi = min(x1, 32 * k + 31) - 32 * k;
+                const uint32_t b = (hi - lo == 31) ? 0xFFFFFFFFu : (((1u << (hi - lo + 1)) - 1u) << lo);
+                atomicOr(&rows[yy * WPR + k], b);
+            }
+        }
+    }
+    DEV bool seen(const uint32_t* rows, int x, int y) const {
+        const int WPR = (W + 31) >> 5;
+        return (rows[y * WPR + (x >> 5)] >> (x & 31)) & 1u;
+    }
+    // PartiallyObservableGameState (rts/PartiallyObservableGameState.java:35-71): the view keeps the
+    // units inside the sight of player p's (live) units, with the assignments they hold now.  Lane =
+    // unit, a uniform loop over the observers (few; painting disks costs more here).
     DEV void snapshot(int p) {
-        // observer units: positions + sight, gathered per 64-slot chunk and broadcast by readlane
         for (int o0 = 0; o0 < nu; o0 += 64) {
             const int o = o0 + lane_id();
             uint32_t cu = 0;
@@ -1717,49 +1752,68 @@ struct Game {
         }
         wsync();
         int32_t* out = D.obs + (size_t)slot * P.C * HW;
-        for (int c = lane_id(); c < HW; c += 64) {
+        auto planes = [&](int c, int v[6]) {
             const int s = (int)scell[c] - 1;
-            int v0 = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+            v[0] = v[1] = v[2] = v[3] = v[4] = 0;
+            v[5] = cell[c] == WALL ? 1 : 0;
             if (s >= 0) {
                 const uint32_t cu = uc[s];
                 const int pl = uplay(cu);
-                v0 = hp[s];
-                v1 = res[s];
-                v2 = pl >= 0 ? ((pl + p) % 2) + 1 : 0;
-                v3 = utyp(cu) + 1;
+                v[0] = hp[s];
+                v[1] = res[s];
+                v[2] = pl >= 0 ? ((pl + p) % 2) + 1 : 0;
+                v[3] = utyp(cu) + 1;
                 const int sa = snap_act(snap[s], p);
-                v4 = sa ? sa - 1 : 0;
+                v[4] = sa ? sa - 1 : 0;
             }
-            out[c] = v0;
-            out[HW + c] = v1;
-            out[2 * HW + c] = v2;
-            out[3 * HW + c] = v3;
-            out[4 * HW + c] = v4;
-            out[5 * HW + c] = cell[c] == WALL ? 1 : 0;
+        };
+        const bool vec4 = (HW & 3) == 0;  // lane = 4 consecutive cells, one dwordx4 store per plane
+        if (vec4) {
+            for (int c4 = lane_id(); c4 < HW / 4; c4 += 64) {
+                int v[4][6];
+#pragma unroll
+                for (int j = 0; j < 4; j++) planes(4 * c4 + j, v[j]);
+#pragma unroll
+                for (int k = 0; k < 6; k++)
+                    *(int4*)(out + k * HW + 4 * c4) = make_int4(v[0][k], v[1][k], v[2][k], v[3][k]);
+            }
+        } else {
+            for (int c = lane_id(); c < HW; c += 64) {
+                int v[6];
+                planes(c, v);
+#pragma unroll
+                for (int k = 0; k < 6; k++) out[k * HW + c] = v[k];
+            }
         }
-        // visibility: lane = cell, uniform loop over the snapshot's owned units
-        for (int c0 = 0; c0 < HW; c0 += 64) {
-            const int c = c0 + lane_id();
-            const int cx = c % W, cy = c / W;
-            int mine = 0, theirs = 0;
-            for (int o0 = 0; o0 < nu; o0 += 64) {
-                const int o = o0 + lane_id();
-                const uint32_t oc = o < nu ? uc[o] : 0u;
-                uint64_t m = ballot(o < nu && snap_in(snap[o], p) && uplay(oc) >= 0);
-                while (m) {
-                    const int k = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint32_t u = (uint32_t)rl((int)oc, k);
-                    const int sr = U.sight[utyp(u)];
-                    const int dx = cx - ux(u), dy = cy - uy(u);
-                    const bool in = abs(dx) <= sr && abs(dy) <= sr && dx * dx + dy * dy <= sr * sr;
-                    if (uplay(u) == p) mine |= in;
-                    else theirs |= in;
+        // visibility planes over the view's units at their current positions (dead ones included: the
+        // view's list still holds them): own / other player's sight disks
+        const int NW = H * ((W + 31) >> 5);
+        uint32_t* mineRows = vis;
+        uint32_t* theirRows = vis + NW;
+        for (int i = lane_id(); i < 2 * NW; i += 64) vis[i] = 0;
+        wsync();
+        for (int o = lane_id(); o < nu; o += 64) {
+            const uint32_t cu = uc[o];
+            if (snap_in(snap[o], p) && uplay(cu) >= 0) paintDisk(uplay(cu) == p ? mineRows : theirRows, cu);
+        }
+        wsync();
+        if (vec4) {
+            for (int c4 = lane_id(); c4 < HW / 4; c4 += 64) {
+                int m[4], t[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int c = 4 * c4 + j, cx = c % W, cy = c / W;
+                    m[j] = seen(mineRows, cx, cy) ? 1 : 0;
+                    t[j] = seen(theirRows, cx, cy) ? 1 : 0;
                 }
+                *(int4*)(out + 6 * HW + 4 * c4) = make_int4(m[0], m[1], m[2], m[3]);
+                *(int4*)(out + 7 * HW + 4 * c4) = make_int4(t[0], t[1], t[2], t[3]);
             }
-            if (c < HW) {
-                out[6 * HW + c] = mine;
-                out[7 * HW + c] = theirs;
+        } else {
+            for (int c = lane_id(); c < HW; c += 64) {
+                const int cx = c % W, cy = c / W;
+                out[6 * HW + c] = seen(mineRows, cx, cy) ? 1 : 0;
+                out[7 * HW + c] = seen(theirRows, cx, cy) ? 1 : 0;
             }
         }
     }
@@ -2496,7 +2550,7 @@ hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts then [n] 
 #endif
 size_t ldsBytes(int HW, int W, int CAP, int po) {
     return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 + 128 +
-           (po ? 4 * (size_t)HW : 0) +
+           (po ? 4 * (size_t)HW + 8 * (size_t)(HW / W) * (size_t)((W + 31) / 32) : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (((size_t)CAP + 3) & ~(size_t)3);
 }
 // MicroRTS-Py GridnetVecEnv observation encoding (gym_microrts `_encode_obs`: clip each plane to

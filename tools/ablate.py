@@ -14,11 +14,12 @@ from microrts_amd import DeviceVecEnv, _lib  # noqa: E402
 
 E = int(os.environ.get("E", 4096))
 MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
+PO = os.environ.get("PO", "0") == "1"
 SEED = 0x5EEDC0DE
 
 
 def run(obs_on, masks_on, burnin=1000, steps=50):
-    env = DeviceVecEnv(2 * E, 0, 2000, [MAP] * (2 * E), seed=1)
+    env = DeviceVecEnv(2 * E, 0, 2000, [MAP] * (2 * E), seed=1, partial_obs=PO)
     L, h = env._h.L, env._h.h
     P = env._p
     stream = torch.cuda.current_stream()

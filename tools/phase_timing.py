@@ -23,6 +23,7 @@ NAMES = ["load", "predecode", "decode(chain)", "issue", "cycle", "outcome+reset"
          "buildIndexCalls(x1000)"]
 E = int(os.environ.get("E", 4096))
 MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
+PO = os.environ.get("PO", "0") == "1"
 SEED = 0x5EEDC0DE
 
 
@@ -33,7 +34,8 @@ def read(reset):
 
 
 for delta in (True, False):
-    env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=1, mask_delta=delta, source_bits=delta)
+    env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=1, mask_delta=delta, source_bits=delta,
+                       partial_obs=PO)
     env.reset()
     for k in range(int(os.environ.get("BURNIN", 1000))):
         env.random_policy(SEED, k)
