@@ -148,6 +148,7 @@ struct Game {
     const KDyn& D;  // the kernel argument itself (kernarg memory): fields load on demand
     const DevUtt& U;
     int g, H, W, HW, CAP;
+    int K, NT, R;  // mask slots per cell, unit types, attack window (2 * max range + 1): table values or constants
     bool po;
     uint32_t* uc;    // unit core: x | y<<8 | type<<16 | (player+1)<<20 | dead<<31
     uint32_t* ua;    // assignment: type | utype<<4 | tx<<8 | ty<<16 | PRESENT/READY/PA/DEC/BAD
@@ -188,8 +189,9 @@ struct Game {
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
     // array offset then folds to an immediate), else the kernel arguments
-    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem, int h, int w, int hw, int cap, bool partial)
-        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), po(partial) {
+    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem, int h, int w, int hw, int cap, bool partial, int k, int nt, int r)
+        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
+          po(partial) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
         ua = (uint32_t*)q; q += 4 * CAP;
@@ -446,7 +448,7 @@ struct Game {
     // UnitAction.fromVectorAction (rts/UnitAction.java:675-709) of row components a[0..6] for a unit
     // with core word cu
     DEV bool decodeFields(uint32_t cu, const int32_t a[7], int& t, int& pr, int& ut, int& tx, int& ty) const {
-        const int R = U.maxAttackRadius, ctr = R / 2;
+        const int ctr = R / 2;
         const int x = ux(cu), y = uy(cu);
         t = (a[0] >= 0 && a[0] <= 5) ? a[0] : ACT_INVALID;
         pr = -1;
@@ -458,7 +460,7 @@ struct Game {
             case T_RETURN: pr = clampdir(a[3]); break;
             case T_PRODUCE:
                 pr = clampdir(a[4]);
-                if (a[5] < 0 || a[5] >= U.ntypes) bad = true;  // utt.getUnitType(int) throws (:697)
+                if (a[5] < 0 || a[5] >= NT) bad = true;  // utt.getUnitType(int) throws (:697)
                 else ut = a[5];
                 break;
             case T_ATTACK: {
@@ -1831,7 +1833,7 @@ struct Game {
         const uint32_t cu = uc[s];
         const int x = ux(cu), y = uy(cu), typ = utyp(cu), pl = uplay(cu);
         const uint32_t fl = U.flags[typ];
-        const int nt = U.ntypes, R = U.maxAttackRadius, ctr = R / 2;
+        const int nt = NT, ctr = R / 2;
         const int atkBase = 1 + 6 + 16 + nt;
         setb(0);
         setb(1 + T_NONE);
@@ -1930,7 +1932,6 @@ struct Game {
     static DEV uint32_t expand4(uint32_t b) { return ((b & 0xFu) * 0x00204081u) & 0x01010101u; }
     // one 16-byte chunk j of the [HW][K] byte mask of player p, from the parked per-unit bits
     DEV uint4 maskChunk(int j, int p) const {
-        const int K = U.K;
         const int o0 = 16 * j;
         const int cA = o0 / K, kA = o0 - cA * K;
         uint64_t lo;
@@ -1960,7 +1961,6 @@ struct Game {
     // unit — the buffer ends up identical.  The dirty cells of both slots are gathered into one list
     // and their chunks are spread over the lanes, so a typical step is a single parallel pass.
     DEV void writeMasks(int slot0, int nslots, int pl0, int pl1) {
-        const int K = U.K;
         const int total = HW * K;
         const int MW = maskWords(HW);
         const bool delta = D.mask_delta && (total & 15) == 0;
@@ -2064,7 +2064,7 @@ struct Game {
     // rewrite the chunks of the listed dirty cells (rslot[0..n): slot index << 15 | cell)
     DEV void flushDirty(int n, int slot0, int pl0, int pl1) {
         wsync();
-        const int K = U.K, total = HW * K;
+        const int total = HW * K;
         const int NCH = (K + 14) / 16 + 1;  // chunks a K-byte record can touch
         for (int base = 0; base < NCH * n; base += 64) {
             const int item = base + lane_id();
@@ -2093,8 +2093,9 @@ template <int MODE, int FIX>
 __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
+    // FIX: the built-in tables' K = 79, 7 types, attack window 7 are constants too (launchEnv checks)
     Game G(P, D, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FIX * FIX + 64 : D.CAP,
-           FIX ? false : P.partial_obs != 0);
+           FIX ? false : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius);
     // games [0, n_sp_games) are self-play (mrts_create's layout): no load needed to place the slots
     const bool selfplay = FIX ? true : G.g < D.n_sp_games;
     const int slot0 = selfplay ? 2 * G.g : 2 * D.n_sp_games + (G.g - D.n_sp_games);
@@ -2713,7 +2714,8 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
     const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);
     dim3 grid((unsigned)hs.n_games), block(64);
     const bool fix16 = hs.H == 16 && hs.W == 16 && hs.CAP == 16 * 16 + 64 && !hs.partial_obs &&
-                       hs.n_sp_games == hs.n_games && D.rows == nullptr;
+                       hs.n_sp_games == hs.n_games && D.rows == nullptr && hs.utt.K == 79 && hs.utt.ntypes == 7 &&
+                       hs.utt.maxAttackRadius == 7;
     switch (mode) {
         case MODE_STEP:
             if (fix16) hipLaunchKernelGGL((k_env<MODE_STEP, 16>), grid, block, lds, stream, ds, D);
