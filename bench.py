@@ -34,11 +34,14 @@ SEED = 0x5EEDC0DE
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
-# BASELINE.json configs: (map, self-play games per GPU, partial observability)
+# BASELINE.json configs: (map, self-play games per GPU, partial observability, max_units)
+# c5: the 32x32 map's live units never exceeded 32 in 2500-step random-policy games (oracle); a
+# 256-unit bound (error flags checked after the run) lets all 2048 games be resident at once.
 CONFIGS = {
-    "c2": ("maps/8x8/basesWorkers8x8.xml", 1024, False),
-    "c3": (MAP, 4096, False),
-    "c5": ("maps/BWDistantResources32x32.xml", 2048, True),
+    "c2": ("maps/8x8/basesWorkers8x8.xml", 1024, False, 0),
+    "c3": (MAP, 4096, False, 0),
+    "c5": ("maps/BWDistantResources32x32.xml", 2048, True, 256),
+    "c5-exact": ("maps/BWDistantResources32x32.xml", 2048, True, 0),
 }
 
 
@@ -66,10 +69,11 @@ def parse():
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per step-kernel launch from a rocprofv3 --pmc pass (profiles/), for roofline.traffic")
     a = ap.parse_args()
-    m, e, po = CONFIGS[a.config]
+    m, e, po, mu = CONFIGS[a.config]
     a.map = a.map or m
     a.envs = a.envs or e
     a.po = po
+    a.max_units = mu
     return a
 
 
@@ -164,7 +168,7 @@ def main():
     E = a.envs
     sh = mdist.shard(rank, E)
     env = DeviceVecEnv(sh["n_slots"], 0, 2000, [os.path.join(ROOT, a.map)] * sh["n_slots"], device=local, seed=SEED,
-                       partial_obs=a.po,
+                       partial_obs=a.po, max_units=a.max_units,
                        slot_id_base=sh["slot_id_base"], mask_delta=a.mask_mode == "delta",
                        source_bits=a.mask_mode == "delta")
     S, H, W, C, K = env.dims
@@ -305,7 +309,8 @@ def main():
         "data": "synthetic (masked uniform random policy, Philox seed 0x5EEDC0DE)",
         "config": {
             "workload": f"{a.config}: {a.map} self-play, {E} games/GPU ({2 * E} player slots), masks+obs every step"
-                        + (", partial observability" if a.po else ""),
+                        + (", partial observability" if a.po else "")
+                        + (f", max_units {a.max_units} (capacity errors checked)" if a.max_units else ""),
             "envs_per_gpu": E,
             "utt": "VERSION_ORIGINAL, CANCEL_BOTH",
             "max_steps": 2000,

@@ -84,6 +84,10 @@ typedef struct {
                                    auto-reset; ai1_kinds / bot_kinds are players 0 / 1's playout policies */
     const char* utt_json;       /* non-NULL: UnitTypeTable.fromJSON(utt_json) (UnitTypeTable.java:414-433)
                                    replaces utt_version / conflict_policy (the JSON names its own policy) */
+    int32_t max_units;          /* 0 = H*W (exact for any game).  A smaller bound on live units per game
+                                   shrinks the per-game LDS footprint (more games resident per CU on
+                                   large maps); a game that runs out of unit slots (max_units plus the
+                                   births-in-a-step slack) gets MRTS_ERR_CAPACITY */
 } mrts_config;
 
 typedef struct {               /* ai/jni/Responses.java:12-30 */

@@ -46,6 +46,7 @@ class MrtsConfig(ctypes.Structure):
         ("n_rewards", ctypes.c_int32),
         ("forward_model", ctypes.c_int32),
         ("utt_json", ctypes.c_char_p),
+        ("max_units", ctypes.c_int32),
     ]
 
 

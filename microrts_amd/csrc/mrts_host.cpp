@@ -409,6 +409,7 @@ struct mrts_env {
     int H = 0, W = 0, HW = 0, CAP = 0, C = 6, K = 79;
     int nSlots = 0, nGames = 0, nSpGames = 0, maxSteps = 0, partialObs = 0;
     int forwardModel = 0;  // games advance through mrts_playout* only (GT_PLAYOUT)
+    int maxUnits = 0;      // live-unit bound (H*W unless mrts_config.max_units)
     uint32_t slotIdBase = 0;
     DevUtt utt;
     UttInfo uttInfo;
@@ -603,7 +604,14 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         for (auto& m : maps)
             if (m.H != env->H || m.W != env->W) throw Fail{-EINVAL, "all maps must share env 0's size (JNIGridnetVecClient.java:127-133)"};
         // capacity: one live unit per cell, plus slack for the step's births over its deaths
-        env->CAP = env->HW + std::max(64, env->HW / 4);
+        // unit slots: at most one live unit per cell, plus slack for the births of a step over its
+        // deaths (dead slots are compacted at the end of the step).  max_units lowers the bound on
+        // live units (fewer LDS bytes per game -> more games resident per CU); a game that would
+        // exceed it sets MRTS_ERR_CAPACITY instead of continuing.
+        if (cfg->max_units < 0) throw Fail{-EINVAL, "max_units < 0"};
+        const int maxUnits = cfg->max_units ? std::min(cfg->max_units, env->HW) : env->HW;
+        env->CAP = maxUnits + std::max(64, maxUnits / 4);
+        env->maxUnits = maxUnits;
         if (env->CAP > 0xFFF0) throw Fail{-EINVAL, "map too large"};
         if ((size_t)env->nSlots * env->HW >= (size_t)1 << 31) throw Fail{-EINVAL, "n_slots * H * W must be < 2^31"};
         hipDeviceProp_t prop;
@@ -611,6 +619,8 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         const size_t lds = ldsBytes(env->HW, env->W, env->CAP, env->partialObs);
         if (lds > 160 * 1024) throw Fail{-EINVAL, "map too large for LDS"};
         if (lds > 64 * 1024) HIPCHK(prepareLds(lds));
+        for (auto& m : maps)
+            if ((int)m.units.size() > maxUnits) throw Fail{-ENOSPC, "a map holds more units than max_units"};
         // templates blob
         std::vector<int32_t> blob;
         std::vector<int> off;
@@ -1168,7 +1178,7 @@ static void jsonToBlock(const mrts_env* env, const std::string& text, std::vecto
             throw Fail{-ENOTSUP, "state json: players must be 0 and 1"};
         const mjson::Value& us = pg.at("units");
         const int nu = (int)us.arr.size();
-        if (nu > CAP - 64) throw Fail{-ENOSPC, "state json: too many units"};
+        if (nu > env->maxUnits) throw Fail{-ENOSPC, "state json: more units than the handle's max_units"};
         int32_t* A = s.data() + H_WORDS;
         std::vector<int64_t> ids((size_t)nu);
         std::vector<char> occ((size_t)HW, 0);

@@ -130,7 +130,7 @@ def _kinds(ais, n):
 
 class _Handle:
     def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base,
-                 ai1s=None, mask_delta=False, rewards=None, forward_model=False):
+                 ai1s=None, mask_delta=False, rewards=None, forward_model=False, max_units=0):
         L = _lib.load()
         self.L = L
         self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
@@ -145,7 +145,7 @@ class _Handle:
                               ctypes.cast(self._ai1, P32) if self._ai1 is not None else None,
                               ctypes.cast(self._paths, ctypes.POINTER(ctypes.c_char_p)), device, seed, slot_id_base,
                               int(bool(mask_delta)), ctypes.cast(self._rk, P32), self.R, int(bool(forward_model)),
-                              utt.json.encode() if utt.json else None)
+                              utt.json.encode() if utt.json else None, int(max_units))
         h = ctypes.c_void_p()
         _lib.check(L.mrts_create(ctypes.byref(cfg), ctypes.byref(h)))
         self.h = h
@@ -325,7 +325,7 @@ class DeviceVecEnv:
 
     def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
                  device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None, mask_delta=True, source_bits=True,
-                 rfs=None):
+                 rfs=None, max_units=0):
         """mask_delta: `masks` is owned by this object and reused every call, so only changed rows are
         rewritten (the tensor must not be written by the caller).  source_bits: also keep mask slot 0
         as bits in `source` ([slots][ceil(H*W/32)] int32), which random_policy uses.  rfs: reward
@@ -338,7 +338,8 @@ class DeviceVecEnv:
         utt = utt or UnitTypeTable()
         paths = [_resolve("", p) for p in map_paths]
         self._h = _Handle(num_selfplay_slots, num_bot_envs, max_steps, paths, ai2s, utt, partial_obs, device, seed,
-                          slot_id_base, ai1s=ai1s, mask_delta=mask_delta and with_masks, rewards=_check_rfs(rfs))
+                          slot_id_base, ai1s=ai1s, mask_delta=mask_delta and with_masks, rewards=_check_rfs(rfs),
+                          max_units=max_units)
         h = self._h
         dev = torch.device("cuda", device)
         self.device = dev

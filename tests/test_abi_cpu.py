@@ -31,11 +31,12 @@ def test_library_loads_and_exports_every_symbol():
 
 def test_config_struct_layout():
     # mrts_config: 6 int32, pointer, pointer, int32, uint64, int32 (natural alignment)
-    assert ctypes.sizeof(_lib.MrtsConfig) == 96
+    assert ctypes.sizeof(_lib.MrtsConfig) == 104
     assert _lib.MrtsConfig.seed.offset == 56
     assert _lib.MrtsConfig.mask_delta.offset == 68
     assert _lib.MrtsConfig.reward_kinds.offset == 72 and _lib.MrtsConfig.n_rewards.offset == 80
     assert _lib.MrtsConfig.forward_model.offset == 84 and _lib.MrtsConfig.utt_json.offset == 88
+    assert _lib.MrtsConfig.max_units.offset == 96
 
 
 def test_config_struct_matches_the_c_header(tmp_path):

@@ -42,14 +42,14 @@ def _compare_step(env, ref, step, dump_every, tag=""):
 
 
 def _rollout(maps, n_sp, n_bot=0, steps=200, max_steps=2000, utt=1, crs=1, policy="masked", dump_every=10, seed=3,
-             players=None, partial_obs=False, bots=None, rfs=None, utt_json=None):
+             players=None, partial_obs=False, bots=None, rfs=None, utt_json=None, max_units=0):
     torch = _torch()
     from microrts_amd import DeviceVecEnv, UnitTypeTable
 
     table = UnitTypeTable.fromJSON(utt_json) if utt_json else UnitTypeTable(utt, crs)
     ntypes = len(table.TYPES)
     env = DeviceVecEnv(n_sp, n_bot, max_steps, maps, utt=table, seed=seed, partial_obs=partial_obs,
-                       ai2s=bots, rfs=rfs)
+                       ai2s=bots, rfs=rfs, max_units=max_units)
     kinds = [1 if b == "RandomBiasedAI" else 0 for b in bots] if bots else None
     ref = oracle_py.OracleVecClient(n_sp, n_bot, max_steps, maps, utt_version=utt, crs=crs, seed=seed,
                                     partial_obs=partial_obs, bot_kinds=kinds,
@@ -526,3 +526,18 @@ def test_utt_from_json_eight_types():
     assert not _rollout([mp] * 8, 6, 2, steps=300, policy="masked", bots=["RandomBiasedAI"] * 2, rfs=ALL_RFS,
                         utt_json=js, dump_every=25, seed=12).any()
     assert _rollout.nonzero[[1, 2, 4, 6, 7]].all()
+
+
+@pytest.mark.parametrize("mp,po,mu", [("maps/BWDistantResources32x32.xml", True, 96), ("maps/16x16/basesWorkers16x16.xml", False, 40)])
+def test_max_units_bound(mp, po, mu):
+    """mrts_config.max_units: a smaller unit-slot capacity (the c5 bench preset) plays identically."""
+    assert not _rollout([mp] * 8, 6, 2, steps=200, partial_obs=po, bots=["RandomBiasedAI"] * 2, max_units=mu,
+                        dump_every=20).any()
+
+
+def test_max_units_below_map_units_rejected():
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    with pytest.raises(RuntimeError):
+        DeviceVecEnv(2, 0, 100, ["maps/16x16/basesWorkers16x16.xml"] * 2, max_units=3)
