@@ -2087,15 +2087,17 @@ DEV void aiGetAction(Game& G, int kind, int p) {
     if (kind == GK_RANDOM_BIASED) G.randomBiased(p);
 }
 
-// FIX = 16: specialised for batches of self-play 16x16 games, full observability, grid action
-// layout (the c3/c4 benchmark: CAP = 320; no PO, bot or Java-row code), 0: anything
-template <int MODE, int FIX>
+// Specialisations (FIX = map width, square maps): batches of self-play games with grid actions and a
+// built-in unit-type table (K = 79, 7 types, attack window 7), the map size, unit slots FCAP and
+// observability compile-time constants, so LDS offsets fold into immediates and the bot / Java-row
+// code vanishes — c3 (16x16, 320 slots), c2 (8x8, 128), c5 (32x32 PO, 320 slots = max_units 256).
+// FIX = 0: anything (launchEnv picks).
+template <int MODE, int FIX, int FCAP = 0, bool FPO = false>
 __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
-    // FIX: the built-in tables' K = 79, 7 types, attack window 7 are constants too (launchEnv checks)
-    Game G(P, D, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FIX * FIX + 64 : D.CAP,
-           FIX ? false : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius);
+    Game G(P, D, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
+           FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius);
     // games [0, n_sp_games) are self-play (mrts_create's layout): no load needed to place the slots
     const bool selfplay = FIX ? true : G.g < D.n_sp_games;
     const int slot0 = selfplay ? 2 * G.g : 2 * D.n_sp_games + (G.g - D.n_sp_games);
@@ -2713,12 +2715,14 @@ hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, f
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
     const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);
     dim3 grid((unsigned)hs.n_games), block(64);
-    const bool fix16 = hs.H == 16 && hs.W == 16 && hs.CAP == 16 * 16 + 64 && !hs.partial_obs &&
-                       hs.n_sp_games == hs.n_games && D.rows == nullptr && hs.utt.K == 79 && hs.utt.ntypes == 7 &&
-                       hs.utt.maxAttackRadius == 7;
+    const bool fixable = hs.n_sp_games == hs.n_games && D.rows == nullptr && hs.utt.K == 79 && hs.utt.ntypes == 7 &&
+                         hs.utt.maxAttackRadius == 7 && hs.H == hs.W;
+    auto is = [&](int w, int cap, bool po) { return fixable && hs.W == w && hs.CAP == cap && (hs.partial_obs != 0) == po; };
     switch (mode) {
         case MODE_STEP:
-            if (fix16) hipLaunchKernelGGL((k_env<MODE_STEP, 16>), grid, block, lds, stream, ds, D);
+            if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, ds, D);
+            else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, ds, D);
+            else if (is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, ds, D);
             else hipLaunchKernelGGL((k_env<MODE_STEP, 0>), grid, block, lds, stream, ds, D);
             break;
         case MODE_RESET: hipLaunchKernelGGL((k_env<MODE_RESET, 0>), grid, block, lds, stream, ds, D); break;

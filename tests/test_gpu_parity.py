@@ -530,9 +530,17 @@ def test_utt_from_json_eight_types():
 
 @pytest.mark.parametrize("mp,po,mu", [("maps/BWDistantResources32x32.xml", True, 96), ("maps/16x16/basesWorkers16x16.xml", False, 40)])
 def test_max_units_bound(mp, po, mu):
-    """mrts_config.max_units: a smaller unit-slot capacity (the c5 bench preset) plays identically."""
+    """mrts_config.max_units: a smaller unit-slot capacity plays identically (generic kernel: bot envs)."""
     assert not _rollout([mp] * 8, 6, 2, steps=200, partial_obs=po, bots=["RandomBiasedAI"] * 2, max_units=mu,
                         dump_every=20).any()
+
+
+@pytest.mark.parametrize("mp,po,mu,policy", [("maps/BWDistantResources32x32.xml", True, 256, "masked"),
+                                             ("maps/BWDistantResources32x32.xml", True, 256, "uniform"),
+                                             ("maps/8x8/basesWorkers8x8.xml", False, 0, "uniform")])
+def test_specialised_shapes(mp, po, mu, policy):
+    """The compile-time specialisations of the step kernel: c5 (32x32 PO, 320 slots) and c2 (8x8)."""
+    assert not _rollout([mp] * 16, 16, steps=250, partial_obs=po, max_units=mu, policy=policy, dump_every=25).any()
 
 
 def test_max_units_below_map_units_rejected():
