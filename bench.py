@@ -4,9 +4,13 @@
 Workload (BASELINE.json configs[2]): maps/16x16/basesWorkers16x16.xml, 4096
 self-play games per GPU (8192 player slots), UTT VERSION_ORIGINAL + CANCEL_BOTH, max_steps 2000,
 masked uniform random policy (Philox, seed 0x5EEDC0DE), legal-action masks and observations written
-every step.  One "step" = one batched gameStep of every game on every GPU: the policy kernel reads
-the masks and writes the int32 action tensor, then the fused step kernel (decode -> issueSafe ->
-cycle -> WinLoss -> auto-reset -> observation -> masks) consumes it.  Default mask mode "delta":
+every step.  One "step" = one batched gameStep of every game on every GPU: the step kernel (decode ->
+issueSafe -> cycle -> WinLoss -> auto-reset -> observation -> masks) consumes the int32 action tensor
+in HBM; the synthetic random-policy actions of the next step are sampled from the masks it writes and
+written back to that tensor by the same launch (--policy fused, the default: mrts_step_fused_dev,
+bit-identical to the standalone policy kernel) or by a separate policy launch before each step
+(--policy kernel: what an external agent's launch would look like).  The JSON line also carries the
+other form's throughput over the next K steps ("other_policy_form").  Default mask mode "delta":
 the mask / action tensors are persistent and only rows that changed are rewritten (identical
 contents to a full rewrite, tested); --mask-mode full rewrites every byte.  An env-step is one game-cycle
 (a self-play game counts once, not twice).  Inputs are resident in HBM; nothing crosses PCIe in
@@ -62,9 +66,14 @@ def parse():
     ap.add_argument("--gather-obs", nargs="?", const="allgather", choices=["allgather", "learner"], default=None,
                     help="per-step RCCL exchange of the observation tensor (int16 transport, on its own stream, "
                          "overlapped with the next step): all-gather to every rank, or gather to rank 0")
+    ap.add_argument("--policy", choices=["kernel", "fused"], default="fused",
+                    help="kernel: the random policy is its own launch before each step; fused: the step kernel "
+                         "samples the next step's actions from the masks it writes (mrts_step_fused_dev, same "
+                         "Philox stream, bit-identical actions)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the timed steps eagerly instead of replaying them as one captured hipGraph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-compare", action="store_true", help="skip the other policy form's comparison window")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per step-kernel launch from a rocprofv3 --pmc pass (profiles/), for roofline.traffic")
@@ -177,17 +186,27 @@ def main():
     if a.gather_obs and use_pg:
         gather_buf = mdist.ObservationGather(env.obs.shape, env.device, mode=a.gather_obs)
 
+    fused = a.policy == "fused"
+    mode = {"fused": fused}
+
     def one_step(k, ev=None):
-        env.random_policy(SEED, k)
+        fused = mode["fused"]
+        if not fused:
+            env.random_policy(SEED, k)
         if ev is not None:
             ev[0].record(torch.cuda.current_stream(env.device))
-        env.step()
+        if fused:
+            env.step_fused(SEED, k + 1)  # consumes the actions of step k, writes those of step k + 1
+        else:
+            env.step()
         if ev is not None:
             ev[1].record(torch.cuda.current_stream(env.device))
         if gather_buf is not None:
             gather_buf.push(env.obs)
 
     env.reset()
+    if fused:
+        env.random_policy(SEED, 0)
     for k in range(a.burnin + a.warmup):
         one_step(k)
     env.synchronize()
@@ -281,6 +300,8 @@ def main():
     n_games = S // 2
     m_bytes = dirty * K if a.mask_mode == "delta" else HW * K
     contract = S * (rows * 28 + C * HW * 4 + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
+    if fused:  # the policy's action rows leave the step kernel too
+        contract += S * (dirty if a.mask_mode == "delta" else HW) * 28
     survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16))
     achieved = contract / (kern_ms * 1e-3) / 1e9
     # roofline.traffic: HBM bytes per k_env launch from the rocprofv3 --pmc passes of this same command
@@ -317,6 +338,8 @@ def main():
             "burnin_steps": a.burnin,
             "mask_mode": a.mask_mode,
             "launch": "hipGraph replay of the K timed steps" if graph is not None else "eager",
+            "policy": ("fused into the step kernel (mrts_step_fused_dev)" if fused
+                       else "separate masked-uniform policy kernel before each step (mrts_policy_dev)"),
             "kernel_timing": (f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
                               if graph is not None else f"{event_kind} around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (
@@ -334,7 +357,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "k_env<MODE_STEP>",
+            "kernel": "k_env<MODE_STEP>" + (" + fused policy rows" if fused else ""),
             "alg_bytes_per_launch": contract,
             "alg_bytes_note": f"step contract bytes, {a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "
                               f"changed mask rows per slot (DESIGN.md §5)",
@@ -342,6 +365,27 @@ def main():
             "survey_8d_equivalent_GBps": survey / (kern_ms * 1e-3) / 1e9,
         },
     }
+    if world == 1 and graph is not None and gather_buf is None and not a.no_compare:
+        # the other policy form over the next K steps, for comparison (same contract otherwise)
+        mode["fused"] = not fused
+        base2 = base + a.steps + 5
+        if mode["fused"]:
+            env.random_policy(SEED, base2)
+        g2 = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(env.device)
+        cap.wait_stream(torch.cuda.current_stream(env.device))
+        with torch.cuda.graph(g2, stream=cap):
+            for k in range(a.steps):
+                one_step(base2 + k)
+        torch.cuda.synchronize(env.device)
+        t1 = time.perf_counter()
+        g2.replay()
+        torch.cuda.synchronize(env.device)
+        t2 = time.perf_counter() - t1
+        out["other_policy_form"] = {"policy": "fused" if mode["fused"] else "kernel", "value": total_games * a.steps / t2,
+                                    "ms_per_step": 1e3 * t2 / a.steps}
+        mode["fused"] = fused
+        assert not env.error_flags().any()
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.po:
         out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin)
     if rank == 0:

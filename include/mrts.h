@@ -138,6 +138,14 @@ int mrts_get_masks_i32_dev(mrts_env* env, int32_t player, int32_t* d_out, void* 
  * call mrts_policy_invalidate() after writing d_actions yourself. */
 int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_source, uint64_t seed, uint32_t step,
                     int32_t* d_actions, void* stream);
+/* mrts_step_dev fused with the policy above: consumes d_actions, writes obs / reward / done / masks
+ * (d_masks required), then overwrites d_actions with the policy's actions for step `next_step`
+ * sampled from the masks just written — identical to mrts_policy_dev(env, d_masks, ..., seed,
+ * next_step, d_actions) afterwards, without the second launch and its full pass.  Consecutive fused
+ * calls on the same buffers rewrite only changed rows (mask_delta). */
+int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                        uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step,
+                        void* stream);
 /* the next mrts_policy_dev call writes every row */
 int mrts_policy_invalidate(mrts_env* env);
 /* Optional compact output of every mask write: mask slot 0 ("own unit without an action here") as

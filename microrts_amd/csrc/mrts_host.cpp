@@ -452,6 +452,7 @@ struct mrts_env {
     std::vector<int32_t> rewardKinds{RF_WINLOSS};  // a_rfs
     const int32_t* lastPolicyActions = nullptr;
     bool polValid = false;
+    const int32_t* fusedActions = nullptr;  // buffer the last fused-policy step wrote (delta base), or null
     int polParity = 0;
     // the kernels store observations and mask chunks as 16-byte vectors
     static void checkAlign(const KDyn& D) {
@@ -725,6 +726,7 @@ int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, doub
         D.masks = d_masks;
         D.mask_player = mask_player;
         env->prepMasks(D);
+        env->fusedActions = nullptr;
         HIPCHK(env->launch(1, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
@@ -748,7 +750,39 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
         D.masks = d_masks;
         D.mask_player = mask_player;
         env->prepMasks(D);
+        if (d_masks || d_actions == env->fusedActions) env->fusedActions = nullptr;
         HIPCHK(env->launch(0, D, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                        uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step,
+                        void* stream) {
+    try {
+        if (!d_actions || !d_masks) throw Fail{-EINVAL, "actions and masks are required"};
+        if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
+        HIPCHK(hipSetDevice(env->device));
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.actions = d_actions;
+        D.players = d_players;
+        D.obs = d_obs;
+        D.reward = d_reward;
+        D.done = d_done;
+        D.masks = d_masks;
+        D.mask_player = mask_player;
+        env->prepMasks(D);
+        D.pol_actions = d_actions;
+        D.pol_seed = seed;
+        D.pol_step = next_step;
+        D.pol_slot_base = env->slotIdBase;
+        D.pol_delta = (D.mask_delta && env->fusedActions == d_actions) ? 1 : 0;
+        HIPCHK(env->launch(0, D, pickStream(env, stream)));
+        env->fusedActions = d_actions;
+        if (env->lastPolicyActions == d_actions) env->polValid = false;  // the standalone policy's delta base is stale
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -782,6 +816,7 @@ int mrts_step_rows_dev(mrts_env* env, const int32_t* d_rows, int32_t n_rows, con
         D.masks = d_masks;
         D.mask_player = mask_player;
         env->prepMasks(D);
+        if (d_masks) env->fusedActions = nullptr;
         HIPCHK(env->launch(0, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
@@ -827,6 +862,7 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
         D.mask_player = player;
         D.players = env->d_players;
         env->prepMasks(D);
+        env->fusedActions = nullptr;
         HIPCHK(env->launch(2, D, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
@@ -837,6 +873,7 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
 int mrts_policy_invalidate(mrts_env* env) {
     if (!env) return fail(Fail{-EINVAL, "null handle"});
     env->polValid = false;
+    env->fusedActions = nullptr;
     return 0;
 }
 
@@ -872,6 +909,7 @@ int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_sou
             Q.delta = (env->polValid && d_actions == env->lastPolicyActions) ? 1 : 0;
         }
         bool prevWritten = false;
+        if (d_actions == env->fusedActions) env->fusedActions = nullptr;
         HIPCHK(launchPolicy(Q, pickStream(env, stream), &prevWritten));
         env->polValid = prevWritten;
         if (prevWritten) env->polParity ^= 1;
@@ -1280,6 +1318,7 @@ int mrts_set_state_json(mrts_env* env, int32_t slot, const char* json) {
         HIPCHK(hipMemcpy(env->d_state + (size_t)g * sw, s.data(), sw * 4, hipMemcpyHostToDevice));
         env->lastMaskPtr = nullptr;  // the next mask write is a full one
         env->polValid = false;
+        env->fusedActions = nullptr;
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1345,6 +1384,7 @@ int mrts_restore(mrts_env* env, const void* buf, int64_t size) {
         HIPCHK(hipMemcpy(env->d_state, (const char*)buf + sizeof(h), (size_t)h.words * h.nGames * 4, hipMemcpyHostToDevice));
         env->lastMaskPtr = nullptr;
         env->polValid = false;
+        env->fusedActions = nullptr;
         return 0;
     } catch (const Fail& f) {
         return fail(f);

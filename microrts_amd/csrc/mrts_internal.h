@@ -108,6 +108,12 @@ struct KDyn {
     int32_t n_rows;
     uint32_t* pairs;               // rows mode: per game [n_rows][2] accepted-pair scratch
     int32_t horizon;               // playout mode: NaiveMCTS.simulate(gs, gs.getTime() + horizon)
+    // fused random policy (mrts_step_fused_dev): the next step's action rows, sampled from the masks
+    // this launch writes, go to pol_actions (the buffer the launch consumed); null = off
+    int32_t* pol_actions;
+    uint64_t pol_seed;
+    uint32_t pol_step, pol_slot_base;
+    int32_t pol_delta;             // 1: pol_actions holds the policy rows of the previous mask write's candidates
 };
 
 struct PolicyParams {

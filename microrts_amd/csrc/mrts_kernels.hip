@@ -143,6 +143,63 @@ constexpr int UTT_WORDS = (int)(sizeof(DevUtt) / 4);
 constexpr int UTT_LDS = (int)((sizeof(DevUtt) + 15) & ~(size_t)15);
 static_assert(sizeof(DevUtt) % 4 == 0 && UTT_WORDS <= 192, "DevUtt copy: 3 words per lane");
 
+DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+        c[0] = n0;
+        c[1] = n1;
+        c[2] = n2;
+        c[3] = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+DEV int pickBit(uint32_t r, uint64_t bitsv, int n) {
+    const uint64_t m = n >= 64 ? ~0ull : ((1ull << n) - 1);
+    bitsv &= m;
+    const int cnt = __popcll(bitsv);
+    if (cnt == 0) return -1;
+    int k = (int)(((uint64_t)r * (uint32_t)cnt) >> 32);
+    while (k--) bitsv &= bitsv - 1;
+    return __builtin_ctzll(bitsv);
+}
+// one cell's action from its mask bits (lo/hi: mask slots 1..K-1 -> bit i-1), Philox counter
+// (slot id, step, cell, 0)
+// Masked-uniform random policy of one cell (the bench / rollout agent): mask slots 1..K-1 as bits
+// (lo: slots 1..64, hi: 65..), Philox4x32-10 with key = seed, counter = (slot id, step, cell, 0)
+DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes, int K, uint64_t lo, uint64_t hi, int c,
+                       int32_t a[7]) {
+    for (int k = 0; k < 7; k++) a[k] = 0;
+    uint32_t ctr[4] = {slotId, step, (uint32_t)c, 0u};
+    philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    auto field = [&](int off, int n) -> uint64_t {  // mask slots [off, off+n) (off >= 1)
+        const int b = off - 1;
+        uint64_t v;
+        if (b >= 64) v = hi >> (b - 64);
+        else v = (lo >> b) | (b ? (hi << (64 - b)) : 0ull);
+        return n >= 64 ? v : (v & ((1ull << n) - 1));
+    };
+    const int t = pickBit(ctr[0], field(1, 6), 6);
+    if (t < 0) return;
+    a[0] = t;
+    switch (t) {
+        case 1: a[1] = pickBit(ctr[1], field(7, 4), 4); break;
+        case 2: a[2] = pickBit(ctr[1], field(11, 4), 4); break;
+        case 3: a[3] = pickBit(ctr[1], field(15, 4), 4); break;
+        case 4:
+            a[4] = pickBit(ctr[1], field(19, 4), 4);
+            a[5] = pickBit(ctr[2], field(23, ntypes), ntypes);
+            break;
+        case 5: {
+            const int off = 23 + ntypes, n = K - off;
+            a[6] = pickBit(ctr[1], field(off, n), n);
+        } break;
+    }
+}
+
 struct Game {
     const KStatic& P;
     const KDyn& D;  // the kernel argument itself (kernarg memory): fields load on demand
@@ -2061,6 +2118,28 @@ struct Game {
         flushDirty(total, slot0, pl0, pl1);
         return true;
     }
+    // the fused random policy's action row of cell c of slot (slot0 + i): masked-uniform sample from
+    // the parked mask bits (bit k = mask slot k) of an own idle unit, else a zero row
+    DEV void policyRow(int slot, int c, int p) const {
+        uint64_t lo;
+        uint32_t hi;
+        cellMaskBits(c, p, lo, hi);
+        int32_t a[7];
+        if (lo & 1ull) {
+            sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)hi << 63),
+                          (uint64_t)(hi >> 1), c, a);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 7; q++) a[q] = 0;
+        }
+        int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
+#pragma unroll
+        for (int q = 0; q < 7; q++) dst[q] = a[q];
+    }
+    DEV void writePolicyAll(int slot0, int nslots, int pl0, int pl1) const {
+        for (int i = 0; i < nslots; i++)
+            for (int c = lane_id(); c < HW; c += 64) policyRow(slot0 + i, c, i ? pl1 : pl0);
+    }
     // rewrite the chunks of the listed dirty cells (rslot[0..n): slot index << 15 | cell)
     DEV void flushDirty(int n, int slot0, int pl0, int pl1) {
         wsync();
@@ -2075,6 +2154,7 @@ struct Game {
                 const int j = ((c * K) >> 4) + t;
                 if (j <= ((c * K + K - 1) >> 4))
                     *(uint4*)(D.masks + (size_t)(slot0 + i) * total + 16 * j) = maskChunk(j, i ? pl1 : pl0);
+                if (t == 0 && D.pol_actions && D.pol_delta) policyRow(slot0 + i, c, i ? pl1 : pl0);
             }
         }
         wsync();
@@ -2260,6 +2340,11 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         PHASE(8);
         if (selfplay) G.writeMasks(slot0, 2, 0, 1);
         else G.writeMasks(slot0, 1, D.mask_player, D.mask_player);
+        if (D.pol_actions && !(D.pol_delta && D.mask_delta && ((G.HW * G.K) & 15) == 0)) {  // no dirty-row pass ran
+            wsync();
+            if (selfplay) G.writePolicyAll(slot0, 2, 0, 1);
+            else G.writePolicyAll(slot0, 1, D.mask_player, D.mask_player);
+        }
         PHASE(9);
     }
     if (MODE != MODE_MASKS) {
@@ -2277,58 +2362,8 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
 }
 
 // ---------------------------------------------------------------- random policy (bench / rollouts)
-DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
-    for (int r = 0; r < 10; r++) {
-        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
-        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
-        c[0] = n0;
-        c[1] = n1;
-        c[2] = n2;
-        c[3] = n3;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-}
-DEV int pickBit(uint32_t r, uint64_t bitsv, int n) {
-    const uint64_t m = n >= 64 ? ~0ull : ((1ull << n) - 1);
-    bitsv &= m;
-    const int cnt = __popcll(bitsv);
-    if (cnt == 0) return -1;
-    int k = (int)(((uint64_t)r * (uint32_t)cnt) >> 32);
-    while (k--) bitsv &= bitsv - 1;
-    return __builtin_ctzll(bitsv);
-}
-// one cell's action from its mask bits (lo/hi: mask slots 1..K-1 -> bit i-1), Philox counter
-// (slot id, step, cell, 0)
 DEV void sampleBits(const PolicyParams& Q, uint64_t lo, uint64_t hi, int slot, int c, int32_t a[7]) {
-    for (int k = 0; k < 7; k++) a[k] = 0;
-    uint32_t ctr[4] = {Q.slot_id_base + (uint32_t)slot, Q.step, (uint32_t)c, 0u};
-    philox(ctr, (uint32_t)Q.seed, (uint32_t)(Q.seed >> 32));
-    auto field = [&](int off, int n) -> uint64_t {  // mask slots [off, off+n) (off >= 1)
-        const int b = off - 1;
-        uint64_t v;
-        if (b >= 64) v = hi >> (b - 64);
-        else v = (lo >> b) | (b ? (hi << (64 - b)) : 0ull);
-        return n >= 64 ? v : (v & ((1ull << n) - 1));
-    };
-    const int t = pickBit(ctr[0], field(1, 6), 6);
-    if (t < 0) return;
-    a[0] = t;
-    switch (t) {
-        case 1: a[1] = pickBit(ctr[1], field(7, 4), 4); break;
-        case 2: a[2] = pickBit(ctr[1], field(11, 4), 4); break;
-        case 3: a[3] = pickBit(ctr[1], field(15, 4), 4); break;
-        case 4:
-            a[4] = pickBit(ctr[1], field(19, 4), 4);
-            a[5] = pickBit(ctr[2], field(23, Q.ntypes), Q.ntypes);
-            break;
-        case 5: {
-            const int off = 23 + Q.ntypes, n = Q.K - off;
-            a[6] = pickBit(ctr[1], field(off, n), n);
-        } break;
-    }
+    sampleBitsRaw(Q.seed, Q.step, Q.slot_id_base + (uint32_t)slot, Q.ntypes, Q.K, lo, hi, c, a);
 }
 DEV void sampleCell(const PolicyParams& Q, const uint8_t* m, int slot, int c, int32_t a[7]) {
     for (int k = 0; k < 7; k++) a[k] = 0;

@@ -377,6 +377,18 @@ class DeviceVecEnv:
         _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self.reward),
                                      self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
 
+    def step_fused(self, seed, next_step, stream=None):
+        """step() on env.actions, then env.actions := random_policy(seed, next_step) from the masks this
+        step wrote (mrts_step_fused_dev: one launch, identical result)."""
+        h = self._h
+        assert self.masks is not None, "the fused policy samples from the masks"
+        if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
+            _lib.check(h.L.mrts_policy_invalidate(h.h))  # written by someone else since
+        _lib.check(h.L.mrts_step_fused_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
+                                           self._p(self.reward), self._p(self.done), self._p(self.masks), self.mask_player,
+                                           seed, next_step, self._s(stream)))
+        self._policy_out, self._policy_version = self.actions, self.actions._version
+
     def step_rows(self, rows, stream=None):
         """gameStep with Java rows: int32 [slots][n_rows][8] on this device (any order, duplicates ok)."""
         h = self._h

@@ -549,3 +549,42 @@ def test_max_units_below_map_units_rejected():
 
     with pytest.raises(RuntimeError):
         DeviceVecEnv(2, 0, 100, ["maps/16x16/basesWorkers16x16.xml"] * 2, max_units=3)
+
+
+@pytest.mark.parametrize("mp,n_sp,n_bot,po,delta", [
+    ("maps/16x16/basesWorkers16x16.xml", 8, 0, False, True),
+    ("maps/8x8/basesWorkers8x8.xml", 8, 0, False, False),
+    ("maps/10x10/basesWorkers10x10.xml", 4, 2, True, True),     # H*W*K % 16 != 0: full mask path
+    ("maps/BWDistantResources32x32.xml", 4, 0, True, True),
+])
+def test_fused_policy_matches_separate_kernels(mp, n_sp, n_bot, po, delta):
+    """mrts_step_fused_dev = mrts_step_dev followed by mrts_policy_dev(next step), bit for bit, including
+    after a reset and a standalone mask write in between."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    S = n_sp + n_bot
+    bots = ["RandomBiasedAI"] * n_bot
+    mk = lambda: DeviceVecEnv(n_sp, n_bot, 400, [mp] * S, ai2s=bots, partial_obs=po, seed=6, mask_delta=delta)  # noqa: E731
+    A, B = mk(), mk()
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+    for k in range(250):
+        A.step()
+        A.random_policy(SEED, k + 1)
+        B.step_fused(SEED, k + 1)
+        A.synchronize()
+        B.synchronize()
+        for name in ("obs", "reward", "done", "masks", "actions"):
+            a, b = getattr(A, name).cpu().numpy(), getattr(B, name).cpu().numpy()
+            assert np.array_equal(a, b), f"{name} differs after step {k}"
+        if k == 90:
+            for e in (A, B):
+                e.reset()
+                e.random_policy(SEED, k + 1)
+        if k == 170:
+            B.get_masks()
+    A.close()
+    B.close()
+    del torch
