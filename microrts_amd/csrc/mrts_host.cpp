@@ -504,6 +504,12 @@ struct mrts_env {
         D.HW = HW;
         D.CAP = CAP;
         D.n_sp_games = nSpGames;
+        D.n_rewards = hstatic.n_rewards;
+        D.max_steps = hstatic.max_steps;
+        D.C = hstatic.C;
+        D.reward_need = hstatic.reward_need;
+        D.reward_kinds4 = 0;
+        for (int j = 0; j < hstatic.n_rewards; j++) D.reward_kinds4 |= (uint32_t)hstatic.reward_kinds[j] << (4 * j);
         return launchEnv(mode, hstatic, d_static, D, s);
     }
     int gameOfSlot(int slot, int* player) const {

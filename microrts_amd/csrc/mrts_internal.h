@@ -114,6 +114,11 @@ struct KDyn {
     uint64_t pol_seed;
     uint32_t pol_step, pol_slot_base;
     int32_t pol_delta;             // 1: pol_actions holds the policy rows of the previous mask write's candidates
+    // copies of the KStatic fields the step reads after its first memory round (kernel arguments sit
+    // in SGPRs from the kernel's start; a KStatic load there is a dependent round trip on the chain)
+    int32_t n_rewards, max_steps, C;
+    uint32_t reward_need;
+    uint32_t reward_kinds4;        // reward_kinds[j] in bits 4j..4j+3
 };
 
 struct PolicyParams {

@@ -109,6 +109,17 @@ DEV int wave_reduce(int v) {
     v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
     return __builtin_amdgcn_readlane(v, 63);
 }
+// Inclusive prefix sum over the wave's lanes with DPP: row_shr 1/2/4/8 scan each 16-lane row
+// (lanes shifted in from outside the row read 0), row_bcast:15 / :31 carry the row totals.
+DEV int wave_incl_sum(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
 DEV int wave_min(int v) { return wave_reduce<true>(v); }
 DEV int wave_sum(int v) { return wave_reduce<false>(v); }
 
@@ -570,7 +581,8 @@ struct Game {
             const uint64_t m = ballot(cand);
             if (m == 0) continue;
             const uint32_t av = pack_ua(t, ut, 0, 0);
-            const uint64_t acc = acceptChain(p, run0, run1, cand, cand ? lanes_below(m) : -1, __popcll(m), t, pr, pos, av, false);
+            int irank = 0;
+            const uint64_t acc = acceptChain(p, run0, run1, cand, cand ? lanes_below(m) : -1, __popcll(m), t, pr, pos, av, false, irank);
             if ((acc >> l) & 1ull) {
                 const int idx = npairs + lanes_below(acc);
                 pairs[(size_t)idx * 2] = (uint32_t)s | ((uint32_t)t << 16) | ((uint32_t)ut << 20);
@@ -638,7 +650,9 @@ struct Game {
     // PlayerAction.fromVectorAction (rts/PlayerAction.java:495-528): decoded rows in ascending cell
     // order; accepted iff ua.ru.consistentWith(running ru) (rts/ResourceUsage.java:31-50).  Only the
     // acceptance chain is serial; accepted units get UA_PA.
-    DEV void decode(int p) {
+    // issueNow (self-play, all units in one wave): the accepted rows are issued straight from the
+    // chain's registers — issueSafe(pa) of the same pairs in the same (cell) order as issuePlayer
+    DEV void decode(int p, bool issueNow = false) {
         int run0, run1;
         // full observability: the base reservations are the issue index (every present MOVE/PRODUCE
         // target + per-player PRODUCE cost sums), kept current across issue batches
@@ -652,7 +666,7 @@ struct Game {
         }
         MPHASE(13);
         if (nu <= 64) {
-            decodeUnits(p, run0, run1, useIx);
+            decodeUnits(p, run0, run1, useIx, issueNow);
             return;
         }
         ixValid = false;  // the chain below adds to `bits`
@@ -668,14 +682,15 @@ struct Game {
             const uint64_t m = ballot(cand);
             if (m == 0) continue;
             const int t = ua_type(a), pr = par[s < CAP ? s : 0];
-            const uint64_t acc = acceptChain(p, run0, run1, cand, cand ? lanes_below(m) : -1, __popcll(m), t, pr, c, a, false);
+            int irank = 0;
+            const uint64_t acc = acceptChain(p, run0, run1, cand, cand ? lanes_below(m) : -1, __popcll(m), t, pr, c, a, false, irank);
             if ((acc >> lane_id()) & 1ull) ua[s] = a | UA_PA;
             wsync();
         }
     }
     // Unit-parallel form (all units in one wave): the candidates' ascending-cell order is a rank
     // computed in registers, so the serial part is the acceptance chain alone.
-    DEV void decodeUnits(int p, int& run0, int& run1, bool keepBits) {
+    DEV void decodeUnits(int p, int& run0, int& run1, bool keepBits, bool issueNow) {
         const int o = lane_id();
         uint32_t a = 0, cu = 0;
         bool cand = false;
@@ -685,15 +700,41 @@ struct Game {
             cand = !(cu & UC_DEAD) && uplay(cu) == p && (a & UA_DEC) && !(a & (UA_PRESENT | UA_BAD));
         }
         const uint64_t m = ballot(cand);
-        if (m == 0) return;
+        if (m == 0) {
+            if (issueNow) {
+                curP = p;
+                issueFills(p, 1);
+            }
+            return;
+        }
         const int c = uy(cu) * W + ux(cu);
         const int pr = o < nu ? par[o] : 0;
         MPHASE(12);
         const int rank = cellRank(m, cand, c);
         MPHASE(14);
-        const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), ua_type(a), pr, c, a, keepBits);
-        if ((acc >> o) & 1ull) ua[o] = a | UA_PA;
+        int irank = 0;
+        const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), ua_type(a), pr, c, a, keepBits, irank);
+        const bool isPA = (acc >> o) & 1ull;
+        if (!issueNow) {
+            if (isPA) ua[o] = a | UA_PA;
+            wsync();
+            return;
+        }
+        MPHASE(2);
+        // issuePlayer(p, 1, false) of the accepted lanes (issuePA's legality + issueBatch, then the fills)
+        curP = p;
+        int t = 0, prm = 0, tx = 0, ty = 0, ut = 0;
+        if (isPA) {
+            t = ua_type(a);
+            prm = pr;
+            tx = ua_tx(a);
+            ty = ua_ty(a);
+            ut = ua_ut(a);
+            legality(o, t, prm, tx, ty, ut);
+        }
         wsync();
+        if (acc) issueBatch(isPA, irank, __popcll(acc), o, t, prm, tx, ty, ut);
+        issueFills(p, 1);
     }
     // rank of each candidate lane among the candidates m by cell c (cells are distinct)
     DEV int cellRank(uint64_t m, bool cand, int c) const {
@@ -703,9 +744,10 @@ struct Game {
     }
     // acceptChain with the reservation bitmap held one word per lane (readlane instead of LDS reads)
     DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB,
-                                bool keepBits) {
+                                bool keepBits, int& irank) {
         uint32_t bv = lane_id() < NB ? bits[lane_id()] : 0u;
         uint64_t acc = 0;
+        int nacc = 0;
         for (int r = 0; r < n; r++) {
             const int k = __builtin_ctzll(ballot(rank == r));
             const bool up = rl(usesPos, k);
@@ -725,6 +767,8 @@ struct Game {
                 if (p == 0) run0 += cst;
                 else run1 += cst;
                 acc |= 1ull << k;
+                if (lane_id() == k) irank = nacc;
+                nacc++;
             }
         }
         if (!keepBits && lane_id() < NB) bits[lane_id()] = bv;
@@ -733,14 +777,16 @@ struct Game {
     // ua.ru.consistentWith(running ru) for the n candidates in rank order (PlayerAction.java:503-520);
     // returns the accepted lanes
     // keepBits: `bits` is left as it was (the chain's additions stay in registers)
+    // irank: each accepted lane's rank among the accepted (the pa's issue order)
     DEV uint64_t acceptChain(int p, int& run0, int& run1, bool cand, int rank, int n, int t, int pr, int c, uint32_t a,
-                             bool keepBits) {
+                             bool keepBits, int& irank) {
         const bool usesPos = cand && (t == T_MOVE || t == T_PRODUCE);
         const int tpos = c + dyo(pr) * W + dxo(pr) + W;  // ResourceUsage position (UnitAction.java:254-291)
         const int cost = (cand && t == T_PRODUCE) ? U.cost[ua_ut(a)] : 0;
         const int NB = (HW + 2 * W + 31) / 32;
-        if (NB <= 64) return acceptChainReg(p, run0, run1, rank, n, usesPos, tpos, cost, NB, keepBits);
+        if (NB <= 64) return acceptChainReg(p, run0, run1, rank, n, usesPos, tpos, cost, NB, keepBits, irank);
         uint64_t acc = 0;
+        int nacc = 0;
         for (int r = 0; r < n; r++) {
             const int k = __builtin_ctzll(ballot(rank == r));
             const bool up = rl(usesPos, k);
@@ -760,6 +806,8 @@ struct Game {
                 if (p == 0) run0 += cst;
                 else run1 += cst;
                 acc |= 1ull << k;
+                if (lane_id() == k) irank = nacc;
+                nacc++;
             }
         }
         return acc;
@@ -923,7 +971,7 @@ struct Game {
                 } else {  // older assignment: only the new one is cancelled (:298-317)
                     // p.m_b = NONE mutates pa's own Pair unless a cancel already replaced p: the
                     // TraceEntry (pa.clone() after issueSafe) then records NONE, not the PRODUCE
-                    if (orig && tIn == T_PRODUCE && (P.reward_need & RN_COUNTS) && lane_id() == 0) {
+                    if (orig && tIn == T_PRODUCE && (D.reward_need & RN_COUNTS) && lane_id() == 0) {
                         const int pc = prodCategory(U.flags[utIn]);
                         if (pc >= 0) rwc[curP * RC_N + pc] -= 1;
                     }
@@ -1002,7 +1050,7 @@ struct Game {
     DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut, bool checkDup = false) {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
-        if (P.reward_need & RN_COUNTS) {  // the pairs as the TraceEntry records them (legality applied)
+        if (D.reward_need & RN_COUNTS) {  // the pairs as the TraceEntry records them (legality applied)
             const int pc = np ? prodCategory(U.flags[ut]) : -1;
             auto cnt = [](bool b) { return (int)__popcll(ballot(b)); };
             const int c[RC_N] = {cnt(act && t == T_HARVEST), cnt(act && t == T_RETURN), cnt(act && t == T_ATTACK),
@@ -1698,22 +1746,22 @@ struct Game {
     // Produce*RewardFunction.java:22-33; Attack: AttackRewardFunction.java:22-38 (a legal attack always
     // targets a minplayer unit of the pre-cycle pgs).  Constants are float 1.
     DEV bool writeRewards(int slot0, int nslots, int pl0, int pl1, bool gameover, int winner) {
-        const int R = P.n_rewards;
+        const int R = D.n_rewards;
         int newSq0 = INF, newSq1 = INF;
-        if (P.reward_need & RN_CLOSER) closerMin(newSq0, newSq1);
+        if (D.reward_need & RN_CLOSER) closerMin(newSq0, newSq1);
         bool resLeft = false;
-        if (P.reward_need & RN_RESOURCES)
+        if (D.reward_need & RN_RESOURCES)
             for (int o0 = 0; o0 < nu; o0 += 64) {
                 const int o = o0 + lane_id();
                 resLeft |= ballot(o < nu && !(uc[o] & UC_DEAD) && (U.flags[utyp(uc[o])] & N_RESOURCE) && res[o] > 0) != 0;
             }
-        const int k0 = P.reward_kinds[0];
+        const int k0 = (int)(D.reward_kinds4 & 15u);
         const bool done0 = k0 == RF_WINLOSS ? gameover : (k0 == RF_RESOURCE_GATHER ? !resLeft : false);
         const int L = lane_id();
         if (L < nslots * R && (D.reward || D.done)) {
             const int i = L / R, j = L - i * R;
             const int p = i ? pl1 : pl0;
-            const int kind = P.reward_kinds[j];
+            const int kind = (int)((D.reward_kinds4 >> (4 * j)) & 15u);
             double r = 0.0;
             bool d = false;
             switch (kind) {
@@ -1760,7 +1808,7 @@ struct Game {
         }
     }
     DEV void writeObsFull(int slot0, int nslots, int player0) {
-        int32_t* o0 = D.obs + (size_t)slot0 * P.C * HW;
+        int32_t* o0 = D.obs + (size_t)slot0 * D.C * HW;
         if ((HW & 3) == 0) {
             for (int c4 = 4 * lane_id(); c4 < HW; c4 += 256) {
                 int v[4][6];
@@ -1770,7 +1818,7 @@ struct Game {
                 for (int pl = 0; pl < 6; pl++)
                     *(int4*)(o0 + (size_t)pl * HW + c4) = make_int4(v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
                 if (nslots == 2) {  // the other player's view differs only in the owner plane
-                    int32_t* o1 = o0 + (size_t)P.C * HW;
+                    int32_t* o1 = o0 + (size_t)D.C * HW;
 #pragma unroll
                     for (int pl = 0; pl < 6; pl++) {
                         int4 w = make_int4(v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
@@ -1786,7 +1834,7 @@ struct Game {
             }
         } else {
             for (int i = 0; i < nslots; i++) {
-                int32_t* o = o0 + (size_t)i * P.C * HW;
+                int32_t* o = o0 + (size_t)i * D.C * HW;
                 for (int c = lane_id(); c < HW; c += 64) {
                     int v[6];
                     obsCell(c, player0 + i, v);
@@ -1810,7 +1858,7 @@ struct Game {
             }
         }
         wsync();
-        int32_t* out = D.obs + (size_t)slot * P.C * HW;
+        int32_t* out = D.obs + (size_t)slot * D.C * HW;
         auto planes = [&](int c, int v[6]) {
             const int s = (int)scell[c] - 1;
             v[0] = v[1] = v[2] = v[3] = v[4] = 0;
@@ -2100,12 +2148,7 @@ struct Game {
         }
         const uint32_t dirty = cur | old;
         const int n = __popc(dirty);
-        int incl = n;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int t = __shfl_up(incl, off);
-            if (l >= off) incl += t;
-        }
+        const int incl = wave_incl_sum(n);
         const int total = rl(incl, 63);
         if (total > 64) return false;
         if (l < NW) {
@@ -2200,9 +2243,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         G.storeTerrain();
         G.resetFromTemplate();
         if (D.mask_delta && D.masks) G.loadPrev();
-        for (int k = lane_id(); k < nslots * P.n_rewards; k += 64) {
-            if (D.reward) D.reward[(size_t)slot0 * P.n_rewards + k] = 0.0;
-            if (D.done) D.done[(size_t)slot0 * P.n_rewards + k] = 0;
+        for (int k = lane_id(); k < nslots * D.n_rewards; k += 64) {
+            if (D.reward) D.reward[(size_t)slot0 * D.n_rewards + k] = 0.0;
+            if (D.done) D.done[(size_t)slot0 * D.n_rewards + k] = 0;
         }
     } else {
         G.load(D.mask_delta && D.masks);
@@ -2247,9 +2290,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
-        if (P.reward_need & RN_COUNTS)
+        if (D.reward_need & RN_COUNTS)
             if (lane_id() < 2 * RC_N) G.rwc[lane_id()] = 0;
-        if (P.reward_need & RN_CLOSER) G.closerBefore();
+        if (D.reward_need & RN_CLOSER) G.closerBefore();
         const bool rowsMode = FIX ? false : D.rows != nullptr;
         if (rowsMode && gtype == GT_SELFPLAY) {
             for (int p = 0; p < 2; p++) {
@@ -2272,9 +2315,13 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
             PHASE(1);
             for (int p = 0; p < 2; p++) {
                 if (G.po) G.snapshot(p);
-                G.decode(p);
-                PHASE(2);
-                G.issuePlayer(p, 1, false);
+                if (G.nu <= 64) {
+                    G.decode(p, true);
+                } else {
+                    G.decode(p);
+                    PHASE(2);
+                    G.issuePlayer(p, 1, false);
+                }
                 PHASE(3);
             }
         } else if (gtype == GT_AGENT_VS_BOT) {
@@ -2307,8 +2354,8 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         const int steps = G.hget(H_STEPS) + 1;
         G.hset(H_STEPS, steps);
         const bool done0 = G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner);
-        const bool reset = done0 || steps >= P.max_steps;
-        if (reset && D.done && lane_id() < nslots) D.done[(size_t)(slot0 + lane_id()) * P.n_rewards] = 1;
+        const bool reset = done0 || steps >= D.max_steps;
+        if (reset && D.done && lane_id() < nslots) D.done[(size_t)(slot0 + lane_id()) * D.n_rewards] = 1;
         if (reset) {
             G.resetFromTemplate();
             if (G.po) G.clearSnap();
@@ -2513,12 +2560,7 @@ __global__ __launch_bounds__(64) void k_policy_delta(PolicyParams Q) {
     if (valid) Q.prev_out[item] = cur;
     const uint32_t dirty = cur | old;
     const int n = __popc(dirty);
-    int incl = n;  // inclusive prefix sum over lanes
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int t = __shfl_up(incl, off);
-        if (lane >= off) incl += t;
-    }
+    const int incl = wave_incl_sum(n);  // inclusive prefix sum over lanes
     const int total = __builtin_amdgcn_readlane(incl, 63);
     if (total == 0) return;
     const uint32_t slot = item / MW, w = item - slot * MW;

@@ -37,18 +37,29 @@ for delta in (True, False):
     env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=1, mask_delta=delta, source_bits=delta,
                        partial_obs=PO)
     env.reset()
-    for k in range(int(os.environ.get("BURNIN", 1000))):
-        env.random_policy(SEED, k)
-        env.step()
+    FUSED = os.environ.get("FUSED", "1") == "1" and delta
+    burn = int(os.environ.get("BURNIN", 1000))
+    if FUSED:
+        env.random_policy(SEED, 0)
+    for k in range(burn):
+        if FUSED:
+            env.step_fused(SEED, k + 1)
+        else:
+            env.random_policy(SEED, k)
+            env.step()
     env.synchronize()
     read(1)
     n = 100
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ms = 0.0
     for k in range(n):
-        env.random_policy(SEED, 5000 + k)
+        if not FUSED:
+            env.random_policy(SEED, 5000 + k)
         s.record()
-        env.step()
+        if FUSED:
+            env.step_fused(SEED, burn + 1 + k)
+        else:
+            env.step()
         e.record()
         e.synchronize()
         ms += s.elapsed_time(e)
@@ -64,7 +75,7 @@ for delta in (True, False):
              "game_us_max": float((en - st).max()) / 100.0,
              "start_us_percentiles": [float(np.percentile(st - t0, q)) / 100.0 for q in (10, 50, 90, 99)]}
     per = {NAMES[i]: round(ph[i] / (n * E)) for i in range(len(NAMES))}
-    print(json.dumps({"mask_delta": delta, "k_env_us": 1e3 * ms / n, "last_launch": spans, "mean_cycles_per_game_step": per,
+    print(json.dumps({"mask_delta": delta, "fused_policy": FUSED, "k_env_us": 1e3 * ms / n, "last_launch": spans, "mean_cycles_per_game_step": per,
                       "total_cycles": sum(per.values()),
                       "max_game_cycles_over_100_steps": {NAMES[i]: ph[16 + i] for i in range(len(NAMES))}}), flush=True)
     env.close()
