@@ -34,7 +34,8 @@ enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2, MODE_PLAYOUT = 3 };
 #ifdef MRTS_PHASE_TIMING
 constexpr int PH_GAMES = 1 << 16;
 __device__ unsigned long long g_phase[16 * PH_GAMES];  // [phase][game], no contention
-__device__ unsigned long long g_span[2 * PH_GAMES];    // last launch: [game] start / end, s_memrealtime (100 MHz)
+__device__ unsigned long long g_span[3 * PH_GAMES];    // last launch: [game] start / end, s_memrealtime (100 MHz),
+                                                       // placement: HW_ID | XCC_ID << 32 | nu at start << 40 | nu at end << 48
 #define PHASE_IN(acc, tt, i)                          \
     do {                                              \
         const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
@@ -248,6 +249,7 @@ struct Game {
 #endif
     bool ixValid;
     bool anyMP;
+    uint32_t lcu, lua;     // load(): lane l's unit core / assignment words (units 0..63) as loaded
     uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
     int curP;              // player whose pa is being issued
     // CloserToEnemyBase/Unit: each player's first Base before the step (x | y << 8, -1 = none) and
@@ -385,6 +387,8 @@ struct Game {
         const uint32_t tw = l < TW ? (uint32_t)terr[l] : 0u;
         const uint32_t pv = (wantPrev && l < PW) ? (uint32_t)arr[N_ARRAYS * CAP + l] : 0u;
         loadHeader(hv);
+        lcu = (uint32_t)r[A_UC];
+        lua = (uint32_t)r[A_UA];
         {
             int32_t* ul = (int32_t*)&U;
             ul[l] = u0;
@@ -473,6 +477,79 @@ struct Game {
     // UnitAction.fromVectorAction (rts/UnitAction.java:675-709) for every idle unit of the external
     // player(s), lane-parallel, in ONE round of global loads: a pure function of (row, unit).  The
     // decoded action is parked in the unit's empty assignment fields with UA_DEC.
+    // JNIGridnetClientSelfPlay.gameStep's two issueSafe passes (tests/JNIGridnetClientSelfPlay.java:
+    // 159-189) for a game whose units fit one wave, under full observability: predecode, then per
+    // player the acceptance chain (PlayerAction.fromVectorAction), issueSafe of the accepted rows in
+    // cell order and fillWithNones(gs, p, 1) in list order — the same sequence as predecode + decode +
+    // issuePlayer, with each lane's own unit fields (load()'s registers) instead of LDS re-reads.
+    // Between steps no unit is dead; decoded rows are never parked in LDS (every idle unit's
+    // assignment is written by its issue or its fill).
+    DEV void selfPlayFast(const int32_t* rows0, const int32_t* rows1) {
+        const int l = lane_id();
+        const uint32_t cu = lcu;
+        const int pl = l < nu ? uplay(cu) : -1;
+        const bool idle = pl >= 0 && !(lua & UA_PRESENT);
+        int32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
+        if (idle) {
+            const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)(uy(cu) * W + ux(cu)) * 7;
+#pragma unroll
+            for (int k = 0; k < 7; k++) a[k] = r[k];
+        }
+        const bool useIx = (HW + 2 * W + 31) / 32 <= 64;
+        if (useIx) buildIndex();  // while the rows are in flight
+        int t = 0, pr = -1, ut = 0, tx = 0, ty = 0;
+        bool bad = false;
+        if (idle) bad = decodeFields(cu, a, t, pr, ut, tx, ty);
+        if (ballot(bad)) addErr(E_PRODUCE_TYPE);
+        const uint32_t adec = pack_ua(t, ut, tx, ty);
+        const int c = uy(cu) * W + ux(cu);
+        MPHASE(1);
+        for (int p = 0; p < 2; p++) {
+            int run0, run1;
+            if (useIx) {
+                if (!ixValid) buildIndex();
+                run0 = sumProd0;
+                run1 = sumProd1;
+            } else {
+                baseReservations(p, run0, run1);
+            }
+            curP = p;
+            const bool mine = idle && pl == p;
+            const bool cand = mine && !bad;
+            const uint64_t m = ballot(cand);
+            bool isPA = false;
+            if (m) {
+                const int rank = cellRank(m, cand, c);
+                int irank = 0;
+                const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), t, pr, c, adec, useIx, irank);
+                MPHASE(2);
+                isPA = (acc >> l) & 1ull;
+                int tt = 0, prm = 0, ttx = 0, tty = 0, tut = 0;
+                if (isPA) {
+                    tt = t;
+                    prm = pr;
+                    ttx = tx;
+                    tty = ty;
+                    tut = ut;
+                    legality(l, cu, tt, prm, ttx, tty, tut);
+                }
+                wsync();
+                if (acc) issueBatch(isPA, irank, __popcll(acc), l, tt, prm, ttx, tty, tut, false, &cu);
+            }
+            // fillWithNones(gs, p, 1): p's idle units left without an action, list order
+            const bool fill = mine && !isPA;
+            const uint64_t mf = ballot(fill);
+            if (fill) {
+                ua[l] = pack_ua(T_NONE, 0, 0, 0) | UA_PRESENT;
+                par[l] = 1;
+                at[l] = time;
+                as[l] = seq + lanes_below(mf);
+            }
+            seq += __popcll(mf);
+            wsync();
+            MPHASE(3);
+        }
+    }
     DEV void predecode(const int32_t* rows0, const int32_t* rows1, int only) {
         bool bad_any = false;
         const int l = lane_id();
@@ -817,8 +894,8 @@ struct Game {
     // Unit.canExecuteAction (rts/units/Unit.java:531-534) = membership in getUnitActions
     // (:382-522) under UnitAction.equals (rts/UnitAction.java:191-208); an illegal action becomes
     // NONE(ETA(original)) (rts/GameState.java:347-354).  Lane-local.
-    DEV void legality(int s, int& t, int& prm, int& tx, int& ty, int& ut) const {
-        const uint32_t cu = uc[s];
+    DEV void legality(int s, int& t, int& prm, int& tx, int& ty, int& ut) const { legality(s, uc[s], t, prm, tx, ty, ut); }
+    DEV void legality(int s, uint32_t cu, int& t, int& prm, int& tx, int& ty, int& ut) const {
         const int x = ux(cu), y = uy(cu), typ = utyp(cu), pl = uplay(cu);
         const uint32_t fl = U.flags[typ];
         bool legal = false;
@@ -1047,7 +1124,9 @@ struct Game {
     // seq + rank); otherwise the batch runs one pair at a time through issueOne.
     // checkDup (Java rows): a unit named by an earlier pair of this pa (same batch, or already issued)
     // forces the one-at-a-time path
-    DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut, bool checkDup = false) {
+    // cuKnown: the lane's unit core word uc[s] (already in a register), or null
+    DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut, bool checkDup = false,
+                        const uint32_t* cuKnown = nullptr) {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
         if (D.reward_need & RN_COUNTS) {  // the pairs as the TraceEntry records them (legality applied)
@@ -1072,7 +1151,7 @@ struct Game {
         if (mpm) {
             if (!ixValid) buildIndex();
             if (mp) {
-                const uint32_t cu = uc[s];
+                const uint32_t cu = cuKnown ? *cuKnown : uc[s];
                 pl = uplay(cu);
                 ntgt = (uy(cu) + dyo(prm)) * W + ux(cu) + dxo(prm);
                 ncost = np ? U.cost[ut] : 0;
@@ -2250,6 +2329,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     } else {
         G.load(D.mask_delta && D.masks);
     }
+#ifdef MRTS_PHASE_TIMING
+    const int nu0_ = G.nu;
+#endif
     const int kind = FIX ? GT_SELFPLAY : G.hget(H_KIND);
     const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
     if (G.po) G.clearSnap();
@@ -2311,6 +2393,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
             G.issuePlayer(1 - side, 10, true);
         } else if (gtype == GT_SELFPLAY) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
+            if (!G.po && G.nu <= 64) {
+                G.selfPlayFast(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride);
+            } else {
             G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1);
             PHASE(1);
             for (int p = 0; p < 2; p++) {
@@ -2323,6 +2408,7 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
                     G.issuePlayer(p, 1, false);
                 }
                 PHASE(3);
+            }
             }
         } else if (gtype == GT_AGENT_VS_BOT) {
             // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203): both views are taken and
@@ -2404,6 +2490,9 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         for (int i = 0; i < 16; i++) g_phase[i * PH_GAMES + G.g] += G.phAcc[i];
         g_span[G.g] = rt0_;
         g_span[PH_GAMES + G.g] = __builtin_amdgcn_s_memrealtime();
+        g_span[2 * PH_GAMES + G.g] = (unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+                                     ((unsigned long long)(__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 15) << 32) |
+                                     ((unsigned long long)(nu0_ & 255) << 40) | ((unsigned long long)(G.nu & 255) << 48);
     }
 #endif
 }
@@ -2617,13 +2706,14 @@ hipError_t phaseTimes(unsigned long long* out, int reset) {
     }
     return e;
 }
-hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts then [n] ends of the last launch
-    std::vector<unsigned long long> h((size_t)2 * PH_GAMES);
+hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts, [n] ends, [n] placements of the last launch
+    std::vector<unsigned long long> h((size_t)3 * PH_GAMES);
     hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_span), h.size() * sizeof(h[0]));
     if (e != hipSuccess) return e;
     for (int i = 0; i < n && i < PH_GAMES; i++) {
         out[i] = h[i];
         out[n + i] = h[PH_GAMES + i];
+        out[2 * n + i] = h[2 * PH_GAMES + i];
     }
     return e;
 }

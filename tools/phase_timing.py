@@ -27,6 +27,45 @@ PO = os.environ.get("PO", "0") == "1"
 SEED = 0x5EEDC0DE
 
 
+def tail_report(st, en, place):
+    """Where the last launch's slow games were: duration vs unit count, and per-SIMD / per-CU load
+    (HW_ID: wave 3:0, simd 5:4, cu 11:8, sh 12, se 15:13; XCC_ID)."""
+    import numpy as np
+    hw = (place & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    xcc = ((place >> np.uint64(32)) & np.uint64(15)).astype(np.int64)
+    nu0 = ((place >> np.uint64(40)) & np.uint64(255)).astype(np.int64)
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 15
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 7
+    dur = (en - st) / 100.0
+    t0 = st.min()
+    end = (en - t0) / 100.0
+    start = (st - t0) / 100.0
+    cu_key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    simd_key = cu_key * 4 + simd
+    out = {"n_cus_used": int(len(np.unique(cu_key))), "n_simds_used": int(len(np.unique(simd_key))),
+           "games_per_simd": np.bincount(np.bincount(simd_key)).tolist(),
+           "games_per_cu": np.bincount(np.bincount(cu_key)).tolist()}
+    for lo, hi in ((0, 16), (16, 24), (24, 32), (32, 40), (40, 48), (48, 64), (64, 256)):
+        sel = (nu0 >= lo) & (nu0 < hi)
+        if sel.any():
+            out[f"nu[{lo},{hi})"] = {"games": int(sel.sum()), "dur_mean": round(float(dur[sel].mean()), 2),
+                                     "dur_max": round(float(dur[sel].max()), 2)}
+    slow = np.argsort(-end)[:16]
+    out["slowest_end"] = [{"g": int(i), "end": round(float(end[i]), 2), "start": round(float(start[i]), 2),
+                           "dur": round(float(dur[i]), 2), "nu": int(nu0[i]),
+                           "simd_mates_dur": sorted([round(float(dur[j]), 1) for j in np.nonzero(simd_key == simd_key[i])[0]])}
+                          for i in slow]
+    simd_sum = np.bincount(simd_key, weights=dur)
+    out["simd_busy_sum_us"] = {"mean": round(float(simd_sum[simd_sum > 0].mean()), 2), "max": round(float(simd_sum.max()), 2)}
+    corr = np.corrcoef(nu0, dur)[0, 1]
+    out["corr_nu_dur"] = round(float(corr), 3)
+    # duration vs start order
+    out["corr_start_dur"] = round(float(np.corrcoef(start, dur)[0, 1]), 3)
+    print(json.dumps({"tail": out}), flush=True)
+
+
 def read(reset):
     buf = (ctypes.c_ulonglong * 32)()
     _lib.check(L.mrts_phase_times(buf, reset))
@@ -64,11 +103,14 @@ for delta in (True, False):
         e.synchronize()
         ms += s.elapsed_time(e)
     ph = read(1)
-    sp = (ctypes.c_ulonglong * (2 * E))()
+    sp = (ctypes.c_ulonglong * (3 * E))()
     _lib.check(L.mrts_phase_spans(sp, E))
     import numpy as np
     st = np.array(sp[:E], dtype=np.float64)
-    en = np.array(sp[E:], dtype=np.float64)
+    en = np.array(sp[E:2 * E], dtype=np.float64)
+    place = np.array(sp[2 * E:3 * E], dtype=np.uint64)
+    if os.environ.get("TAIL", "0") == "1" and delta:
+        tail_report(st, en, place)
     t0 = st.min()
     spans = {"dispatch_spread_us": (st.max() - t0) / 100.0, "kernel_span_us": (en.max() - t0) / 100.0,
              "game_us_mean": float((en - st).mean()) / 100.0, "game_us_p99": float(np.percentile(en - st, 99)) / 100.0,
