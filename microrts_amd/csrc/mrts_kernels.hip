@@ -2240,6 +2240,125 @@ struct Game {
         flushDirty(total, slot0, pl0, pl1);
         return true;
     }
+    // One cell's K-byte mask record (byte k = bit k of lo:hi) at dst, byte-exact: up to 3 head bytes to
+    // reach dword alignment, whole dwords (dwordx4 / dwordx3 stores, 4-byte aligned), then the tail
+    // bytes — neighbouring records written by other lanes are never touched.
+    DEV void storeRecord(uint8_t* dst, uint64_t lo, uint32_t hi) const {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+        typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
+        const int head = (int)((4u - ((uint32_t)(uintptr_t)dst & 3u)) & 3u);
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+            if (i < head) dst[i] = (uint8_t)((lo >> i) & 1u);
+        // bits head.. as a 96-bit value v0:v1:v2
+        const uint64_t sl = (lo >> head) | (head ? ((uint64_t)hi << (64 - head)) : 0ull);
+        const uint32_t sh = hi >> head;
+        const uint32_t v[3] = {(uint32_t)sl, (uint32_t)(sl >> 32), sh};
+        const int nd = (K - head) >> 2;  // whole dwords
+        uint32_t* dw = (uint32_t*)(dst + head);
+        auto nib = [&](int k) -> uint32_t { return expand4(v[k >> 3] >> (4 * (k & 7))); };
+        if (K == 79) {  // nd == 19 for every head
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                u32x4 w = {nib(4 * q), nib(4 * q + 1), nib(4 * q + 2), nib(4 * q + 3)};
+                *(u32x4*)(dw + 4 * q) = w;
+            }
+            u32x3 w3 = {nib(16), nib(17), nib(18)};
+            *(u32x3*)(dw + 16) = w3;
+        } else {
+            for (int k = 0; k < nd; k++) dw[k] = nib(k);
+        }
+        const int t0 = head + 4 * nd;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int b = t0 + i;
+            if (b < K) dst[b] = (uint8_t)((b < 64 ? (lo >> b) : (uint64_t)(hi >> (b - 64))) & 1u);
+        }
+    }
+    // Delta mask writes with every unit in one wave (nu <= 64, K <= 96): each own idle unit's lane
+    // computes its Unit.getUnitActions mask bits in registers and stores its whole record (and, fused
+    // policy, its action row) itself; cells that held an idle unit at the previous write and hold none
+    // now get a zero record (and a zero row).  Same buffer contents as stashMasks + writeMasks.
+    DEV void writeMasksLanes(int slot0, int nslots, int pl0, int pl1) {
+        const int MW = maskWords(HW), NW = nslots * MW;
+        const int l = lane_id();
+        const int total = HW * K;
+        uint32_t* nb = (uint32_t*)rseq;  // cycle() scratch, free here: [slot i][MW] new bits
+        if (l < NW) nb[l] = 0;
+        int si = -1;  // slot index of this lane's unit record, -1 = none
+        uint32_t cu = 0;
+        if (l < nu) {
+            cu = uc[l];
+            if (!(cu & UC_DEAD) && !(ua[l] & UA_PRESENT)) {
+                const int op = uplay(cu);
+                if (op >= 0 && op == pl0) si = 0;
+                else if (nslots > 1 && op >= 0 && op == pl1) si = 1;
+            }
+        }
+        const int c = uy(cu) * W + ux(cu);
+        wsync();
+        if (si >= 0) atomicOr(&nb[si * MW + (c >> 5)], 1u << (c & 31));
+        uint32_t w0 = 0, w1 = 0, w2 = 0;
+        if (si >= 0) unitMask(l, w0, w1, w2);
+        wsync();
+        uint32_t cur = 0, old = 0;
+        int i = 0, w = 0;
+        if (l < NW) {
+            i = l >= MW;
+            w = l - i * MW;
+            cur = nb[l];
+            old = mprev[(i ? pl1 : pl0) * MW + w];
+            if (D.source) D.source[(size_t)(slot0 + i) * MW + w] = cur;
+            prevG()[(i ? pl1 : pl0) * MW + w] = cur;
+        }
+        const bool pol = D.pol_actions && D.pol_delta;
+        // the kernel's full policy pass (writePolicyAll, no delta base) reads the parked bits
+        if (si >= 0 && D.pol_actions && !(D.pol_delta && D.mask_delta && (total & 15) == 0)) {
+            at[l] = (int32_t)w0;
+            as[l] = (int32_t)w1;
+            ua[l] = w2 & 0xFFFFu;
+        }
+        if (si >= 0) {
+            const int slot = slot0 + si;
+            const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
+            storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, lo, w2);
+            if (pol) {
+                int32_t a[7];
+                sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
+                              (uint64_t)(w2 >> 1), c, a);
+                int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
+#pragma unroll
+                for (int q = 0; q < 7; q++) dst[q] = a[q];
+            }
+        }
+        // cells whose idle unit is gone: zero record + zero row
+        const uint32_t gone = old & ~cur;
+        const int n = __popc(gone);
+        const int incl = wave_incl_sum(n);
+        const int ngone = rl(incl, 63);
+        if (ngone == 0) {
+            wsync();
+            return;
+        }
+        for (int b0 = 0; b0 < ngone; b0 += 64) {  // rslot holds 64 list entries at a time
+            wsync();
+            int k = incl - n;
+            for (uint32_t d = gone; d; d &= d - 1, k++)
+                if (k >= b0 && k < b0 + 64) rslot[k - b0] = (uint16_t)((i << 15) | (32 * w + __builtin_ctz(d)));
+            wsync();
+            if (b0 + l < ngone) {
+                const uint32_t e = rslot[l];
+                const int slot = slot0 + (int)(e >> 15), cz = (int)(e & 0x7FFFu);
+                storeRecord(D.masks + (size_t)slot * total + (size_t)cz * K, 0ull, 0u);
+                if (pol) {
+                    int32_t* dst = D.pol_actions + ((size_t)slot * HW + cz) * 7;
+#pragma unroll
+                    for (int q = 0; q < 7; q++) dst[q] = 0;
+                }
+            }
+        }
+        wsync();
+    }
     // the fused random policy's action row of cell c of slot (slot0 + i): masked-uniform sample from
     // the parked mask bits (bit k = mask slot k) of an own idle unit, else a zero row
     DEV void policyRow(int slot, int c, int p) const {
@@ -2467,12 +2586,19 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
     PHASE(7);
     if (D.masks && external) {
+        const int nsl = selfplay ? 2 : 1;
+        if (D.mask_delta && G.nu <= 64 && nsl * maskWords(G.HW) <= 64 && G.K <= 96) {
+            PHASE(8);
+            if (selfplay) G.writeMasksLanes(slot0, 2, 0, 1);
+            else G.writeMasksLanes(slot0, 1, D.mask_player, D.mask_player);
+        } else {
         wsync();
         G.stashMasks(selfplay ? 3 : (1 << D.mask_player));
         wsync();
         PHASE(8);
         if (selfplay) G.writeMasks(slot0, 2, 0, 1);
         else G.writeMasks(slot0, 1, D.mask_player, D.mask_player);
+        }
         if (D.pol_actions && !(D.pol_delta && D.mask_delta && ((G.HW * G.K) & 15) == 0)) {  // no dirty-row pass ran
             wsync();
             if (selfplay) G.writePolicyAll(slot0, 2, 0, 1);
