@@ -4,7 +4,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmrts.so")
+LIB_PATH = os.environ.get("MRTS_LIB_PATH") or os.path.join(HERE, "libmrts.so")  # override: diagnostics builds only
 
 MRTS_BOT_PASSIVE, MRTS_BOT_RANDOM_BIASED = 0, 1
 MRTS_MAX_HORIZON = 65536

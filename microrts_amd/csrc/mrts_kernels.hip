@@ -33,7 +33,8 @@ enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2, MODE_PLAYOUT = 3 };
 // summed over games; not compiled into libmrts.so.
 #ifdef MRTS_PHASE_TIMING
 constexpr int PH_GAMES = 1 << 16;
-__device__ unsigned long long g_phase[16 * PH_GAMES];  // [phase][game], no contention
+constexpr int NPH = 32;  // phase slots
+__device__ unsigned long long g_phase[NPH * PH_GAMES];  // [phase][game], no contention
 __device__ unsigned long long g_span[3 * PH_GAMES];    // last launch: [game] start / end, s_memrealtime (100 MHz),
                                                        // placement: HW_ID | XCC_ID << 32 | nu at start << 40 | nu at end << 48
 #define PHASE_IN(acc, tt, i)                          \
@@ -94,7 +95,13 @@ DEV uint64_t ballot(bool p) { return __ballot(p); }
 DEV int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
-DEV void wsync() { __syncthreads(); }  // one wave per workgroup: s_barrier is nearly free
+// A game is one wave and its LDS is private to that wave: LDS operations of one wave execute in
+// order, so a wave-scope fence (a compiler barrier, no instruction) orders them across lanes.
+DEV void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // Whole-wave reductions with DPP (GFX9 row_bcast forms): quad swaps, half-row and row mirrors
 // reduce each 16-lane row; row_bcast:15/31 chain the rows; lane 63 holds the result.
@@ -245,7 +252,7 @@ struct Game {
     // the sum of present PRODUCE costs
 #ifdef MRTS_PHASE_TIMING
     uint64_t tph_;
-    uint64_t phAcc[16];  // per-phase cycles (registers: constant indices), flushed at kernel end
+    uint64_t phAcc[NPH];  // per-phase cycles (registers: constant indices), flushed at kernel end
 #endif
     bool ixValid;
     bool anyMP;
@@ -387,6 +394,7 @@ struct Game {
         const uint32_t tw = l < TW ? (uint32_t)terr[l] : 0u;
         const uint32_t pv = (wantPrev && l < PW) ? (uint32_t)arr[N_ARRAYS * CAP + l] : 0u;
         loadHeader(hv);
+        MPHASE(20);
         lcu = (uint32_t)r[A_UC];
         lua = (uint32_t)r[A_UA];
         {
@@ -420,6 +428,7 @@ struct Game {
             for (int i = l + 64; i < PW; i += 64) mprev[i] = prevG()[i];
         }
         wsync();
+        MPHASE(21);
         placeUnits();
     }
     DEV void store() {
@@ -497,6 +506,7 @@ struct Game {
         }
         const bool useIx = (HW + 2 * W + 31) / 32 <= 64;
         if (useIx) buildIndex();  // while the rows are in flight
+        MPHASE(22);
         int t = 0, pr = -1, ut = 0, tx = 0, ty = 0;
         bool bad = false;
         if (idle) bad = decodeFields(cu, a, t, pr, ut, tx, ty);
@@ -520,6 +530,7 @@ struct Game {
             bool isPA = false;
             if (m) {
                 const int rank = cellRank(m, cand, c);
+                MPHASE(23);
                 int irank = 0;
                 const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), t, pr, c, adec, useIx, irank);
                 MPHASE(2);
@@ -534,6 +545,7 @@ struct Game {
                     legality(l, cu, tt, prm, ttx, tty, tut);
                 }
                 wsync();
+                MPHASE(24);
                 if (acc) issueBatch(isPA, irank, __popcll(acc), l, tt, prm, ttx, tty, tut, false, &cu);
             }
             // fillWithNones(gs, p, 1): p's idle units left without an action, list order
@@ -819,37 +831,46 @@ struct Game {
         for (uint64_t mm = m; mm; mm &= mm - 1) rank += rl(c, __builtin_ctzll(mm)) < c;
         return cand ? rank : -1;
     }
-    // acceptChain with the reservation bitmap held one word per lane (readlane instead of LDS reads)
+    // acceptChain with the reservation bitmap held one word per lane (readlane instead of LDS reads).
+    // The candidates' (usesPos, cost, position) keys are first permuted into rank order (lane r holds
+    // rank r's key, via rseq), so each chain step is one readlane and a few scalar tests.  The other
+    // player's running sum cannot change during p's chain: if it blocks (ResourceUsage.java:38-46),
+    // every candidate is rejected.
     DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB,
                                 bool keepBits, int& irank) {
-        uint32_t bv = lane_id() < NB ? bits[lane_id()] : 0u;
-        uint64_t acc = 0;
-        int nacc = 0;
-        for (int r = 0; r < n; r++) {
-            const int k = __builtin_ctzll(ballot(rank == r));
-            const bool up = rl(usesPos, k);
-            const int bi = rl(tpos, k), cst = rl(cost, k);
-            bool ok = true;
-            if (up) ok = !(((uint32_t)rl((int)bv, bi >> 5) >> (bi & 31)) & 1u);
-            if (run0 != 0) {
-                const int sum = (p == 0 ? cst : 0) + run0;
-                if (sum > 0 && sum > pres0) ok = false;
-            }
-            if (run1 != 0) {
-                const int sum = (p == 1 ? cst : 0) + run1;
-                if (sum > 0 && sum > pres1) ok = false;
-            }
-            if (ok) {
-                if (up && lane_id() == (bi >> 5)) bv |= 1u << (bi & 31);
-                if (p == 0) run0 += cst;
-                else run1 += cst;
-                acc |= 1ull << k;
-                if (lane_id() == k) irank = nacc;
-                nacc++;
+        const int l = lane_id();
+        uint32_t bv = l < NB ? bits[l] : 0u;
+        if (rank >= 0) rseq[rank] = (int)(((uint32_t)usesPos << 31) | ((uint32_t)cost << 16) | ((uint32_t)tpos & 0xFFFFu));
+        wsync();
+        const int keyR = l < n ? rseq[l] : 0;
+        const int runQ = p == 0 ? run1 : run0, presQ = p == 0 ? pres1 : pres0, presP = p == 0 ? pres0 : pres1;
+        int runP = p == 0 ? run0 : run1;
+        uint64_t accR = 0;  // accepted, bit r = rank r
+        if (!(runQ != 0 && runQ > 0 && runQ > presQ)) {
+            for (int r = 0; r < n; r++) {
+                const uint32_t key = uniu((uint32_t)rl(keyR, r));
+                const int bi = (int)(key & 0xFFFFu), cst = (int)((key >> 16) & 0x7FFFu);
+                const bool up = key >> 31;
+                bool ok = true;
+                if (up) ok = !(((uint32_t)rl((int)bv, bi >> 5) >> (bi & 31)) & 1u);
+                if (runP != 0) {
+                    const int sum = cst + runP;
+                    if (sum > 0 && sum > presP) ok = false;
+                }
+                if (ok) {
+                    if (up && l == (bi >> 5)) bv |= 1u << (bi & 31);
+                    runP += cst;
+                    accR |= 1ull << r;
+                }
             }
         }
-        if (!keepBits && lane_id() < NB) bits[lane_id()] = bv;
-        return acc;
+        if (p == 0) run0 = runP;
+        else run1 = runP;
+        wsync();  // rseq is read again by the next chain
+        if (!keepBits && l < NB) bits[l] = bv;
+        const bool isAcc = rank >= 0 && ((accR >> rank) & 1ull);
+        if (isAcc) irank = __popcll(accR & ((1ull << rank) - 1ull));
+        return ballot(isAcc);
     }
     // ua.ru.consistentWith(running ru) for the n candidates in rank order (PlayerAction.java:503-520);
     // returns the accepted lanes
@@ -2007,7 +2028,8 @@ struct Game {
     // ------------------------------------------------------------------ legal-action masks
     // JNIGridnetClient.getMasks (tests/JNIGridnetClient.java:210-223) + UnitAction.getValidActionArray
     // (rts/UnitAction.java:711-751) over Unit.getUnitActions(gs, 10) (rts/units/Unit.java:382-522).
-    DEV void unitMask(int s, uint32_t& w0, uint32_t& w1, uint32_t& w2) const {
+    // farFromLanes: the range > 1 attack bits are left to farAttackBits (the caller's whole wave)
+    DEV void unitMask(int s, uint32_t& w0, uint32_t& w1, uint32_t& w2, bool farFromLanes = false) const {
         uint64_t lo = 0;
         uint32_t hi = 0;
         auto setb = [&](int k) {
@@ -2064,7 +2086,7 @@ struct Game {
                 }
             }
         }
-        if ((fl & F_ATTACK) && r > 1) {
+        if (!farFromLanes && (fl & F_ATTACK) && r > 1) {
             for (int dy = -r; dy <= r; dy++)
                 for (int dx = -r; dx <= r; dx++) {
                     if (dx * dx + dy * dy > r * r || !inb(x + dx, y + dy)) continue;
@@ -2081,6 +2103,153 @@ struct Game {
         w0 = (uint32_t)lo;
         w1 = (uint32_t)(lo >> 32);
         w2 = hi;
+    }
+    // Wave-uniform per-type bit sets for maskBitsFast (bit t = unit type t has the property), the
+    // produce lists as 8-bit type sets (type t's set in bits 8t..8t+7; mask bits ignore list order)
+    // and, per player, the types whose cost the player's current resources cover.
+    struct MaskTables {
+        uint32_t attack1, attackFar, harvest, move, resource, stockpile, aff0, aff1;
+        uint64_t prod;
+    };
+    DEV MaskTables maskTables() const {
+        const int t = lane_id();
+        const bool ok = t < NT;
+        const uint32_t fl = ok ? U.flags[t] : 0u;
+        const int r = ok ? U.range[t] : 0, cost = ok ? U.cost[t] : 0, np = ok ? U.nprod[t] : 0;
+        uint32_t pm = 0;
+#pragma unroll
+        for (int i = 0; i < MAX_PRODUCES; i++)
+            if (i < np) pm |= 1u << U.prod[t][i];
+        MaskTables T;
+        T.attack1 = (uint32_t)ballot(ok && (fl & F_ATTACK) && r == 1);
+        T.attackFar = (uint32_t)ballot(ok && (fl & F_ATTACK) && r > 1);
+        T.harvest = (uint32_t)ballot(ok && (fl & F_HARVEST));
+        T.move = (uint32_t)ballot(ok && (fl & F_MOVE));
+        T.resource = (uint32_t)ballot(ok && (fl & F_RESOURCE));
+        T.stockpile = (uint32_t)ballot(ok && (fl & F_STOCKPILE));
+        T.aff0 = (uint32_t)ballot(ok && pres0 >= cost);
+        T.aff1 = (uint32_t)ballot(ok && pres1 >= cost);
+        T.prod = 0;
+#pragma unroll
+        for (int k = 0; k < MAX_TYPES; k++) T.prod |= (uint64_t)(uniu((uint32_t)rl((int)pm, k)) & 0xFFu) << (8 * k);
+        return T;
+    }
+    // unitMask's bits for range <= 1 units (the range > 1 attack window: farAttackBits) from the
+    // tables: two LDS rounds (the 4 neighbour cells, then the units on them) instead of a dependent
+    // read chain per neighbour and produce-list entry.  cu = the unit's core word, carried = its
+    // resources.  Same bits as unitMask(s, ..., true).
+    DEV void maskBitsFast(const MaskTables& T, uint32_t cu, int carried, uint32_t& w0, uint32_t& w1, uint32_t& w2) const {
+        const int x = ux(cu), y = uy(cu), typ = utyp(cu), pl = uplay(cu);
+        const int ctr = R / 2, atkBase = 1 + 6 + 16 + NT;
+        int n[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const int nx = x + dxo(d), ny = y + dyo(d);
+            n[d] = inb(nx, ny) ? cell[ny * W + nx] : WALL;
+        }
+        uint32_t oc[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) oc[d] = n[d] < CAP ? uc[n[d]] : 0u;
+        const bool atk = (T.attack1 >> typ) & 1u, harv = (T.harvest >> typ) & 1u, mov = (T.move >> typ) & 1u;
+        const uint32_t canProd = (uint32_t)(T.prod >> (8 * typ)) & 0xFFu & (pl == 0 ? T.aff0 : T.aff1);
+        uint64_t lo = 1ull | (1ull << (1 + T_NONE));
+        uint32_t hi = 0;
+        auto setb = [&](int k) {
+            if (k < 64) lo |= 1ull << k;
+            else hi |= 1u << (k - 64);
+        };
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            if (n[d] < CAP) {
+                const int op = uplay(oc[d]), ot = utyp(oc[d]);
+                if (atk && op >= 0 && op != pl) {
+                    setb(1 + T_ATTACK);
+                    setb(atkBase + (ctr + dyo(d)) * R + (ctr + dxo(d)));
+                }
+                if (harv && carried == 0 && ((T.resource >> ot) & 1u)) {
+                    setb(1 + T_HARVEST);
+                    setb(1 + 6 + 4 + d);
+                }
+                if (harv && carried > 0 && ((T.stockpile >> ot) & 1u) && op == pl) {
+                    setb(1 + T_RETURN);
+                    setb(1 + 6 + 8 + d);
+                }
+            } else if (n[d] == EMPTY) {
+                if (canProd) {
+                    setb(1 + T_PRODUCE);
+                    setb(1 + 6 + 12 + d);
+                }
+                if (mov) {
+                    setb(1 + T_MOVE);
+                    setb(1 + 6 + d);
+                }
+            }
+        }
+        // produce-type bits 23 + ut (below 64 for any table with <= 8 types)
+        if (canProd && (n[0] == EMPTY || n[1] == EMPTY || n[2] == EMPTY || n[3] == EMPTY)) lo |= (uint64_t)canProd << (1 + 6 + 16);
+        w0 = (uint32_t)lo;
+        w1 = (uint32_t)(lo >> 32);
+        w2 = hi;
+    }
+    // The range > 1 attack bits of unitMask (Unit.java:424-434: every enemy unit within the disk) for
+    // lanes with far = true, from the unit list held one unit per lane (cuLane = unit core word of
+    // lane j, all units in one wave, none dead): one pass over the live owned units instead of a
+    // (2r+1)^2 cell scan per ranged unit — the same set, as a cell holds at most one unit.  Whole wave.
+    DEV void farAttackBits(bool far, uint32_t cu, uint32_t cuLane, uint64_t owned, uint32_t& w0, uint32_t& w1,
+                           uint32_t& w2) const {
+        if (!ballot(far)) return;
+        const int x = ux(cu), y = uy(cu), pl = uplay(cu);
+        const int r = far ? U.range[utyp(cu)] : 0, ctr = R / 2, atkBase = 1 + 6 + 16 + NT;
+        uint64_t lo = 0;
+        uint32_t hi = 0;
+        for (uint64_t m = owned; m; m &= m - 1) {
+            const uint32_t cj = uniu((uint32_t)rl((int)cuLane, __builtin_ctzll(m)));
+            const int dx = ux(cj) - x, dy = uy(cj) - y;
+            if (far && uplay(cj) != pl && dx * dx + dy * dy <= r * r) {
+                const int k = atkBase + (ctr + dy) * R + (ctr + dx);
+                if (k < 64) lo |= 1ull << k;
+                else hi |= 1u << (k - 64);
+                lo |= 1ull << (1 + T_ATTACK);
+            }
+        }
+        w0 |= (uint32_t)lo;
+        w1 |= (uint32_t)(lo >> 32);
+        w2 |= hi;
+    }
+    // farAttackBits from per-player unit row bitmaps (rows[p * H + y] bit x = a unit of player p at
+    // (x, y); W <= 32): each far lane reads the 2r + 1 enemy rows around it and keeps the bits inside
+    // the disk.  Whole wave; rows complete (after a wsync).
+    DEV void farAttackRows(bool far, uint32_t cu, const uint32_t* rows, uint32_t& w0, uint32_t& w1, uint32_t& w2) const {
+        if (!ballot(far)) return;
+        const int x = ux(cu), y = uy(cu), pl = uplay(cu);
+        const int r = far ? U.range[utyp(cu)] : 0, ctr = R / 2, atkBase = 1 + 6 + 16 + NT;
+        const uint32_t* er = rows + (far ? (1 - pl) * H : 0);
+        uint64_t lo = 0;
+        uint32_t hi = 0;
+#pragma unroll
+        for (int dy = -ctr; dy <= ctr; dy++) {
+            const int yy = y + dy;
+            if (!far || dy < -r || dy > r || yy < 0 || yy >= H) continue;
+            const uint64_t word = er[yy];
+            uint64_t win = x >= r ? (word >> (x - r)) : (word << (r - x));  // bit j = column x - r + j
+            uint64_t disk = 0;
+#pragma unroll
+            for (int j = 0; j <= 2 * ctr; j++)
+                if (j <= 2 * r && (j - r) * (j - r) + dy * dy <= r * r) disk |= 1ull << j;
+            win &= disk;
+            if (!win) continue;
+            const int base = atkBase + (ctr + dy) * R + (ctr - r);
+            if (base < 64) {
+                lo |= win << base;
+                if (base > 0) hi |= (uint32_t)(win >> (64 - base));
+            } else {
+                hi |= (uint32_t)(win << (base - 64));
+            }
+            lo |= 1ull << (1 + T_ATTACK);
+        }
+        w0 |= (uint32_t)lo;
+        w1 |= (uint32_t)(lo >> 32);
+        w2 |= hi;
     }
     // Park each idle unit's 79-bit mask in its unused assignment words (at/as/ua low bits).
     // pset: bit p = park the masks of player p's idle units (both players in one pass for self-play)
@@ -2285,6 +2454,10 @@ struct Game {
         const int total = HW * K;
         uint32_t* nb = (uint32_t*)rseq;  // cycle() scratch, free here: [slot i][MW] new bits
         if (l < NW) nb[l] = 0;
+        // per-player unit row bitmaps for the range > 1 attack bits (rslot scratch, free here)
+        uint32_t* rows = (uint32_t*)rslot;
+        const bool rowB = W <= 32 && 2 * H <= 32;
+        if (rowB && l < 2 * H) rows[l] = 0;
         int si = -1;  // slot index of this lane's unit record, -1 = none
         uint32_t cu = 0;
         if (l < nu) {
@@ -2298,9 +2471,26 @@ struct Game {
         const int c = uy(cu) * W + ux(cu);
         wsync();
         if (si >= 0) atomicOr(&nb[si * MW + (c >> 5)], 1u << (c & 31));
+        if (rowB && l < nu && !(cu & UC_DEAD) && uplay(cu) >= 0) atomicOr(&rows[uplay(cu) * H + uy(cu)], 1u << ux(cu));
         uint32_t w0 = 0, w1 = 0, w2 = 0;
-        if (si >= 0) unitMask(l, w0, w1, w2);
+        {
+            MPHASE(16);
+            const MaskTables T = maskTables();
+            MPHASE(17);
+            const int carried = l < nu ? res[l] : 0;
+            if (si >= 0) maskBitsFast(T, cu, carried, w0, w1, w2);
+            MPHASE(18);
+            const bool far = si >= 0 && ((T.attackFar >> utyp(cu)) & 1u);
+            if (rowB) {
+                wsync();
+                farAttackRows(far, cu, rows, w0, w1, w2);
+            } else {
+                farAttackBits(far, cu, cu, ballot(l < nu && !(cu & UC_DEAD) && uplay(cu) >= 0), w0, w1, w2);
+            }
+            MPHASE(19);
+        }
         wsync();
+        MPHASE(12);
         uint32_t cur = 0, old = 0;
         int i = 0, w = 0;
         if (l < NW) {
@@ -2322,6 +2512,7 @@ struct Game {
             const int slot = slot0 + si;
             const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
             storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, lo, w2);
+            MPHASE(13);
             if (pol) {
                 int32_t a[7];
                 sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
@@ -2331,6 +2522,7 @@ struct Game {
                 for (int q = 0; q < 7; q++) dst[q] = a[q];
             }
         }
+        MPHASE(14);
         // cells whose idle unit is gone: zero record + zero row
         const uint32_t gone = old & ~cur;
         const int n = __popc(gone);
@@ -2427,7 +2619,7 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     const int side = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
     bool freshObs = true;  // observation comes from the current (post-step or fresh) state
 #ifdef MRTS_PHASE_TIMING
-    for (int i = 0; i < 16; i++) G.phAcc[i] = 0;
+    for (int i = 0; i < NPH; i++) G.phAcc[i] = 0;
     G.tph_ = __builtin_amdgcn_s_memtime();
     const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -2613,7 +2805,7 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
     PHASE(10);
 #ifdef MRTS_PHASE_TIMING
     if (lane_id() == 0 && G.g < PH_GAMES) {
-        for (int i = 0; i < 16; i++) g_phase[i * PH_GAMES + G.g] += G.phAcc[i];
+        for (int i = 0; i < NPH; i++) g_phase[i * PH_GAMES + G.g] += G.phAcc[i];
         g_span[G.g] = rt0_;
         g_span[PH_GAMES + G.g] = __builtin_amdgcn_s_memrealtime();
         g_span[2 * PH_GAMES + G.g] = (unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
@@ -2814,17 +3006,17 @@ namespace mrts {
 #ifdef MRTS_PHASE_TIMING
 // out[16]: per-phase sums over games (and the max over games in out[16..31] when given 32 slots)
 hipError_t phaseTimes(unsigned long long* out, int reset) {
-    std::vector<unsigned long long> h((size_t)16 * PH_GAMES);
+    std::vector<unsigned long long> h((size_t)NPH * PH_GAMES);
     hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_phase), h.size() * sizeof(h[0]));
     if (e != hipSuccess) return e;
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < NPH; i++) {
         unsigned long long sum = 0, mx = 0;
         for (int g = 0; g < PH_GAMES; g++) {
             sum += h[(size_t)i * PH_GAMES + g];
             mx = h[(size_t)i * PH_GAMES + g] > mx ? h[(size_t)i * PH_GAMES + g] : mx;
         }
         out[i] = sum;
-        out[16 + i] = mx;
+        out[NPH + i] = mx;
     }
     if (reset) {
         std::fill(h.begin(), h.end(), 0ull);

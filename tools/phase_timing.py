@@ -20,7 +20,8 @@ from microrts_amd import DeviceVecEnv  # noqa: E402
 
 NAMES = ["load", "predecode", "decode(chain)", "issue", "cycle", "outcome+reset", "obs", "compact", "stashMasks",
          "writeMasks(flush)", "store", "slowIssueBatches(x1000)", "decode(unitLoads)", "decode(baseRes)", "decode(cellRank)",
-         "buildIndexCalls(x1000)"]
+         "buildIndexCalls(x1000)"] + [f"p{i}" for i in range(16, 32)]
+NPH = 32
 E = int(os.environ.get("E", 4096))
 MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
 PO = os.environ.get("PO", "0") == "1"
@@ -67,7 +68,7 @@ def tail_report(st, en, place):
 
 
 def read(reset):
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * (2 * NPH))()
     _lib.check(L.mrts_phase_times(buf, reset))
     return list(buf)
 
@@ -119,5 +120,5 @@ for delta in (True, False):
     per = {NAMES[i]: round(ph[i] / (n * E)) for i in range(len(NAMES))}
     print(json.dumps({"mask_delta": delta, "fused_policy": FUSED, "k_env_us": 1e3 * ms / n, "last_launch": spans, "mean_cycles_per_game_step": per,
                       "total_cycles": sum(per.values()),
-                      "max_game_cycles_over_100_steps": {NAMES[i]: ph[16 + i] for i in range(len(NAMES))}}), flush=True)
+                      "max_game_cycles_over_100_steps": {NAMES[i]: ph[NPH + i] for i in range(len(NAMES))}}), flush=True)
     env.close()
