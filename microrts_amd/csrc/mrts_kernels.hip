@@ -2639,6 +2639,14 @@ __global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn
         }
     } else {
         G.load(D.mask_delta && D.masks);
+        // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
+        // slowest one, so the games with the most units (the longest serial chains) issue first.
+        {
+            const int q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
+            if (q == 1) __builtin_amdgcn_s_setprio(1);
+            else if (q == 2) __builtin_amdgcn_s_setprio(2);
+            else if (q == 3) __builtin_amdgcn_s_setprio(3);
+        }
     }
 #ifdef MRTS_PHASE_TIMING
     const int nu0_ = G.nu;
