@@ -1661,6 +1661,10 @@ struct Game {
     DEV void cycle() {
         time++;
         ixValid = false;
+        if (nu <= 64) {
+            cycleLanes();
+            return;
+        }
         // gather the ready list into LDS (slot order), count R
         int R = 0;
         for (int o0 = 0; o0 < nu; o0 += 64) {
@@ -1732,6 +1736,40 @@ struct Game {
                 execute(os);
             }
         }
+    }
+    // cycle() with every unit in one wave: lane = unit.  Each ready assignment leaves the map first
+    // (in parallel); NONE executes as a no-op, so only the other ready assignments are ordered — by
+    // insertion sequence (unique), ranked in registers — and executed one by one from registers.
+    DEV void cycleLanes() {
+        const int l = lane_id();
+        bool ready = false;
+        uint32_t a = 0, cu = 0;
+        int prm = 0, sq = 0;
+        if (l < nu) {
+            a = ua[l];
+            cu = uc[l];
+            prm = par[l];
+            sq = as[l];
+            const int t0 = at[l];
+            if (a & UA_PRESENT) ready = eta(ua_type(a), prm, ua_ut(a), utyp(cu)) + t0 <= time;
+        }
+        if (ready) ua[l] = a & ~(UA_READY | UA_PRESENT);
+        const bool wk = ready && ua_type(a) != T_NONE;
+        const uint64_t work = ballot(wk);
+        wsync();
+        if (!work) return;
+        int rank = 0;
+        for (uint64_t m = work; m; m &= m - 1) rank += rl(sq, __builtin_ctzll(m)) < sq;
+        killedLanes = 0;
+        readySlot = wk ? l : -1;
+        const int nw = __popcll(work);
+        for (int r = 0; r < nw; r++) {
+            const int k = __builtin_ctzll(ballot(wk && rank == r));
+            uint32_t c = uniu((uint32_t)rl((int)cu, k));
+            if ((killedLanes >> k) & 1ull) c |= UC_DEAD;
+            execute(k, c, uniu((uint32_t)rl((int)a, k)) & ~(UA_READY | UA_PRESENT), rl(prm, k));
+        }
+        readySlot = -1;
     }
     // PhysicalGameState.gameover/winner (rts/PhysicalGameState.java:334-387)
     DEV void outcome(bool& gameover, int& winner) {
