@@ -69,6 +69,43 @@ enum : uint32_t {
 };
 
 DEV int lane_id() { return (int)threadIdx.x; }
+// Output stores.  WT = streaming (`nt`) stores, so output lines do not sit dirty in the XCD's L2
+// until the end-of-kernel write-back.  Builtins, not inline asm: the wait-count and store-data
+// hazard passes must see the stores.  MRTS_WT bits (measured on c3 / c5 / --mask-mode full,
+// profiles/r12_summary.md): 1 full-observability planes (c3 +4.5 %, full masks +3 %: on),
+// 2 delta mask records + policy rows (c3 -1.3 %), 4 full-rewrite mask chunks (-15 %),
+// 8 state block (neutral), 16 partial-observability planes (c5 -18 %).
+#ifndef MRTS_WT
+#define MRTS_WT 1
+#endif
+typedef int32_t i32x4v __attribute__((ext_vector_type(4)));
+typedef int32_t i32x4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef int32_t i32x3u __attribute__((ext_vector_type(3), aligned(4)));
+template <bool WT>
+DEV void st4(void* p, int a, int b, int c, int d) {  // 16-byte aligned
+    const i32x4v v = {a, b, c, d};
+    if (WT) __builtin_nontemporal_store(v, (i32x4v*)p);
+    else *(i32x4v*)p = v;
+}
+template <bool WT>
+DEV void st4u(void* p, int a, int b, int c, int d) {  // 4-byte aligned
+    const i32x4u v = {a, b, c, d};
+    if (WT) __builtin_nontemporal_store(v, (i32x4u*)p);
+    else *(i32x4u*)p = v;
+}
+template <bool WT>
+DEV void st3u(void* p, int a, int b, int c) {  // 4-byte aligned
+    const i32x3u v = {a, b, c};
+    if (WT) __builtin_nontemporal_store(v, (i32x3u*)p);
+    else *(i32x3u*)p = v;
+}
+template <bool WT>
+DEV void st1(int32_t* p, int a) {
+    if (WT) __builtin_nontemporal_store(a, p);
+    else *p = a;
+}
+constexpr bool WT_OBS = (MRTS_WT & 1) != 0, WT_MASK = (MRTS_WT & 2) != 0, WT_FULLMASK = (MRTS_WT & 4) != 0,
+               WT_STATE = (MRTS_WT & 8) != 0, WT_POOBS = (MRTS_WT & 16) != 0;
 DEV int ux(uint32_t c) { return (int)(c & 0xFF); }
 DEV int uy(uint32_t c) { return (int)((c >> 8) & 0xFF); }
 DEV int utyp(uint32_t c) { return (int)((c >> 16) & 0xF); }
@@ -442,16 +479,16 @@ struct Game {
             case H_RES1: hv = pres1; break;
             case H_SEQ: hv = seq; break;
         }
-        if (l < H_WORDS) s[l] = hv;
+        if (l < H_WORDS) st1<WT_STATE>(s + l, hv);
         int32_t* arr = s + H_WORDS;
         for (int i = l; i < nu; i += 64) {
-            arr[A_UC * CAP + i] = (int32_t)uc[i];
-            arr[A_HP * CAP + i] = hp[i];
-            arr[A_RES * CAP + i] = res[i];
-            arr[A_UA * CAP + i] = (int32_t)ua[i];
-            arr[A_PAR * CAP + i] = par[i];
-            arr[A_AT * CAP + i] = at[i];
-            arr[A_AS * CAP + i] = as[i];
+            st1<WT_STATE>(arr + A_UC * CAP + i, (int32_t)uc[i]);
+            st1<WT_STATE>(arr + A_HP * CAP + i, hp[i]);
+            st1<WT_STATE>(arr + A_RES * CAP + i, res[i]);
+            st1<WT_STATE>(arr + A_UA * CAP + i, (int32_t)ua[i]);
+            st1<WT_STATE>(arr + A_PAR * CAP + i, par[i]);
+            st1<WT_STATE>(arr + A_AT * CAP + i, at[i]);
+            st1<WT_STATE>(arr + A_AS * CAP + i, as[i]);
         }
     }
     // new GameState(PhysicalGameState.load(map)) — JNIGridnetClient.reset (tests/JNIGridnetClient.java:239-241)
@@ -1954,7 +1991,7 @@ struct Game {
                 for (int j = 0; j < 4; j++) obsCell(c4 + j, player0, v[j]);
 #pragma unroll
                 for (int pl = 0; pl < 6; pl++)
-                    *(int4*)(o0 + (size_t)pl * HW + c4) = make_int4(v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
+                    st4<WT_OBS>(o0 + (size_t)pl * HW + c4, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
                 if (nslots == 2) {  // the other player's view differs only in the owner plane
                     int32_t* o1 = o0 + (size_t)D.C * HW;
 #pragma unroll
@@ -1966,7 +2003,7 @@ struct Game {
                             w.z = w.z ? 3 - w.z : 0;
                             w.w = w.w ? 3 - w.w : 0;
                         }
-                        *(int4*)(o1 + (size_t)pl * HW + c4) = w;
+                        st4<WT_OBS>(o1 + (size_t)pl * HW + c4, w.x, w.y, w.z, w.w);
                     }
                 }
             }
@@ -2020,7 +2057,7 @@ struct Game {
                 for (int j = 0; j < 4; j++) planes(4 * c4 + j, v[j]);
 #pragma unroll
                 for (int k = 0; k < 6; k++)
-                    *(int4*)(out + k * HW + 4 * c4) = make_int4(v[0][k], v[1][k], v[2][k], v[3][k]);
+                    st4<WT_POOBS>(out + k * HW + 4 * c4, v[0][k], v[1][k], v[2][k], v[3][k]);
             }
         } else {
             for (int c = lane_id(); c < HW; c += 64) {
@@ -2051,8 +2088,8 @@ struct Game {
                     m[j] = seen(mineRows, cx, cy) ? 1 : 0;
                     t[j] = seen(theirRows, cx, cy) ? 1 : 0;
                 }
-                *(int4*)(out + 6 * HW + 4 * c4) = make_int4(m[0], m[1], m[2], m[3]);
-                *(int4*)(out + 7 * HW + 4 * c4) = make_int4(t[0], t[1], t[2], t[3]);
+                st4<WT_POOBS>(out + 6 * HW + 4 * c4, m[0], m[1], m[2], m[3]);
+                st4<WT_POOBS>(out + 7 * HW + 4 * c4, t[0], t[1], t[2], t[3]);
             }
         } else {
             for (int c = lane_id(); c < HW; c += 64) {
@@ -2394,7 +2431,10 @@ struct Game {
             const int p = i ? pl1 : pl0;
             uint8_t* out = D.masks + (size_t)(slot0 + i) * total;
             if ((total & 15) == 0) {
-                for (int j = l; j < total / 16; j += 64) *(uint4*)(out + 16 * j) = maskChunk(j, p);
+                for (int j = l; j < total / 16; j += 64) {
+                    const uint4 v = maskChunk(j, p);
+                    st4<WT_FULLMASK>(out + 16 * j, (int)v.x, (int)v.y, (int)v.z, (int)v.w);
+                }
             } else {
                 for (int o = l; o < total; o += 64) {
                     const int c = o / K, k = o - c * K;
@@ -2451,8 +2491,6 @@ struct Game {
     // reach dword alignment, whole dwords (dwordx4 / dwordx3 stores, 4-byte aligned), then the tail
     // bytes — neighbouring records written by other lanes are never touched.
     DEV void storeRecord(uint8_t* dst, uint64_t lo, uint32_t hi) const {
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
-        typedef uint32_t u32x3 __attribute__((ext_vector_type(3), aligned(4)));
         const int head = (int)((4u - ((uint32_t)(uintptr_t)dst & 3u)) & 3u);
 #pragma unroll
         for (int i = 0; i < 3; i++)
@@ -2467,11 +2505,9 @@ struct Game {
         if (K == 79) {  // nd == 19 for every head
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                u32x4 w = {nib(4 * q), nib(4 * q + 1), nib(4 * q + 2), nib(4 * q + 3)};
-                *(u32x4*)(dw + 4 * q) = w;
+                st4u<WT_MASK>(dw + 4 * q, (int)nib(4 * q), (int)nib(4 * q + 1), (int)nib(4 * q + 2), (int)nib(4 * q + 3));
             }
-            u32x3 w3 = {nib(16), nib(17), nib(18)};
-            *(u32x3*)(dw + 16) = w3;
+            st3u<WT_MASK>(dw + 16, (int)nib(16), (int)nib(17), (int)nib(18));
         } else {
             for (int k = 0; k < nd; k++) dw[k] = nib(k);
         }
@@ -2556,8 +2592,8 @@ struct Game {
                 sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
                               (uint64_t)(w2 >> 1), c, a);
                 int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
-#pragma unroll
-                for (int q = 0; q < 7; q++) dst[q] = a[q];
+                st4u<WT_MASK>(dst, a[0], a[1], a[2], a[3]);
+                st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
             }
         }
         MPHASE(14);
@@ -2582,8 +2618,8 @@ struct Game {
                 storeRecord(D.masks + (size_t)slot * total + (size_t)cz * K, 0ull, 0u);
                 if (pol) {
                     int32_t* dst = D.pol_actions + ((size_t)slot * HW + cz) * 7;
-#pragma unroll
-                    for (int q = 0; q < 7; q++) dst[q] = 0;
+                    st4u<WT_MASK>(dst, 0, 0, 0, 0);
+                    st3u<WT_MASK>(dst + 4, 0, 0, 0);
                 }
             }
         }
