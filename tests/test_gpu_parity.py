@@ -236,8 +236,9 @@ def test_full_size_properties():
                                           ("maps/10x10/basesWorkers10x10.xml", True, 6),
                                           ("maps/4x4/base4x4.xml", False, 4)])
 def test_delta_masks_and_source_policy_match_full(mp, po, n_bot):
-    """Delta mask writes (only dirty rows rewritten) leave the buffer byte-identical to full writes,
-    and the source-bit policy kernel picks exactly the actions of the full-read policy kernel."""
+    """Delta mask and observation writes (only dirty rows / 4-cell chunks rewritten) leave the buffers
+    byte-identical to full writes after every step (auto-resets at 150 steps included), and the
+    source-bit policy kernel picks exactly the actions of the full-read policy kernel."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
 
@@ -260,6 +261,7 @@ def test_delta_masks_and_source_policy_match_full(mp, po, n_bot):
             b.random_policy(SEED, step)
         a.synchronize()
         b.synchronize()
+        assert torch.equal(a.obs, b.obs), f"delta observations differ at step {step}"
         assert torch.equal(a.masks, b.masks), f"delta masks differ at step {step}"
         assert torch.equal(a.actions, b.actions), f"source-bit / delta policy differs at step {step}"
         src = a.source.cpu().numpy().view(np.uint32)
