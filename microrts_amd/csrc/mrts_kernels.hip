@@ -263,6 +263,8 @@ struct Game {
     int g, H, W, HW, CAP;
     int K, NT, R;  // mask slots per cell, unit types, attack window (2 * max range + 1): table values or constants
     bool po;
+    int32_t* stBase;  // the state blocks (a leading kernel argument: preloaded into SGPRs)
+    int stWords;      // words per state block (a constant in a specialised kernel)
     uint32_t* uc;    // unit core: x | y<<8 | type<<16 | (player+1)<<20 | dead<<31
     uint32_t* ua;    // assignment: type | utype<<4 | tx<<8 | ty<<16 | PRESENT/READY/PA/DEC/BAD
     int32_t* at;     // assignment issue time (UnitActionAssignment.time)
@@ -303,9 +305,10 @@ struct Game {
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
     // array offset then folds to an immediate), else the kernel arguments
-    DEV Game(const KStatic& p, const KDyn& d, uint8_t* smem, int h, int w, int hw, int cap, bool partial, int k, int nt, int r)
+    DEV Game(const KStatic& p, const KDyn& d, int32_t* stb, int stw, uint8_t* smem, int h, int w, int hw, int cap, bool partial,
+             int k, int nt, int r)
         : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
-          po(partial) {
+          po(partial), stBase(stb), stWords(stw) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
         ua = (uint32_t*)q; q += 4 * CAP;
@@ -348,7 +351,7 @@ struct Game {
     }
     DEV bool inb(int x, int y) const { return x >= 0 && x < W && y >= 0 && y < H; }
     DEV const int32_t* tmpl() const { return P.tmpl + P.tmpl_off[g]; }
-    DEV int32_t* st() const { return D.state + (size_t)g * D.state_words; }
+    DEV int32_t* st() const { return stBase + (size_t)g * stWords; }
 
     // UnitAction.ETA (rts/UnitAction.java:307-329)
     DEV int eta(int t, int prm, int ut, int unitType) const {
@@ -2680,10 +2683,13 @@ DEV void aiGetAction(Game& G, int kind, int p) {
 // code vanishes — c3 (16x16, 320 slots), c2 (8x8, 128), c5 (32x32 PO, 320 slots = max_units 256).
 // FIX = 0: anything (launchEnv picks).
 template <int MODE, int FIX, int FCAP = 0, bool FPO = false>
-__global__ __launch_bounds__(64) void k_env(const KStatic* __restrict__ PS, KDyn D) {
+// stateArg and PS lead the argument list so that kernarg preloading (-amdgpu-kernarg-preload-count,
+// Makefile) hands them over in SGPRs: the first memory round (state block, unit-type table) issues
+// without waiting for a scalar load of the kernel arguments.
+__global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
-    Game G(P, D, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
+    Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
            FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius);
     // games [0, n_sp_games) are self-play (mrts_create's layout): no load needed to place the slots
     const bool selfplay = FIX ? true : G.g < D.n_sp_games;
@@ -3287,14 +3293,14 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
     auto is = [&](int w, int cap, bool po) { return fixable && hs.W == w && hs.CAP == cap && (hs.partial_obs != 0) == po; };
     switch (mode) {
         case MODE_STEP:
-            if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, ds, D);
-            else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, ds, D);
-            else if (is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, ds, D);
-            else hipLaunchKernelGGL((k_env<MODE_STEP, 0>), grid, block, lds, stream, ds, D);
+            if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
+            else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, D.state, ds, D);
+            else if (is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, D.state, ds, D);
+            else hipLaunchKernelGGL((k_env<MODE_STEP, 0>), grid, block, lds, stream, D.state, ds, D);
             break;
-        case MODE_RESET: hipLaunchKernelGGL((k_env<MODE_RESET, 0>), grid, block, lds, stream, ds, D); break;
-        case MODE_PLAYOUT: hipLaunchKernelGGL((k_env<MODE_PLAYOUT, 0>), grid, block, lds, stream, ds, D); break;
-        default:hipLaunchKernelGGL((k_env<MODE_MASKS, 0>), grid, block, lds, stream, ds, D); break;
+        case MODE_RESET: hipLaunchKernelGGL((k_env<MODE_RESET, 0>), grid, block, lds, stream, D.state, ds, D); break;
+        case MODE_PLAYOUT: hipLaunchKernelGGL((k_env<MODE_PLAYOUT, 0>), grid, block, lds, stream, D.state, ds, D); break;
+        default:hipLaunchKernelGGL((k_env<MODE_MASKS, 0>), grid, block, lds, stream, D.state, ds, D); break;
     }
     return hipGetLastError();
 }
