@@ -1989,9 +1989,34 @@ struct Game {
         int32_t* o0 = D.obs + (size_t)slot0 * D.C * HW;
         if ((HW & 3) == 0) {
             for (int c4 = 4 * lane_id(); c4 < HW; c4 += 256) {
+                // obsCell for 4 cells without branches: the 4 cell entries, then the occupants' 4
+                // fields each (an empty cell reads slot 0 and is masked), so the lane waits for two
+                // LDS rounds instead of one pair per occupied cell
+                int sc[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) sc[j] = cell[c4 + j];
+                uint32_t cu[4], ca[4];
+                int ch[4], cr[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int s = sc[j] < CAP ? sc[j] : 0;
+                    cu[j] = uc[s];
+                    ca[j] = ua[s];
+                    ch[j] = hp[s];
+                    cr[j] = res[s];
+                }
                 int v[4][6];
 #pragma unroll
-                for (int j = 0; j < 4; j++) obsCell(c4 + j, player0, v[j]);
+                for (int j = 0; j < 4; j++) {
+                    const bool occ = sc[j] < CAP;
+                    const int pl = uplay(cu[j]);
+                    v[j][0] = occ ? ch[j] : 0;
+                    v[j][1] = occ ? cr[j] : 0;
+                    v[j][2] = (occ && pl >= 0) ? ((pl + player0) % 2) + 1 : 0;
+                    v[j][3] = occ ? utyp(cu[j]) + 1 : 0;
+                    v[j][4] = (occ && (ca[j] & UA_PRESENT)) ? ua_type(ca[j]) : 0;
+                    v[j][5] = sc[j] == WALL ? 1 : 0;
+                }
 #pragma unroll
                 for (int pl = 0; pl < 6; pl++)
                     st4<WT_OBS>(o0 + (size_t)pl * HW + c4, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
