@@ -70,8 +70,11 @@ def parse():
                     help="kernel: the random policy is its own launch before each step; fused: the step kernel "
                          "samples the next step's actions from the masks it writes (mrts_step_fused_dev, same "
                          "Philox stream, bit-identical actions)")
-    ap.add_argument("--no-graph", action="store_true",
-                    help="launch the timed steps eagerly instead of replaying them as one captured hipGraph")
+    ap.add_argument("--launch", choices=["native", "graph", "eager"], default=None,
+                    help="how the K timed steps are enqueued: native = one mrts_rollout_fused_dev call (K launches "
+                         "from C++; fused policy only, the default there), graph = replay of a captured hipGraph "
+                         "(the default for --policy kernel), eager = one Python call per step")
+    ap.add_argument("--no-graph", action="store_true", help="alias of --launch eager")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-compare", action="store_true", help="skip the other policy form's comparison window")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -83,6 +86,12 @@ def parse():
     a.envs = a.envs or e
     a.po = po
     a.max_units = mu
+    if a.no_graph:
+        a.launch = "eager"
+    if a.launch is None:
+        a.launch = "native" if a.policy == "fused" else "graph"
+    if a.launch == "native" and a.policy != "fused":
+        ap.error("--launch native needs --policy fused")
     return a
 
 
@@ -207,8 +216,11 @@ def main():
     env.reset()
     if fused:
         env.random_policy(SEED, 0)
-    for k in range(a.burnin + a.warmup):
-        one_step(k)
+    if a.launch == "native" and gather_buf is None:  # burn-in + warmup through the timed window's own path
+        env.rollout_fused(SEED, 1, a.burnin + a.warmup)
+    else:
+        for k in range(a.burnin + a.warmup):
+            one_step(k)
     env.synchronize()
     # rows decoded per step (sum of mask[...,0]) and live units, for the algorithmic-byte count
     rows = float(env.masks[..., 0].sum().item()) / S
@@ -217,14 +229,19 @@ def main():
         units.append(env.dump_state(s)[4])
     mean_units = float(np.mean(units))
 
-    # The K timed steps (policy kernel + step kernel each) are captured once into a hipGraph and
-    # replayed as one launch, so host launch overhead does not pace the GPU ("capture launch-bound
-    # inner loops in hipGraphs").  Same kernels, same arguments.  Events cannot be timed inside a
-    # replayed graph on ROCm, so the step kernel's duration comes from HIP events around each launch
-    # in an eager pass over the K steps that follow (same stream, same episode phase).
+    # The K timed steps are enqueued so that host launch overhead does not pace the GPU: by default
+    # (fused policy) one native call, mrts_rollout_fused_dev, issues the K step launches from C++;
+    # --launch graph captures them once into a hipGraph and replays it.  Same kernels, same arguments
+    # either way (tests/test_gpu_parity.py::test_native_rollout_matches_fused_steps).  The native form
+    # has the smallest fixed cost per window (tools/launch_overhead.py: 23 us vs 32 us for a warm
+    # graph replay; a first replay costs ~20 us more), which matters at small K.  The step kernel's
+    # duration comes from HIP events around each launch in an eager pass over the K steps that
+    # follow (same stream, same episode phase): events cannot be timed inside the native or graph
+    # window without changing it.
     base = a.burnin + a.warmup
     graph = None
-    if not a.no_graph and gather_buf is None:
+    native = a.launch == "native" and gather_buf is None
+    if a.launch == "graph" and gather_buf is None:
         try:
             graph = torch.cuda.CUDAGraph()
             cap = torch.cuda.Stream(env.device)
@@ -248,19 +265,20 @@ def main():
     torch.cuda.synchronize(env.device)
     env.synchronize()
     t0 = time.perf_counter()
-    if graph is not None:
+    if native:
+        env.rollout_fused(SEED, base + 1, a.steps)
+    elif graph is not None:
         graph.replay()
     else:
         for k in range(a.steps):
             one_step(base + k, evs[k])
     if gather_buf is not None:
         gather_buf.wait()  # the last step's exchange belongs to the timed window
-    torch.cuda.synchronize(env.device)
-    env.synchronize()
+    torch.cuda.synchronize(env.device)  # device-wide: covers the env's stream too
     if world > 1:
         dist.barrier()
     t = time.perf_counter() - t0
-    if graph is not None:  # kernel-duration pass (untimed for `value`)
+    if native or graph is not None:  # kernel-duration pass (untimed for `value`)
         # hold the stream in a GPU spin while the host enqueues the K eager steps, so each event
         # pair brackets back-to-back kernels instead of the host's launch latency
         try:
@@ -328,6 +346,9 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (masked uniform random policy, Philox seed 0x5EEDC0DE)",
+        "parity": "bit-exact vs the C++ oracle (trace-pinned: all 280 reference traces replay exactly; Java itself "
+                  "cannot run in this image) — tests/test_gpu_parity.py, tests/test_kats.py; value over the K timed "
+                  "steps above",
         "config": {
             "workload": f"{a.config}: {a.map} self-play, {E} games/GPU ({2 * E} player slots), masks+obs every step"
                         + (", partial observability" if a.po else "")
@@ -337,11 +358,12 @@ def main():
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": a.mask_mode,
-            "launch": "hipGraph replay of the K timed steps" if graph is not None else "eager",
+            "launch": ("one mrts_rollout_fused_dev call (K step launches from C++)" if native
+                       else "hipGraph replay of the K timed steps" if graph is not None else "eager"),
             "policy": ("fused into the step kernel (mrts_step_fused_dev)" if fused
                        else "separate masked-uniform policy kernel before each step (mrts_policy_dev)"),
             "kernel_timing": (f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
-                              if graph is not None else f"{event_kind} around each step-kernel launch in the timed window"),
+                              if (native or graph is not None) else f"{event_kind} around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (
                 f", per-step RCCL int16 observation {a.gather_obs} overlapped on a comm stream" if gather_buf is not None
                 else ", no collective in the step"),
@@ -365,7 +387,7 @@ def main():
             "survey_8d_equivalent_GBps": survey / (kern_ms * 1e-3) / 1e9,
         },
     }
-    if world == 1 and graph is not None and gather_buf is None and not a.no_compare:
+    if world == 1 and (native or graph is not None) and gather_buf is None and not a.no_compare:
         # the other policy form over the next K steps, for comparison (same contract otherwise)
         mode["fused"] = not fused
         base2 = base + a.steps + 5

@@ -146,6 +146,13 @@ int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_sou
 int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                         uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step,
                         void* stream);
+/* n_steps consecutive mrts_step_fused_dev calls (next_step = first_next_step, first_next_step + 1,
+ * ...) enqueued from native code: the same launches with the same arguments, without a host
+ * language's per-call overhead between them (a random-policy rollout; the outputs of the last step
+ * remain in the buffers).  n_steps >= 0. */
+int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                           uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
+                           int32_t n_steps, void* stream);
 /* the next mrts_policy_dev call writes every row */
 int mrts_policy_invalidate(mrts_env* env);
 /* Optional compact output of every mask write: mask slot 0 ("own unit without an action here") as

@@ -414,6 +414,7 @@ struct mrts_env {
     DevUtt utt;
     UttInfo uttInfo;
     std::vector<int> tmplOffHost;
+    uint32_t cfgHash = 0;  // game kinds, map templates, max_steps, reward kinds, PO (checkpoint compatibility)
     int32_t* d_state = nullptr;
     int32_t* d_tmpl = nullptr;
     int32_t* d_tmplOff = nullptr;
@@ -558,8 +559,6 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         if (!cfg->map_paths) throw Fail{-EINVAL, "map_paths is null"};
         env = new mrts_env();
         env->device = cfg->device;
-        HIPCHK(hipSetDevice(cfg->device));
-        HIPCHK(hipStreamCreateWithFlags(&env->stream, hipStreamNonBlocking));
         env->uttInfo = cfg->utt_json ? uttFromJson(cfg->utt_json) : makeUtt(cfg->utt_version, cfg->conflict_policy);
         env->utt = env->uttInfo.dev;
         env->K = env->utt.K;
@@ -589,6 +588,23 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
             if (k1 < 0 || k1 > 1 || k2 < 0 || k2 > 1) throw Fail{-ENOTSUP, "only PassiveAI / RandomBiasedAI are native"};
             const int type = env->forwardModel ? 3 : (cfg->ai1_kinds ? 2 : 1);  // GT_PLAYOUT / BOT_VS_BOT / AGENT_VS_BOT
             env->gameKindHost[(size_t)(env->nSpGames + j)] = type | (k1 << 4) | (k2 << 8);
+            // JNIGridnetClient.gameStep runs the opponent on its PartiallyObservableGameState
+            // (tests/JNIGridnetClient.java:164-173).  The GPU RandomBiasedAI takes getUnitActions of an
+            // owned unit from the full cell map, which equals the view's only when every cell the unit
+            // can act on (its 4 neighbours, its attack disk) lies inside its own sight disk.  Every
+            // built-in table satisfies that; a custom table that does not is refused, not run with
+            // different action lists.
+            if (cfg->partial_obs && type == 1 && k2 == MRTS_BOT_RANDOM_BIASED) {
+                const DevUtt& u = env->utt;
+                for (int t = 0; t < u.ntypes; t++) {
+                    const bool acts = (u.flags[t] & (F_MOVE | F_ATTACK | F_HARVEST)) || u.nprod[t] > 0;
+                    const int need = std::max(1, (u.flags[t] & F_ATTACK) ? u.range[t] : 1);
+                    if (acts && u.sight[t] < need)
+                        throw Fail{-ENOTSUP, "partial_obs + RandomBiasedAI: unit type " + env->uttInfo.names[(size_t)t] +
+                                                 " has sightRadius < max(1, attackRange); its PO action list would "
+                                                 "differ from the full-state one this build computes"};
+                }
+            }
         }
         // maps: one template per distinct path
         std::map<std::string, int> tmplIndex;
@@ -621,6 +637,9 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         env->maxUnits = maxUnits;
         if (env->CAP > 0xFFF0) throw Fail{-EINVAL, "map too large"};
         if ((size_t)env->nSlots * env->HW >= (size_t)1 << 31) throw Fail{-EINVAL, "n_slots * H * W must be < 2^31"};
+        // everything above is host-only validation (testable without a GPU); device work starts here
+        HIPCHK(hipSetDevice(cfg->device));
+        HIPCHK(hipStreamCreateWithFlags(&env->stream, hipStreamNonBlocking));
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, cfg->device));
         const size_t lds = ldsBytes(env->HW, env->W, env->CAP, env->partialObs);
@@ -649,6 +668,21 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         }
         env->tmplOffHost.resize((size_t)env->nGames);
         for (int g = 0; g < env->nGames; g++) env->tmplOffHost[(size_t)g] = off[(size_t)gameTmpl[(size_t)g]];
+        {  // what a state block does not carry but its meaning depends on: a restore must match it
+            uint32_t hv = 2166136261u;
+            auto mix = [&hv](const void* p, size_t n) {
+                for (size_t i = 0; i < n; i++) hv = (hv ^ ((const uint8_t*)p)[i]) * 16777619u;
+            };
+            mix(env->gameKindHost.data(), env->gameKindHost.size() * 4);
+            mix(blob.data(), blob.size() * 4);
+            mix(env->tmplOffHost.data(), env->tmplOffHost.size() * 4);
+            mix(&env->maxSteps, 4);
+            mix(&env->partialObs, sizeof(env->partialObs));
+            const int nrk = (int)env->rewardKinds.size();
+            mix(&nrk, 4);
+            mix(env->rewardKinds.data(), env->rewardKinds.size() * sizeof(env->rewardKinds[0]));
+            env->cfgHash = hv;
+        }
         const size_t sw = (size_t)stateWords(env->CAP, env->HW);
         HIPCHK(hipMalloc(&env->d_state, sw * env->nGames * 4));
         HIPCHK(hipMalloc(&env->d_tmpl, blob.size() * 4));
@@ -793,6 +827,18 @@ int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_play
     } catch (const Fail& f) {
         return fail(f);
     }
+}
+
+int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                           uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
+                           int32_t n_steps, void* stream) {
+    if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
+    for (int32_t k = 0; k < n_steps; k++) {
+        const int r = mrts_step_fused_dev(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
+                                          first_next_step + (uint32_t)k, stream);
+        if (r) return r;
+    }
+    return 0;
 }
 
 int mrts_step_rows_dev(mrts_env* env, const int32_t* d_rows, int32_t n_rows, const int32_t* d_players, int32_t* d_obs,
@@ -1337,6 +1383,8 @@ struct CkptHeader {
     char magic[8];
     int32_t version, H, W, CAP, nGames, nSpGames, words;
     uint32_t uttHash;
+    uint32_t cfgHash;  // mrts_env::cfgHash: game kinds (opponents), map templates, max_steps, reward kinds, PO
+    int32_t pad_;
 };
 uint32_t uttHash(const DevUtt& u) {
     uint32_t h = 2166136261u;
@@ -1358,7 +1406,7 @@ int mrts_checkpoint(mrts_env* env, void* buf, int64_t cap) {
         CkptHeader h;
         std::memset(&h, 0, sizeof(h));
         std::memcpy(h.magic, "MRTSCKP1", 8);
-        h.version = 1;
+        h.version = 2;
         h.H = env->H;
         h.W = env->W;
         h.CAP = env->CAP;
@@ -1366,6 +1414,7 @@ int mrts_checkpoint(mrts_env* env, void* buf, int64_t cap) {
         h.nSpGames = env->nSpGames;
         h.words = stateWords(env->CAP, env->HW);
         h.uttHash = uttHash(env->utt);
+        h.cfgHash = env->cfgHash;
         std::memcpy(buf, &h, sizeof(h));
         HIPCHK(hipDeviceSynchronize());
         HIPCHK(hipMemcpy((char*)buf + sizeof(h), env->d_state, (size_t)h.words * h.nGames * 4, hipMemcpyDeviceToHost));
@@ -1381,10 +1430,13 @@ int mrts_restore(mrts_env* env, const void* buf, int64_t size) {
         CkptHeader h;
         if (size < (int64_t)sizeof(h)) throw Fail{-EINVAL, "checkpoint too short"};
         std::memcpy(&h, buf, sizeof(h));
-        if (std::memcmp(h.magic, "MRTSCKP1", 8) != 0 || h.version != 1) throw Fail{-EINVAL, "not a checkpoint"};
+        if (std::memcmp(h.magic, "MRTSCKP1", 8) != 0 || h.version != 2) throw Fail{-EINVAL, "not a checkpoint"};
         if (h.H != env->H || h.W != env->W || h.CAP != env->CAP || h.nGames != env->nGames || h.nSpGames != env->nSpGames ||
             h.words != stateWords(env->CAP, env->HW) || h.uttHash != uttHash(env->utt))
             throw Fail{-EINVAL, "checkpoint of a different configuration"};
+        if (h.cfgHash != env->cfgHash)
+            throw Fail{-EINVAL, "checkpoint of a different configuration (opponents, maps, max_steps, reward functions "
+                                "or partial observability differ)"};
         if (size != mrts_checkpoint_size(env)) throw Fail{-EINVAL, "checkpoint size mismatch"};
         HIPCHK(hipDeviceSynchronize());
         HIPCHK(hipMemcpy(env->d_state, (const char*)buf + sizeof(h), (size_t)h.words * h.nGames * 4, hipMemcpyHostToDevice));

@@ -494,13 +494,14 @@ struct Game {
             st1<WT_STATE>(arr + A_AS * CAP + i, as[i]);
         }
     }
-    // new GameState(PhysicalGameState.load(map)) — JNIGridnetClient.reset (tests/JNIGridnetClient.java:239-241)
+    // new GameState(PhysicalGameState.load(map)) — JNIGridnetClient.reset (tests/JNIGridnetClient.java:239-241).
+    // envSteps is NOT part of it: VecClient.reset (tests/JNIGridnetVecClient.java:179-211) never touches
+    // envSteps[]; only the auto-reset path zeroes it (:229,264-265,285).
     DEV void resetFromTemplate() {
         const int32_t* t = tmpl();
         const int nu_t = t[T_NU];
         time = 0;
         seq = 0;
-        hset(H_STEPS, 0);
         deaths = 0;
         pres0 = t[T_RES0];
         pres1 = t[T_RES1];
@@ -2867,6 +2868,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         const bool reset = done0 || steps >= D.max_steps;
         if (reset && D.done && lane_id() < nslots) D.done[(size_t)(slot0 + lane_id()) * D.n_rewards] = 1;
         if (reset) {
+            G.hset(H_STEPS, 0);  // envSteps[i] = 0 (JNIGridnetVecClient.java:229,264-265,285)
             G.resetFromTemplate();
             if (G.po) G.clearSnap();
         } else {

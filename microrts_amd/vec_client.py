@@ -131,6 +131,8 @@ def _kinds(ais, n):
 class _Handle:
     def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base,
                  ai1s=None, mask_delta=False, rewards=None, forward_model=False, max_units=0):
+        if len(map_paths) < n_selfplay + n_bot:  # mapPaths[i] per env (JNIGridnetVecClient.java:119,122)
+            raise ValueError(f"{len(map_paths)} map paths for {n_selfplay + n_bot} environments")
         L = _lib.load()
         self.L = L
         self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
@@ -209,6 +211,12 @@ class JNIGridnetVecClient:
     def __init__(self, a_num_selfplayenvs, a_num_envs, a_max_steps, a_rfs, a_micrortsPath, a_mapPaths, a_ai2s=None,
                  a_utt=None, partial_obs=False, device=0, seed=0, slot_id_base=0, _ai1s=None):
         rewards = _check_rfs(a_rfs)
+        # Java indexes a_ai2s[i] (and a_ai1s[i] in the bot-only constructor) for every bot env
+        # (JNIGridnetVecClient.java:121-123,163-165) and throws on a null or short array; no silent
+        # PassiveAI default here (DeviceVecEnv keeps one, documented there)
+        for name, ais in (("a_ai2s", a_ai2s), ("a_ai1s", _ai1s)):
+            if (name == "a_ai2s" or _ai1s is not None) and a_num_envs > 0 and (ais is None or len(ais) < a_num_envs):
+                raise ValueError(f"{name} names {0 if ais is None else len(ais)} bots for {a_num_envs} bot environments")
         utt = a_utt or UnitTypeTable()
         paths = [_resolve(a_micrortsPath, p) for p in a_mapPaths]
         self._h = _Handle(a_num_selfplayenvs, a_num_envs, a_max_steps, paths, a_ai2s, utt, partial_obs, device, seed,
@@ -326,7 +334,9 @@ class DeviceVecEnv:
     def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
                  device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None, mask_delta=True, source_bits=True,
                  rfs=None, max_units=0):
-        """mask_delta: `masks` is owned by this object and reused every call, so only changed rows are
+        """ai2s / ai1s: the bot of each bot env (names or objects named like the Java classes); a missing
+        or short list is padded with PassiveAI (the JNIGridnetVecClient mirror raises instead, like
+        Java).  mask_delta: `masks` is owned by this object and reused every call, so only changed rows are
         rewritten (the tensor must not be written by the caller).  source_bits: also keep mask slot 0
         as bits in `source` ([slots][ceil(H*W/32)] int32), which random_policy uses.  rfs: reward
         function names (a_rfs); reward / done are [S] for one function, [S][R] otherwise."""
@@ -387,6 +397,18 @@ class DeviceVecEnv:
         _lib.check(h.L.mrts_step_fused_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
                                            self._p(self.reward), self._p(self.done), self._p(self.masks), self.mask_player,
                                            seed, next_step, self._s(stream)))
+        self._policy_out, self._policy_version = self.actions, self.actions._version
+
+    def rollout_fused(self, seed, first_next_step, n_steps, stream=None):
+        """n_steps step_fused calls (next_step = first_next_step, first_next_step + 1, ...) enqueued by
+        native code (mrts_rollout_fused_dev): identical launches, no Python between them."""
+        h = self._h
+        assert self.masks is not None, "the fused policy samples from the masks"
+        if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
+            _lib.check(h.L.mrts_policy_invalidate(h.h))
+        _lib.check(h.L.mrts_rollout_fused_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
+                                              self._p(self.reward), self._p(self.done), self._p(self.masks),
+                                              self.mask_player, seed, first_next_step, n_steps, self._s(stream)))
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
     def step_rows(self, rows, stream=None):

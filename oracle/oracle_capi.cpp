@@ -292,7 +292,8 @@ struct VecClient {
         for (auto& e : selfPlay) e->reset(0);
         int nsp = (int)selfPlay.size() * 2;
         for (size_t j = 0; j < bots.size(); j++) bots[j]->reset(players ? players[nsp + (int)j] : 0);
-        std::fill(envSteps.begin(), envSteps.end(), 0);
+        // envSteps[] is left alone: reset() never touches it (JNIGridnetVecClient.java:179-211); it is
+        // zeroed only by the constructor (:116) and the auto-reset path (:229,264-265,285)
     }
     // gameStep (:213-297) with the grid layout [slot][HW][7] (row r = cell r, ascending)
     void step(const int32_t* actions, const int32_t* players) {

@@ -90,3 +90,55 @@ def _load_missing(tmp_path):
         _lib.load(str(tmp_path / "nope.so"))
     finally:
         _lib._lib = saved
+
+
+def test_vecclient_mirror_rejects_missing_bots():
+    """Java indexes a_ai2s[i] / a_ai1s[i] / mapPaths[i] for every env (JNIGridnetVecClient.java:119-123,
+    163-165): a null or short array throws there, so the mirror raises before creating anything."""
+    from microrts_amd import JNIGridnetVecClient
+
+    m = "maps/8x8/basesWorkers8x8.xml"
+    with pytest.raises(ValueError, match="a_ai2s"):
+        JNIGridnetVecClient(2, 2, 100, None, "", [m] * 4)
+    with pytest.raises(ValueError, match="a_ai2s"):
+        JNIGridnetVecClient(2, 2, 100, None, "", [m] * 4, ["PassiveAI"])
+    with pytest.raises(ValueError, match="a_ai1s"):
+        JNIGridnetVecClient.bots(100, None, "", [m] * 2, ["PassiveAI"], ["PassiveAI"] * 2)
+    with pytest.raises(ValueError, match="map paths"):
+        JNIGridnetVecClient(4, 0, 100, None, "", [m] * 3)
+
+
+def _utt_with(sight_of_worker):
+    import json
+
+    t = json.load(open(os.path.join(ROOT, "tests", "golden", "utts", "TestUnitTypeTable.json")))
+    for ut in t["unitTypes"]:
+        if ut["name"] == "Worker":
+            ut["sightRadius"] = sight_of_worker
+    return json.dumps(t)
+
+
+def test_po_random_biased_needs_sight_covering_actions():
+    """the GPU RandomBiasedAI computes an owned unit's actions on the full cell map, which
+    equals its PartiallyObservableGameState view (JNIGridnetClient.java:164-173) only if the unit sees
+    every cell it can act on.  A table with a blind Worker is refused at create (before any GPU
+    call); the same table without PO, or with PassiveAI, passes this check."""
+    from microrts_amd.vec_client import _Handle
+
+    m = "maps/8x8/basesWorkers8x8.xml"
+    blind = UnitTypeTable.fromJSON(_utt_with(0))
+    with pytest.raises(RuntimeError, match="sightRadius"):
+        _Handle(0, 2, 100, [m] * 2, ["RandomBiasedAI"] * 2, blind, True, 0, 0, 0)
+    # the check is specific: no error of that kind for PassiveAI or full observability (these
+    # then fail only on the missing GPU, or succeed on a GPU box)
+    for ai, po in (("PassiveAI", True), ("RandomBiasedAI", False)):
+        try:
+            h = _Handle(0, 2, 100, [m] * 2, [ai] * 2, blind, po, 0, 0, 0)
+            h.close()
+        except RuntimeError as e:
+            assert "sightRadius" not in str(e)
+    ok = UnitTypeTable.fromJSON(_utt_with(1))
+    try:
+        _Handle(0, 2, 100, [m] * 2, ["RandomBiasedAI"] * 2, ok, True, 0, 0, 0).close()
+    except RuntimeError as e:
+        assert "sightRadius" not in str(e)

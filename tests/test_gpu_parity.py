@@ -590,3 +590,33 @@ def test_fused_policy_matches_separate_kernels(mp, n_sp, n_bot, po, delta):
     A.close()
     B.close()
     del torch
+
+
+@pytest.mark.parametrize("mp,n_sp", [("maps/16x16/basesWorkers16x16.xml", 64), ("maps/8x8/basesWorkers8x8.xml", 16)])
+def test_native_rollout_matches_fused_steps(mp, n_sp):
+    """mrts_rollout_fused_dev(n) = n mrts_step_fused_dev calls (the bench's timed launch form), bit for
+    bit: observations, rewards, dones, masks, next actions and every game's state."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mk = lambda: DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=3)  # noqa: E731
+    A, B = mk(), mk()
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+    k = 0
+    for n in (1, 7, 0, 40, 180):  # crosses max_steps 300: auto-resets inside a rollout
+        for i in range(n):
+            A.step_fused(SEED, k + i + 1)
+        B.rollout_fused(SEED, k + 1, n)
+        k += n
+        A.synchronize()
+        B.synchronize()
+        for name in ("obs", "reward", "done", "masks", "actions"):
+            assert np.array_equal(getattr(A, name).cpu().numpy(), getattr(B, name).cpu().numpy()), f"{name} after {k}"
+        for s in range(0, n_sp, 2):
+            assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
+    assert np.array_equal(A._h.env_steps(), B._h.env_steps())
+    A.close()
+    B.close()
+    del torch

@@ -340,10 +340,71 @@ def kat_reward_functions(tmp, backend):
     r.close()
 
 
+class VecRunner:
+    """Two self-play slots + one agent-vs-PassiveAI env through the JNIGridnetVecClient mirror (GPU:
+    mrts_reset / mrts_step) or the oracle VecClient; all-zero grid actions (NONE rows)."""
+
+    def __init__(self, backend, map_path, max_steps):
+        self.backend = backend
+        if backend == "oracle":
+            self.e = oracle_py.OracleVecClient(2, 1, max_steps, [map_path] * 3, bot_kinds=[oracle_py.BOT_PASSIVE])
+        else:
+            from microrts_amd import JNIGridnetVecClient
+
+            self.e = JNIGridnetVecClient(2, 1, max_steps, ["WinLossRewardFunction"], "", [map_path] * 3,
+                                         a_ai2s=["PassiveAI"])
+        self.S = 3
+
+    def reset(self):
+        self.e.reset([0] * self.S)
+
+    def step(self):
+        """-> done[0] per slot (bool[S])."""
+        if self.backend == "oracle":
+            _, _, d = self.e.step(np.zeros((self.S, 25, 7), np.int32), [0] * self.S)
+            return d.astype(bool)
+        r = self.e.gameStep(np.zeros((self.S, 25, 7), np.int32), [0] * self.S)
+        return r.done[:, 0].copy()
+
+    def env_steps(self):
+        if self.backend == "oracle":
+            return [self.e.env_steps(s) for s in range(self.S)]
+        return self.e.envSteps.tolist()
+
+    def close(self):
+        self.e.close()
+
+
+def kat_env_steps_survive_reset(tmp, backend):
+    """A.10 — JNIGridnetVecClient.reset (JNIGridnetVecClient.java:179-211) reloads every game but never
+    touches envSteps[]; only the constructor (:116) and the auto-reset path (:229,264-265,285) zero it.
+    So with maxSteps = 10: 4 steps, reset() -> envSteps stays 4 and the next auto-reset comes after 6
+    more steps (envSteps 10 >= maxSteps, done[0] forced true), then after every 10 steps.  The map
+    keeps both players alive and idle (all rows NONE; the bot is PassiveAI), so gameover never fires."""
+    m = write_map(tmp / "k12.xml", 5, 5, [(BASE, 0, 0, 0), (BASE, 1, 4, 4)])
+    r = VecRunner(backend, m, 10)
+    r.reset()
+    assert r.env_steps() == [0, 0, 0]
+    for _ in range(4):
+        assert not r.step().any()
+    assert r.env_steps() == [4, 4, 4]
+    r.reset()
+    assert r.env_steps() == [4, 4, 4]  # NOT zeroed by reset()
+    for k in range(5):
+        assert not r.step().any(), f"step {k}"
+    assert r.env_steps() == [9, 9, 9]
+    assert r.step().all()  # 6th step after reset(): envSteps reaches 10 -> auto-reset
+    assert r.env_steps() == [0, 0, 0]
+    for k in range(9):
+        assert not r.step().any(), f"step {k}"
+    assert r.step().all()
+    r.close()
+
+
 KATS = [kat_illegal_becomes_none_eta, kat_resource_quirk_row_order, kat_rows_that_do_not_count,
         kat_player1_sees_player0_reservations, kat_dead_unit_still_executes, kat_simultaneous_kill_is_a_draw,
         kat_harvest_deplete_return, kat_duplicate_row_keeps_map_position, kat_po_killed_unit_in_view, kat_mask_record,
-        kat_reward_functions]
+        kat_reward_functions, kat_env_steps_survive_reset]
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k.__name__ for k in KATS])
@@ -355,3 +416,24 @@ def test_kat_oracle(kat, tmp_path):
 @pytest.mark.parametrize("kat", KATS, ids=[k.__name__ for k in KATS])
 def test_kat_gpu(kat, tmp_path):
     kat(tmp_path, "gpu")
+
+
+@pytest.mark.gpu
+def test_env_steps_survive_reset_bot_only():
+    """A.10 for the bot-only constructor (JNIGridnetVecClient.java:157-177): reset (:180-190) leaves
+    envSteps[] alone, the bot-only gameStep zeroes it on auto-reset (:217-229)."""
+    from microrts_amd import JNIGridnetVecClient
+
+    maps = ["maps/16x16/basesWorkers16x16.xml"] * 2
+    cl = JNIGridnetVecClient.bots(10, ["WinLossRewardFunction"], "", maps, ["PassiveAI"] * 2, ["PassiveAI"] * 2)
+    cl.reset([0, 0])
+    for _ in range(3):
+        assert not cl.gameStep(None, [0, 0]).done[:, 0].any()
+    assert cl.envSteps.tolist() == [3, 3]
+    cl.reset([0, 0])
+    assert cl.envSteps.tolist() == [3, 3]
+    for _ in range(6):
+        assert not cl.gameStep(None, [0, 0]).done[:, 0].any()
+    assert cl.gameStep(None, [0, 0]).done[:, 0].all()
+    assert cl.envSteps.tolist() == [0, 0]
+    cl.close()

@@ -196,3 +196,30 @@ def test_gpu_checkpoint_restore_replays_identically(crs, bots):
     other.close()
     env.close()
     del torch
+
+
+@pytest.mark.gpu
+def test_gpu_restore_rejects_other_opponents_or_limits():
+    """a checkpoint restored into a handle of the same shape but other opponents (PassiveAI
+    vs RandomBiasedAI), another max_steps, other reward functions or other maps would silently run
+    the checkpoint's game kinds until each game's next auto-reset.  The header carries a hash of
+    those, and restore refuses a mismatch; the identical configuration restores."""
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    base = dict(ai2s=["RandomBiasedAI"] * 2, seed=4)
+    env = DeviceVecEnv(2, 2, 2000, [M8] * 4, **base)
+    env.reset()
+    ck = env.checkpoint()
+    same = DeviceVecEnv(2, 2, 2000, [M8] * 4, **base)
+    same.restore(ck)
+    same.close()
+    for args, kw in (((2, 2, 2000, [M8] * 4), dict(ai2s=["PassiveAI"] * 2)),
+                     ((2, 2, 1000, [M8] * 4), base),
+                     ((2, 2, 2000, [M8] * 4), dict(base, rfs=["WinLossRewardFunction", "AttackRewardFunction"])),
+                     ((2, 2, 2000, [M8] * 2 + ["maps/8x8/bases8x8.xml"] * 2), base)):
+        other = DeviceVecEnv(*args, **kw)
+        with pytest.raises(RuntimeError, match="different configuration"):
+            other.restore(ck)
+        other.close()
+    env.close()
