@@ -216,13 +216,20 @@ def main():
     env.reset()
     if fused:
         env.random_policy(SEED, 0)
-    if a.launch == "native" and gather_buf is None:  # burn-in + warmup through the timed window's own path
-        env.rollout_fused(SEED, 1, a.burnin + a.warmup)
-    else:
-        for k in range(a.burnin + a.warmup):
-            one_step(k)
+    native_path = a.launch == "native" and gather_buf is None
+
+    def run_steps(first, n):  # steps first .. first + n - 1, through the timed window's own path
+        if native_path:
+            env.rollout_fused(SEED, first + 1, n)
+        else:
+            for k in range(first, first + n):
+                one_step(k)
+
+    run_steps(0, a.burnin)
     env.synchronize()
-    # rows decoded per step (sum of mask[...,0]) and live units, for the algorithmic-byte count
+    # rows decoded per step (sum of mask[...,0]) and live units, for the algorithmic-byte count —
+    # taken after the burn-in, so that the warmup steps run right before the timed window (no host
+    # work leaves the GPU idle in between)
     rows = float(env.masks[..., 0].sum().item()) / S
     units = []
     for s in range(0, min(S, 64), 2):
@@ -240,7 +247,7 @@ def main():
     # window without changing it.
     base = a.burnin + a.warmup
     graph = None
-    native = a.launch == "native" and gather_buf is None
+    native = native_path
     if a.launch == "graph" and gather_buf is None:
         try:
             graph = torch.cuda.CUDAGraph()
@@ -260,6 +267,7 @@ def main():
         print(f"bench: fence-free events unavailable ({ex!r}); torch.cuda.Event", file=sys.stderr)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
         event_kind = "torch.cuda.Event"
+    run_steps(a.burnin, a.warmup)  # the W untimed warmup steps, immediately before the window
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(env.device)
