@@ -22,6 +22,9 @@ using namespace mrts;
 namespace mrts {
 size_t ldsBytes(int HW, int W, int CAP, int po);
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream);
+#ifdef MRTS_ABLATE
+hipError_t setAblate(uint32_t v);
+#endif
 #ifdef MRTS_PHASE_TIMING
 hipError_t phaseTimes(unsigned long long* out, int reset);
 hipError_t phaseSpans(unsigned long long* out, int n);
@@ -1561,6 +1564,10 @@ int mrts_evaluate(mrts_env* env, int32_t maxplayer, float* out) {
     }
 }
 
+#ifdef MRTS_ABLATE
+// diagnostic build only: g_ablate (tools/ablate_price.py)
+int mrts_set_ablate(unsigned v) { return mrts::setAblate(v) == hipSuccess ? 0 : -EIO; }
+#endif
 #ifdef MRTS_PHASE_TIMING
 // diagnostic build only: per-phase cycle sums of k_env (tools/phase_timing.py)
 int mrts_phase_times(unsigned long long* out, int reset) { return mrts::phaseTimes(out, reset) == hipSuccess ? 0 : -EIO; }

@@ -53,6 +53,27 @@ __device__ unsigned long long g_span[3 * PH_GAMES];    // last launch: [game] st
     do {          \
     } while (0)
 #endif
+// Diagnostic build only (-DMRTS_ABLATE, tools/ablate_price.py): g_ablate bit b runs phase b twice
+// (idempotently, inputs laundered so the copies cannot be merged) — the marginal cost of a phase in
+// the real, contended kernel.  Never loaded by the package.
+#ifdef MRTS_ABLATE
+__device__ uint32_t g_ablate;
+template <class T>
+DEV T launder(T v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+template <class T>
+DEV void keepv(T v) {
+    asm volatile("" ::"v"(v));
+}
+#define ABL(b) ((G_AB >> (b)) & 1u)
+enum { AB_LOAD = 0, AB_OBS = 1, AB_STORE = 2, AB_MASKBITS = 3, AB_RECORD = 4, AB_POLICY = 5, AB_ACCEPT = 6,
+       AB_LEGAL = 7, AB_OUTCOME = 8, AB_INDEX = 9, AB_GONE = 10, AB_TABLES = 11, AB_RANK = 12, AB_DECODE = 13,
+       AB_ISSUE = 14, AB_CYCLERANK = 15,
+       // skips (outputs nothing in the step reads back): the observation, the mask record stores
+       AB_SKIP_OBS = 16, AB_SKIP_RECORD = 17 };
+#endif
 enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2, GT_PLAYOUT = 3 };  // game_kind & 15
 // per-player counters of this step's issued pairs, as the TraceEntry holds them (after issueSafe's
 // legality rewrite, before issue()'s conflict cancellations): HARVEST, RETURN, ATTACK, and PRODUCE
@@ -292,6 +313,10 @@ struct Game {
 #ifdef MRTS_PHASE_TIMING
     uint64_t tph_;
     uint64_t phAcc[NPH];  // per-phase cycles (registers: constant indices), flushed at kernel end
+#endif
+#ifdef MRTS_ABLATE
+    uint32_t G_AB = 0;
+    DEV bool ab(int b) const { return (G_AB >> b) & 1u; }
 #endif
     bool ixValid;
     bool anyMP;
@@ -547,9 +572,21 @@ struct Game {
         }
         const bool useIx = (HW + 2 * W + 31) / 32 <= 64;
         if (useIx) buildIndex();  // while the rows are in flight
+#ifdef MRTS_ABLATE
+        if (useIx && ab(AB_INDEX)) buildIndex();
+#endif
         MPHASE(22);
         int t = 0, pr = -1, ut = 0, tx = 0, ty = 0;
         bool bad = false;
+#ifdef MRTS_ABLATE
+        if (ab(AB_DECODE) && idle) {
+            int32_t b2[7];
+            for (int k = 0; k < 7; k++) b2[k] = launder(a[k]);
+            int t2 = 0, pr2 = -1, ut2 = 0, tx2 = 0, ty2 = 0;
+            const bool bad2 = decodeFields(launder(cu), b2, t2, pr2, ut2, tx2, ty2);
+            keepv(t2 + pr2 + ut2 + tx2 + ty2 + (int)bad2);
+        }
+#endif
         if (idle) bad = decodeFields(cu, a, t, pr, ut, tx, ty);
         if (ballot(bad)) addErr(E_PRODUCE_TYPE);
         const uint32_t adec = pack_ua(t, ut, tx, ty);
@@ -571,6 +608,15 @@ struct Game {
             bool isPA = false;
             if (m) {
                 const int rank = cellRank(m, cand, c);
+#ifdef MRTS_ABLATE
+                if (ab(AB_RANK)) keepv(cellRank(m, cand, launder(c)));
+                if (ab(AB_ACCEPT)) {
+                    int r0 = run0, r1 = run1, ir = 0;
+                    const uint64_t a2 = acceptChain(p, r0, r1, cand, launder(rank), __popcll(m), launder(t), launder(pr),
+                                                    launder(c), launder(adec), true, ir);
+                    keepv(ir + (int)a2 + r0 + r1);
+                }
+#endif
                 MPHASE(23);
                 int irank = 0;
                 const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), t, pr, c, adec, useIx, irank);
@@ -583,6 +629,13 @@ struct Game {
                     ttx = tx;
                     tty = ty;
                     tut = ut;
+#ifdef MRTS_ABLATE
+                    if (ab(AB_LEGAL)) {
+                        int a1 = launder(t), a2 = launder(pr), a3 = launder(tx), a4 = launder(ty), a5 = launder(ut);
+                        legality(l, launder(cu), a1, a2, a3, a4, a5);
+                        keepv(a1 + a2 + a3 + a4 + a5);
+                    }
+#endif
                     legality(l, cu, tt, prm, ttx, tty, tut);
                 }
                 wsync();
@@ -2579,6 +2632,13 @@ struct Game {
         {
             MPHASE(16);
             const MaskTables T = maskTables();
+#ifdef MRTS_ABLATE
+            if (ab(AB_TABLES)) {
+                const MaskTables T2 = maskTables();
+                keepv(T2.attack1 ^ T2.attackFar ^ T2.harvest ^ T2.move ^ T2.resource ^ T2.stockpile ^ T2.aff0 ^ T2.aff1 ^
+                      (uint32_t)T2.prod);
+            }
+#endif
             MPHASE(17);
             const int carried = l < nu ? res[l] : 0;
             if (si >= 0) maskBitsFast(T, cu, carried, w0, w1, w2);
@@ -2590,6 +2650,15 @@ struct Game {
             } else {
                 farAttackBits(far, cu, cu, ballot(l < nu && !(cu & UC_DEAD) && uplay(cu) >= 0), w0, w1, w2);
             }
+#ifdef MRTS_ABLATE
+            if (ab(AB_MASKBITS) && rowB) {
+                uint32_t v0 = 0, v1 = 0, v2 = 0;
+                const uint32_t cu2 = launder(cu);
+                if (si >= 0) maskBitsFast(T, cu2, launder(carried), v0, v1, v2);
+                farAttackRows(far, cu2, rows, v0, v1, v2);
+                keepv(v0 ^ v1 ^ v2);
+            }
+#endif
             MPHASE(19);
         }
         wsync();
@@ -2614,10 +2683,24 @@ struct Game {
         if (si >= 0) {
             const int slot = slot0 + si;
             const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
+#ifdef MRTS_ABLATE
+            if (!ab(AB_SKIP_RECORD))
+#endif
             storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, lo, w2);
+#ifdef MRTS_ABLATE
+            if (ab(AB_RECORD)) storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, launder(lo), launder(w2));
+#endif
             MPHASE(13);
             if (pol) {
                 int32_t a[7];
+#ifdef MRTS_ABLATE
+                if (ab(AB_POLICY)) {
+                    int32_t a2[7];
+                    sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)launder(slot), NT, K,
+                                  launder((lo >> 1) | ((uint64_t)w2 << 63)), launder((uint64_t)(w2 >> 1)), launder(c), a2);
+                    keepv(a2[0] + a2[1] + a2[2] + a2[3] + a2[4] + a2[5] + a2[6]);
+                }
+#endif
                 sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
                               (uint64_t)(w2 >> 1), c, a);
                 int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
@@ -2635,6 +2718,9 @@ struct Game {
             wsync();
             return;
         }
+#ifdef MRTS_ABLATE
+        for (int rep_ = 0; rep_ < (ab(AB_GONE) ? 2 : 1); rep_++)
+#endif
         for (int b0 = 0; b0 < ngone; b0 += 64) {  // rslot holds 64 list entries at a time
             wsync();
             int k = incl - n;
@@ -2717,6 +2803,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     const KStatic& P = *PS;
     Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
            FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius);
+#ifdef MRTS_ABLATE
+    G.G_AB = g_ablate;
+#endif
     // games [0, n_sp_games) are self-play (mrts_create's layout): no load needed to place the slots
     const bool selfplay = FIX ? true : G.g < D.n_sp_games;
     const int slot0 = selfplay ? 2 * G.g : 2 * D.n_sp_games + (G.g - D.n_sp_games);
@@ -2745,6 +2834,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         }
     } else {
         G.load(D.mask_delta && D.masks);
+#ifdef MRTS_ABLATE
+        if (G.ab(AB_LOAD)) G.load(D.mask_delta && D.masks);
+#endif
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
         {
@@ -2859,6 +2951,12 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         PHASE(4);
         bool gameover;
         int winner;
+#ifdef MRTS_ABLATE
+        if (G.ab(AB_OUTCOME)) {
+            G.outcome(gameover, winner);
+            G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner);
+        }
+#endif
         G.outcome(gameover, winner);
         // reward functions + VecClient auto-reset on done[0] or max steps, keeping the terminal
         // reward/done and forcing done[0] (tests/JNIGridnetVecClient.java:214-287)
@@ -2886,7 +2984,13 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
                 G.writeObsPO(slot0 + i, p);
             }
         } else {
+#ifdef MRTS_ABLATE
+            if (!G.ab(AB_SKIP_OBS))
+#endif
             G.writeObsFull(slot0, nslots, side);
+#ifdef MRTS_ABLATE
+            if (G.ab(AB_OBS)) G.writeObsFull(slot0, nslots, side);
+#endif
         }
     }
     PHASE(6);
@@ -2916,6 +3020,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     if (MODE != MODE_MASKS) {
         wsync();
         G.store();
+#ifdef MRTS_ABLATE
+        if (G.ab(AB_STORE)) G.store();
+#endif
     }
     PHASE(10);
 #ifdef MRTS_PHASE_TIMING
@@ -3118,6 +3225,9 @@ __global__ __launch_bounds__(64) void k_policy(PolicyParams Q) {
 }  // namespace
 
 namespace mrts {
+#ifdef MRTS_ABLATE
+hipError_t setAblate(uint32_t v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_ablate), &v, sizeof(v)); }
+#endif
 #ifdef MRTS_PHASE_TIMING
 // out[16]: per-phase sums over games (and the max over games in out[16..31] when given 32 slots)
 hipError_t phaseTimes(unsigned long long* out, int reset) {
