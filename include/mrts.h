@@ -153,6 +153,16 @@ int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_play
 int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                            uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
                            int32_t n_steps, void* stream);
+/* Persistent-buffer observations (default off; always on for the library-owned buffer of the
+ * host-pointer API).  When a call writes observations into the same buffer as this handle's previous
+ * call did, partially observable views re-render only the 4-cell chunks whose cells can have changed
+ * (maps with W % 4 == 0, W <= 32, H <= 32; every unit in one wave) — the buffer ends byte-identical
+ * to a full rewrite, provided nothing else wrote to it in between (Java's clients also hand out
+ * internal arrays that the next call refills or replaces: GameState.java:923-925).
+ * A call without an observation buffer, a restore / state injection / copy, or mrts_obs_invalidate
+ * makes the next write a full one. */
+int mrts_set_obs_delta(mrts_env* env, int32_t on);
+int mrts_obs_invalidate(mrts_env* env);
 /* the next mrts_policy_dev call writes every row */
 int mrts_policy_invalidate(mrts_env* env);
 /* Optional compact output of every mask write: mask slot 0 ("own unit without an action here") as

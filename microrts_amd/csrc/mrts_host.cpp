@@ -84,6 +84,17 @@ static void finishUtt(UttInfo& I) {
     for (int t = 0; t < u.ntypes; t++) maxRange = std::max(maxRange, u.range[t]);
     u.maxAttackRadius = 2 * maxRange + 1;
     u.K = 1 + 6 + 4 + 4 + 4 + 4 + u.ntypes + u.maxAttackRadius * u.maxAttackRadius;
+    for (int t = 0; t < u.ntypes; t++) {  // integer floor(sqrt(r^2 - dy^2)): the cells dx^2 + dy^2 <= r^2
+        const int r = u.sight[t];
+        u.diskLo[t] = u.diskHi[t] = 0;
+        if (r > 15) continue;  // painted with the sqrt form
+        for (int dy = 0; dy <= r; dy++) {
+            int w = 0;
+            while ((w + 1) * (w + 1) + dy * dy <= r * r) w++;
+            if (dy < 8) u.diskLo[t] |= (uint32_t)w << (4 * dy);
+            else u.diskHi[t] |= (uint32_t)w << (4 * (dy - 8));
+        }
+    }
 }
 
 // new UnitTypeTable(version, crs) — reference src/rts/units/UnitTypeTable.java:104-289
@@ -437,6 +448,13 @@ struct mrts_env {
 
     KStatic hstatic;
     KStatic* d_static = nullptr;
+    // persistent-buffer observations (mrts_set_obs_delta; partially observable views): the buffer the
+    // last launch wrote observations to (null after a launch that changed the state without one, or
+    // after an invalidation) and the per-game render records (PO handles on delta-capable maps)
+    int obsDelta = 0;
+    const int32_t* lastObsPtr = nullptr;
+    int32_t* d_poPrev = nullptr;
+    int poWords = 0;
     // delta mask writes: which buffer / player the last mask write went to
     int maskDelta = 0;
     const uint8_t* lastMaskPtr = nullptr;
@@ -463,6 +481,14 @@ struct mrts_env {
         if (((uintptr_t)D.obs & 15) || ((uintptr_t)D.masks & 15)) throw Fail{-EINVAL, "obs / masks buffers must be 16-byte aligned"};
         if (((uintptr_t)D.reward & 7) || ((uintptr_t)D.actions & 3) || ((uintptr_t)D.rows & 3) || ((uintptr_t)D.players & 3))
             throw Fail{-EINVAL, "misaligned buffer"};
+    }
+    // every launch that changes the state or writes observations; the library-owned buffer of the
+    // host-pointer API is always persistent
+    void prepObs(KDyn& D) {
+        D.obs_delta = (D.obs && D.obs == lastObsPtr && (obsDelta || D.obs == d_obs)) ? 1 : 0;
+        D.po_prev = D.obs ? d_poPrev : nullptr;
+        D.po_words = poWords;
+        lastObsPtr = D.obs;
     }
     void prepMasks(KDyn& D) {
         checkAlign(D);
@@ -688,6 +714,11 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         }
         const size_t sw = (size_t)stateWords(env->CAP, env->HW);
         HIPCHK(hipMalloc(&env->d_state, sw * env->nGames * 4));
+        if (env->partialObs && poDeltaShape(env->H, env->W)) {  // PO render records (delta observations)
+            env->poWords = poPrevWords(env->CAP, env->H, env->HW);
+            HIPCHK(hipMalloc(&env->d_poPrev, (size_t)env->poWords * env->nGames * 4));
+            HIPCHK(hipMemset(env->d_poPrev, 0, (size_t)env->poWords * env->nGames * 4));
+        }
         HIPCHK(hipMalloc(&env->d_tmpl, blob.size() * 4));
         HIPCHK(hipMalloc(&env->d_tmplOff, (size_t)env->nGames * 4));
         HIPCHK(hipMalloc(&env->d_gameKind, (size_t)env->nGames * 4));
@@ -769,6 +800,7 @@ int mrts_reset_dev(mrts_env* env, const int32_t* d_players, int32_t* d_obs, doub
         D.masks = d_masks;
         D.mask_player = mask_player;
         env->prepMasks(D);
+        env->prepObs(D);
         env->fusedActions = nullptr;
         HIPCHK(env->launch(1, D, pickStream(env, stream)));
         return 0;
@@ -793,6 +825,7 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
         D.masks = d_masks;
         D.mask_player = mask_player;
         env->prepMasks(D);
+        env->prepObs(D);
         if (d_masks || d_actions == env->fusedActions) env->fusedActions = nullptr;
         HIPCHK(env->launch(0, D, pickStream(env, stream)));
         return 0;
@@ -818,6 +851,7 @@ int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_play
         D.masks = d_masks;
         D.mask_player = mask_player;
         env->prepMasks(D);
+        env->prepObs(D);
         D.pol_actions = d_actions;
         D.pol_seed = seed;
         D.pol_step = next_step;
@@ -871,6 +905,7 @@ int mrts_step_rows_dev(mrts_env* env, const int32_t* d_rows, int32_t n_rows, con
         D.masks = d_masks;
         D.mask_player = mask_player;
         env->prepMasks(D);
+        env->prepObs(D);
         if (d_masks) env->fusedActions = nullptr;
         HIPCHK(env->launch(0, D, pickStream(env, stream)));
         return 0;
@@ -929,6 +964,19 @@ int mrts_policy_invalidate(mrts_env* env) {
     if (!env) return fail(Fail{-EINVAL, "null handle"});
     env->polValid = false;
     env->fusedActions = nullptr;
+    return 0;
+}
+
+int mrts_set_obs_delta(mrts_env* env, int32_t on) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    env->obsDelta = on ? 1 : 0;
+    env->lastObsPtr = nullptr;
+    return 0;
+}
+
+int mrts_obs_invalidate(mrts_env* env) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    env->lastObsPtr = nullptr;
     return 0;
 }
 
@@ -1172,6 +1220,7 @@ void mrts_destroy(mrts_env* env) {
     (void)hipSetDevice(env->device);
     if (env->stream) (void)hipStreamSynchronize(env->stream);
     (void)hipFree(env->d_static);
+    (void)hipFree(env->d_poPrev);
     (void)hipFree(env->d_state);
     (void)hipFree(env->d_polPrev);
     (void)hipFree(env->d_pairs);
@@ -1371,7 +1420,8 @@ int mrts_set_state_json(mrts_env* env, int32_t slot, const char* json) {
         jsonToBlock(env, json, s);
         const size_t sw = s.size();
         HIPCHK(hipMemcpy(env->d_state + (size_t)g * sw, s.data(), sw * 4, hipMemcpyHostToDevice));
-        env->lastMaskPtr = nullptr;  // the next mask write is a full one
+        env->lastMaskPtr = nullptr;  // the next mask and observation writes are full ones
+        env->lastObsPtr = nullptr;
         env->polValid = false;
         env->fusedActions = nullptr;
         return 0;
@@ -1444,6 +1494,7 @@ int mrts_restore(mrts_env* env, const void* buf, int64_t size) {
         HIPCHK(hipDeviceSynchronize());
         HIPCHK(hipMemcpy(env->d_state, (const char*)buf + sizeof(h), (size_t)h.words * h.nGames * 4, hipMemcpyHostToDevice));
         env->lastMaskPtr = nullptr;
+        env->lastObsPtr = nullptr;
         env->polValid = false;
         env->fusedActions = nullptr;
         return 0;
@@ -1469,6 +1520,7 @@ int mrts_copy_games_dev(mrts_env* dst, const mrts_env* src, const int32_t* d_pai
         HIPCHK(hipSetDevice(dst->device));
         HIPCHK(launchCopyGames(dst->d_state, src->d_state, d_pairs, n, dst->nGames, src->nGames, dst->CAP, dst->HW,
                                pickStream(dst, stream)));
+        dst->lastObsPtr = nullptr;
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1504,6 +1556,7 @@ int mrts_copy_games(mrts_env* dst, const mrts_env* src, const int32_t* pairs, in
         HIPCHK(hipMemcpyAsync(dst->d_copyPairs, pairs, (size_t)n * 2 * 4, hipMemcpyHostToDevice, dst->stream));
         HIPCHK(launchCopyGames(dst->d_state, src->d_state, dst->d_copyPairs, n, dst->nGames, src->nGames, dst->CAP,
                                dst->HW, dst->stream));
+        dst->lastObsPtr = nullptr;
         HIPCHK(hipStreamSynchronize(dst->stream));
         return 0;
     } catch (const Fail& f) {
@@ -1520,6 +1573,7 @@ int mrts_playout_dev(mrts_env* env, int32_t horizon, void* stream) {
         std::memset(&D, 0, sizeof(D));
         D.horizon = horizon;
         HIPCHK(env->launch(3, D, pickStream(env, stream)));
+        env->lastObsPtr = nullptr;
         return 0;
     } catch (const Fail& f) {
         return fail(f);

@@ -24,6 +24,9 @@ struct DevUtt {
     int32_t crs;                // move-conflict resolution strategy 1/2/3
     int32_t maxAttackRadius;    // 2 * max attack range + 1 (JNIGridnetClient.java:125)
     int32_t K;                  // mask slots per cell (JNIGridnetClient.java:138)
+    // sight disk half-widths floor(sqrt(r^2 - dy^2)) for r = sight[t] <= 15, 4 bits per |dy|:
+    // dy 0..7 in diskLo, 8..15 in diskHi (PartiallyObservableGameState visibility, painted per row)
+    uint32_t diskLo[MAX_TYPES], diskHi[MAX_TYPES];
 };
 enum : uint32_t { F_RESOURCE = 1, F_STOCKPILE = 2, F_HARVEST = 4, F_MOVE = 8, F_ATTACK = 16,
                   // the type-name tests of the reward functions (src/ai/reward/*.java), set from the names
@@ -119,7 +122,21 @@ struct KDyn {
     int32_t n_rewards, max_steps, C;
     uint32_t reward_need;
     uint32_t reward_kinds4;        // reward_kinds[j] in bits 4j..4j+3
+    // persistent-buffer partially observable observations (mrts_set_obs_delta): obs_delta = 1 when
+    // `obs` holds this handle's last observation write; po_prev = per game [po_words] the previous
+    // render's record (poPrevWords), rewritten by every observation write
+    int32_t obs_delta;
+    int32_t po_words;
+    int32_t* po_prev;
 };
+// PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);
+// snapshot bytes of the unit slots (after the end-of-step compaction); per view p the sight rows
+// (own, other) the render used; per view the 4-cell chunks of rendered units that died (they leave
+// the list before the next render).  Delta rendering needs W % 4 == 0, W <= 32, H <= 32.
+constexpr int poSnapWords(int cap) { return (cap + 3) / 4; }
+constexpr int poChunkWords(int hw) { return (hw / 4 + 31) / 32; }
+constexpr int poPrevWords(int cap, int h, int hw) { return 1 + poSnapWords(cap) + 4 * h + 2 * poChunkWords(hw); }
+constexpr bool poDeltaShape(int h, int w) { return (w & 3) == 0 && w <= 32 && h <= 32; }
 
 struct PolicyParams {
     int32_t HW, K, ntypes, n_slots;

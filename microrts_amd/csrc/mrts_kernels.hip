@@ -72,7 +72,11 @@ enum { AB_LOAD = 0, AB_OBS = 1, AB_STORE = 2, AB_MASKBITS = 3, AB_RECORD = 4, AB
        AB_LEGAL = 7, AB_OUTCOME = 8, AB_INDEX = 9, AB_GONE = 10, AB_TABLES = 11, AB_RANK = 12, AB_DECODE = 13,
        AB_ISSUE = 14, AB_CYCLERANK = 15,
        // skips (outputs nothing in the step reads back): the observation, the mask record stores
-       AB_SKIP_OBS = 16, AB_SKIP_RECORD = 17 };
+       AB_SKIP_OBS = 16, AB_SKIP_RECORD = 17,
+       // PO observation split: everything but the stores (values kept alive) / only the stores (zeros)
+       AB_PO_NOSTORE = 18, AB_PO_ZEROSTORE = 19,
+       // PO observation pieces skipped: sight-disk painting, the last-writer cell map, the render record
+       AB_PO_NOPAINT = 20, AB_PO_NOSCELL = 21, AB_PO_NORECORD = 22, AB_PO_NOSNAPSHOT = 23 };
 #endif
 enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2, GT_PLAYOUT = 3 };  // game_kind & 15
 // per-player counters of this step's issued pairs, as the TraceEntry holds them (after issueSafe's
@@ -293,6 +297,12 @@ struct Game {
     uint32_t* bits;  // running ResourceUsage positions, indices [-W, HW+W)
     uint32_t* scell; // PO: last snapshot unit per cell (slot+1, 0 = none)
     uint32_t* vis;   // PO: 2 x H rows x ceil(W/32) words of sight-disk bitmaps (after scell)
+    // PO delta rendering (poDeltaShape maps only, after vis): the previous render's sight rows [view][2][H]
+    // and dead-unit chunks [view][NCW], this view's dirty chunk bits [NCW] and chunk list [HW / 4]
+    uint32_t* poVis;
+    uint32_t* poPend;
+    uint32_t* poDirty;
+    uint16_t* poList;
     int32_t* rseq;   // ready-list scratch (64)
     uint32_t* mprev; // previous mask row sets, [2][maskWords(HW)] (delta mask writes)
     int32_t* rwc;    // reward counters [player][RC_*] of the pairs issued this step
@@ -321,6 +331,7 @@ struct Game {
     bool ixValid;
     bool anyMP;
     uint32_t lcu, lua;     // load(): lane l's unit core / assignment words (units 0..63) as loaded
+    uint32_t lkey, lsnap;  // PO delta: lane l's hp | resources << 16 as loaded, its previous render's snapshot byte
     uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
     int curP;              // player whose pa is being issued
     // CloserToEnemyBase/Unit: each player's first Base before the step (x | y << 8, -1 = none) and
@@ -352,10 +363,14 @@ struct Game {
         snap = (uint8_t*)q; q += (CAP + 3) & ~3;
         scell = (uint32_t*)q;  // PO only, last: the offsets above do not depend on it
         vis = scell + HW;
+        poVis = vis + 2 * H * ((W + 31) / 32);
+        poPend = poVis + 4 * H;
+        poDirty = poPend + 2 * poChunkWords(HW);
+        poList = (uint16_t*)(poDirty + poChunkWords(HW));
         ixValid = false;
     }
     // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
-    enum { HX_SNAP = 16, HX_BASE = 18, HX_OLDSQ = 20 };
+    enum { HX_SNAP = 16, HX_BASE = 18, HX_OLDSQ = 20, HX_POVALID = 22 };
     DEV int hget(int i) const { return uni(hdr[i]); }
     DEV void hset(int i, int v) const {
         if (lane_id() == 0) hdr[i] = v;
@@ -458,10 +473,30 @@ struct Game {
         for (int a = 0; a < N_ARRAYS; a++) r[a] = arr[a * CAP + l];
         const uint32_t tw = l < TW ? (uint32_t)terr[l] : 0u;
         const uint32_t pv = (wantPrev && l < PW) ? (uint32_t)arr[N_ARRAYS * CAP + l] : 0u;
+        // PO delta: the previous render's record, in the same memory round
+        const bool poRec = po && D.obs_delta && D.po_prev && poDeltaShape(H, W);
+        const int32_t* pr = poRec ? D.po_prev + (size_t)g * D.po_words : nullptr;
+        const int NCW = poChunkWords(HW), SW = poSnapWords(CAP);
+        int32_t prv0 = 0, prsb = 0, prvv = 0, prv2 = 0, prpd = 0;
+        if (poRec) {
+            prv0 = pr[0];
+            prsb = pr[1 + (l >> 2)];
+            prvv = l < 4 * H ? pr[1 + SW + l] : 0;
+            prv2 = l + 64 < 4 * H ? pr[1 + SW + l + 64] : 0;
+            prpd = l < 2 * NCW ? pr[1 + SW + 4 * H + l] : 0;
+        }
         loadHeader(hv);
         MPHASE(20);
         lcu = (uint32_t)r[A_UC];
         lua = (uint32_t)r[A_UA];
+        if (poRec) {
+            lkey = (uint32_t)(uint16_t)r[A_HP] | ((uint32_t)(uint16_t)r[A_RES] << 16);
+            lsnap = ((uint32_t)prsb >> (8 * (l & 3))) & 0xFFu;
+            if (l < 4 * H) poVis[l] = (uint32_t)prvv;
+            if (l + 64 < 4 * H) poVis[l + 64] = (uint32_t)prv2;
+            if (l < 2 * NCW) poPend[l] = (uint32_t)prpd;
+            if (l == 0) hdr[HX_POVALID] = prv0;
+        }
         {
             int32_t* ul = (int32_t*)&U;
             ul[l] = u0;
@@ -1582,14 +1617,21 @@ struct Game {
     // lane = seeing unit, one atomicOr per covered row word; a cell is seen iff its bit is set.
     DEV void paintDisk(uint32_t* rows, uint32_t u) const {
         const int WPR = (W + 31) >> 5;
-        const int sr = U.sight[utyp(u)], x = ux(u), y = uy(u);
+        const int t = utyp(u), sr = U.sight[t], x = ux(u), y = uy(u);
+        const uint32_t dlo = U.diskLo[t], dhi = U.diskHi[t];
         for (int dy = -sr; dy <= sr; dy++) {
             const int yy = y + dy;
             if (yy < 0 || yy >= H) continue;
-            const int lim = sr * sr - dy * dy;
-            int w = (int)__builtin_sqrtf((float)lim);
-            while (w * w > lim) w--;
-            while ((w + 1) * (w + 1) <= lim) w++;
+            const int ady = dy < 0 ? -dy : dy;
+            int w;
+            if (sr <= 15) {  // the table's half-width (host-computed, DevUtt::diskLo/Hi)
+                w = (int)(((ady < 8 ? dlo : dhi) >> (4 * (ady & 7))) & 0xFu);
+            } else {
+                const int lim = sr * sr - dy * dy;
+                w = (int)__builtin_sqrtf((float)lim);
+                while (w * w > lim) w--;
+                while ((w + 1) * (w + 1) <= lim) w++;
+            }
             const int x0 = max(0, x - w), x1 = min(W - 1, x + w);
             for (int k = x0 >> 5; k <= (x1 >> 5); k++) {
                 const int lo = max(x0, 32 * k) - 32 * k, hi = min(x1, 32 * k + 31) - 32 * k;
@@ -1898,10 +1940,11 @@ struct Game {
             const bool alive = o < nu && !(uc[o] & UC_DEAD);
             const uint64_t m = ballot(alive);
             const int idx = base + lanes_below(m);
-            uint32_t c = 0, a = 0;
+            uint32_t c = 0, a = 0, sb = 0;
             int32_t t0 = 0, t1 = 0;
             int16_t h = 0, r = 0, pr = 0;
             if (alive) {
+                if (po) sb = snap[o];
                 c = uc[o];
                 a = ua[o];
                 t0 = at[o];
@@ -1912,6 +1955,7 @@ struct Game {
             }
             wsync();
             if (alive) {
+                if (po) snap[idx] = (uint8_t)sb;
                 uc[idx] = c;
                 ua[idx] = a;
                 at[idx] = t0;
@@ -2104,82 +2148,164 @@ struct Game {
     // PartiallyObservableGameState.getVectorObservation (rts/PartiallyObservableGameState.java:137-209):
     // the snapshot's units (live fields, possibly dead) in list order, last writer per cell; the
     // snapshot's assignments; walls; own / enemy sight disks of the snapshot units (:211-234).
-    DEV void writeObsPO(int slot, int p) {
+    // delta: the buffer holds this game's view-p render of the previous observation write and the PO
+    // record (poVis / poPend / lsnap) describes it.  A cell's planes 0-5 come from the last snapshot
+    // unit on it (its current hp, resources, owner, type and snapshot assignment), planes 6-7 from
+    // the sight rows; so the cells that can differ are: those of units whose membership in the view
+    // or rendered fields changed (before and after — slots keep their index until the compaction),
+    // those of rendered units that died last step (gone from the list: poPend), and the exact XOR
+    // of old and new sight rows.  Only the 4-cell chunks holding them are rendered and stored.
+    DEV void writeObsPO(int slot, int p, bool delta = false) {
+#ifdef MRTS_ABLATE
+        if (!ab(AB_PO_NOSCELL))
+#endif
         for (int c = lane_id(); c < HW; c += 64) scell[c] = 0;
-        wsync();
-        for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
-            if (o < nu && snap_in(snap[o], p)) {
-                const uint32_t cu = uc[o];
-                atomicMax(&scell[uy(cu) * W + ux(cu)], (uint32_t)(o + 1));
-            }
-        }
-        wsync();
-        int32_t* out = D.obs + (size_t)slot * D.C * HW;
-        auto planes = [&](int c, int v[6]) {
-            const int s = (int)scell[c] - 1;
-            v[0] = v[1] = v[2] = v[3] = v[4] = 0;
-            v[5] = cell[c] == WALL ? 1 : 0;
-            if (s >= 0) {
-                const uint32_t cu = uc[s];
-                const int pl = uplay(cu);
-                v[0] = hp[s];
-                v[1] = res[s];
-                v[2] = pl >= 0 ? ((pl + p) % 2) + 1 : 0;
-                v[3] = utyp(cu) + 1;
-                const int sa = snap_act(snap[s], p);
-                v[4] = sa ? sa - 1 : 0;
-            }
-        };
-        const bool vec4 = (HW & 3) == 0;  // lane = 4 consecutive cells, one dwordx4 store per plane
-        if (vec4) {
-            for (int c4 = lane_id(); c4 < HW / 4; c4 += 64) {
-                int v[4][6];
-#pragma unroll
-                for (int j = 0; j < 4; j++) planes(4 * c4 + j, v[j]);
-#pragma unroll
-                for (int k = 0; k < 6; k++)
-                    st4<WT_POOBS>(out + k * HW + 4 * c4, v[0][k], v[1][k], v[2][k], v[3][k]);
-            }
-        } else {
-            for (int c = lane_id(); c < HW; c += 64) {
-                int v[6];
-                planes(c, v);
-#pragma unroll
-                for (int k = 0; k < 6; k++) out[k * HW + c] = v[k];
-            }
-        }
-        // visibility planes over the view's units at their current positions (dead ones included: the
-        // view's list still holds them): own / other player's sight disks
         const int NW = H * ((W + 31) >> 5);
         uint32_t* mineRows = vis;
         uint32_t* theirRows = vis + NW;
         for (int i = lane_id(); i < 2 * NW; i += 64) vis[i] = 0;
         wsync();
-        for (int o = lane_id(); o < nu; o += 64) {
-            const uint32_t cu = uc[o];
-            if (snap_in(snap[o], p) && uplay(cu) >= 0) paintDisk(uplay(cu) == p ? mineRows : theirRows, cu);
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lane_id();
+            if (o < nu && snap_in(snap[o], p)) {
+                const uint32_t cu = uc[o];
+#ifdef MRTS_ABLATE
+                if (!ab(AB_PO_NOSCELL))
+#endif
+                atomicMax(&scell[uy(cu) * W + ux(cu)], (uint32_t)(o + 1));
+                // visibility planes over the view's units at their current positions (dead ones
+                // included: the view's list still holds them): own / other player's sight disks
+#ifdef MRTS_ABLATE
+                if (!ab(AB_PO_NOPAINT))
+#endif
+                if (uplay(cu) >= 0) paintDisk(uplay(cu) == p ? mineRows : theirRows, cu);
+            }
         }
         wsync();
-        if (vec4) {
-            for (int c4 = lane_id(); c4 < HW / 4; c4 += 64) {
-                int m[4], t[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int c = 4 * c4 + j, cx = c % W, cy = c / W;
-                    m[j] = seen(mineRows, cx, cy) ? 1 : 0;
-                    t[j] = seen(theirRows, cx, cy) ? 1 : 0;
+        const int NC = (HW + 3) >> 2, NCW = poChunkWords(HW);
+        int n = NC;  // chunks to render: all, or the dirty list (delta maps have HW % 4 == 0)
+        if (delta) {
+            const int l = lane_id();
+            if (l < NCW) poDirty[l] = poPend[p * NCW + l];
+            wsync();
+            const int nu0 = hget(H_NU);  // the header holds the loaded unit count until store()
+            if (l < nu || l < nu0) {
+                const uint32_t cu = l < nu ? uc[l] : 0u;
+                const uint32_t sb = l < nu ? (uint32_t)snap[l] : 0u;
+                const bool inC = l < nu && snap_in(sb, p), inP = l < nu0 && ((lsnap >> p) & 1u);
+                const int cc = uy(cu) * W + ux(cu), cp = uy(lcu) * W + ux(lcu);
+                bool chg = inC != inP;
+                if (inC && inP) {
+                    const uint32_t key = (uint32_t)(uint16_t)hp[l] | ((uint32_t)(uint16_t)res[l] << 16);
+                    chg = cc != cp || key != lkey || snap_act(sb, p) != (int)((lsnap >> (2 + 3 * p)) & 7u);
                 }
-                st4<WT_POOBS>(out + 6 * HW + 4 * c4, m[0], m[1], m[2], m[3]);
-                st4<WT_POOBS>(out + 7 * HW + 4 * c4, t[0], t[1], t[2], t[3]);
+                if (chg && inP) atomicOr(&poDirty[cp >> 7], 1u << ((cp >> 2) & 31));
+                if (chg && inC) atomicOr(&poDirty[cc >> 7], 1u << ((cc >> 2) & 31));
             }
-        } else {
-            for (int c = lane_id(); c < HW; c += 64) {
-                const int cx = c % W, cy = c / W;
-                out[6 * HW + c] = seen(mineRows, cx, cy) ? 1 : 0;
-                out[7 * HW + c] = seen(theirRows, cx, cy) ? 1 : 0;
+            // sight rows (W <= 32: one word per row): changed columns -> chunk bits of that row
+            for (int i = l; i < 2 * H; i += 64) {
+                const uint32_t d = vis[i] ^ poVis[p * 2 * H + i];
+                if (d) {
+                    const int y = i < H ? i : i - H;
+                    uint32_t g = 0;  // bit j = column group 4j..4j+3 changed
+#pragma unroll
+                    for (int j = 0; j < 8; j++) g |= ((d >> (4 * j)) & 0xFu) ? (1u << j) : 0u;
+                    const int k0 = y * (W >> 2);  // first chunk of row y (W/4 chunks per row, <= 8)
+                    if ((k0 & 31) + (W >> 2) <= 32) {
+                        atomicOr(&poDirty[k0 >> 5], g << (k0 & 31));
+                    } else {
+                        for (uint32_t gg = g; gg; gg &= gg - 1) {
+                            const int k = k0 + __builtin_ctz(gg);
+                            atomicOr(&poDirty[k >> 5], 1u << (k & 31));
+                        }
+                    }
+                }
+            }
+            wsync();
+            n = 0;
+            for (int c0 = 0; c0 < NC; c0 += 64) {
+                const int k = c0 + l;
+                const bool dk = k < NC && ((poDirty[k >> 5] >> (k & 31)) & 1u);
+                const uint64_t m = ballot(dk);
+                if (dk) poList[n + lanes_below(m)] = (uint16_t)k;
+                n += __popcll(m);
+            }
+            wsync();
+        }
+        int32_t* out = D.obs + (size_t)slot * D.C * HW;
+        for (int it = lane_id(); it < n; it += 64) {
+            const int c4 = delta ? (int)poList[it] : it;  // lane = 4 consecutive cells, dwordx4 per plane
+            int sc[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) sc[j] = 4 * c4 + j < HW ? (int)scell[4 * c4 + j] - 1 : -1;
+            uint32_t cu[4];
+            int ch[4], cr[4], ca[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {  // branch-free: an empty cell reads slot 0 and is masked
+                const int s = sc[j] >= 0 ? sc[j] : 0;
+                cu[j] = uc[s];
+                ch[j] = hp[s];
+                cr[j] = res[s];
+                ca[j] = snap_act(snap[s], p);
+            }
+            const int cy = (4 * c4) / W, cx0 = (4 * c4) % W;  // W % 4 == 0 here, or one cell per lane below
+            int v[4][8];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool occ = sc[j] >= 0;
+                const int pl = uplay(cu[j]);
+                v[j][0] = occ ? ch[j] : 0;
+                v[j][1] = occ ? cr[j] : 0;
+                v[j][2] = (occ && pl >= 0) ? ((pl + p) % 2) + 1 : 0;
+                v[j][3] = occ ? utyp(cu[j]) + 1 : 0;
+                v[j][4] = (occ && ca[j]) ? ca[j] - 1 : 0;
+                const bool in = 4 * c4 + j < HW;
+                v[j][5] = in && cell[4 * c4 + j] == WALL ? 1 : 0;
+                const int x = (W & 3) == 0 ? cx0 + j : (4 * c4 + j) % W, y = (W & 3) == 0 ? cy : (4 * c4 + j) / W;
+                v[j][6] = in && seen(mineRows, x, y) ? 1 : 0;
+                v[j][7] = in && seen(theirRows, x, y) ? 1 : 0;
+            }
+            if ((HW & 3) == 0) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) st4<WT_POOBS>(out + k * HW + 4 * c4, v[0][k], v[1][k], v[2][k], v[3][k]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (4 * c4 + j < HW)
+#pragma unroll
+                        for (int k = 0; k < 8; k++) out[k * HW + 4 * c4 + j] = v[j][k];
             }
         }
+#ifdef MRTS_ABLATE
+        if (!ab(AB_PO_NORECORD))
+#endif
+        if (D.po_prev && poDeltaShape(H, W)) poRecord(p);
+    }
+    // the PO record of view p for the next write: this render's sight rows and the chunks of its units
+    // that died (the compaction removes them before the next render)
+    DEV void poRecord(int p) {
+        const int l = lane_id(), NCW = poChunkWords(HW), SW = poSnapWords(CAP);
+        int32_t* pr = D.po_prev + (size_t)g * D.po_words;
+        for (int i = l; i < 2 * H; i += 64) pr[1 + SW + p * 2 * H + i] = (int32_t)vis[i];
+        if (l < NCW) poDirty[l] = 0;
+        wsync();
+        for (int o = l; o < nu; o += 64) {
+            const uint32_t cu = uc[o];
+            if ((cu & UC_DEAD) && snap_in(snap[o], p)) {
+                const int c = uy(cu) * W + ux(cu);
+                atomicOr(&poDirty[c >> 7], 1u << ((c >> 2) & 31));
+            }
+        }
+        wsync();
+        if (l < NCW) pr[1 + SW + 4 * H + p * NCW + l] = (int32_t)poDirty[l];
+        wsync();
+    }
+    // after the compaction: the snapshot bytes of the final slots and the views this launch rendered
+    DEV void poRecordSnaps(uint32_t views) {
+        int32_t* pr = D.po_prev + (size_t)g * D.po_words;
+        const uint32_t* sw = (const uint32_t*)snap;
+        for (int w = lane_id(); w < (nu + 3) / 4; w += 64) pr[1 + w] = (int32_t)sw[w];
+        if (lane_id() == 0) pr[0] = (int32_t)views;
     }
 
     // ------------------------------------------------------------------ legal-action masks
@@ -2978,10 +3104,18 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     const bool external = gtype != GT_BOT_VS_BOT;  // bot-only clients return no observation / masks
     if (MODE != MODE_MASKS && D.obs && external) {
         if (G.po) {
+            // persistent buffer: the views the previous write rendered for this game can be updated
+            // in place (writeObsPO's delta)
+            const bool canDelta = MODE == MODE_STEP && !freshObs && D.obs_delta && D.po_prev && poDeltaShape(G.H, G.W) &&
+                                  G.nu <= 64 && G.hget(H_NU) <= 64;
+            const uint32_t valid = canDelta ? (uint32_t)G.hget(Game::HX_POVALID) : 0u;
             for (int i = 0; i < nslots; i++) {
                 const int p = selfplay ? i : side;
                 if (freshObs) G.snapshot(p);  // PO view of the reset state
-                G.writeObsPO(slot0 + i, p);
+#ifdef MRTS_ABLATE
+                if (!G.ab(AB_SKIP_OBS))
+#endif
+                G.writeObsPO(slot0 + i, p, ((valid >> p) & 1u) != 0);
             }
         } else {
 #ifdef MRTS_ABLATE
@@ -3019,6 +3153,8 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     }
     if (MODE != MODE_MASKS) {
         wsync();
+        if (G.po && D.obs && external && D.po_prev && poDeltaShape(G.H, G.W))
+            G.poRecordSnaps(selfplay ? 3u : (1u << side));
         G.store();
 #ifdef MRTS_ABLATE
         if (G.ab(AB_STORE)) G.store();
@@ -3264,6 +3400,7 @@ hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts, [n] ends
 size_t ldsBytes(int HW, int W, int CAP, int po) {
     return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 + 128 +
            (po ? 4 * (size_t)HW + 8 * (size_t)(HW / W) * (size_t)((W + 31) / 32) : 0) +
+           (po && poDeltaShape(HW / W, W) ? 4 * (4 * (size_t)(HW / W) + 3 * (size_t)poChunkWords(HW)) + 2 * (size_t)((HW / 4 + 1) & ~1) : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (((size_t)CAP + 3) & ~(size_t)3);
 }
 // MicroRTS-Py GridnetVecEnv observation encoding (gym_microrts `_encode_obs`: clip each plane to

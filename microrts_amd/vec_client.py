@@ -333,13 +333,16 @@ class DeviceVecEnv:
 
     def __init__(self, num_selfplay_slots, num_bot_envs, max_steps, map_paths, ai2s=None, utt=None, partial_obs=False,
                  device=0, seed=0, slot_id_base=0, with_masks=True, ai1s=None, mask_delta=True, source_bits=True,
-                 rfs=None, max_units=0):
+                 rfs=None, max_units=0, obs_delta=True):
         """ai2s / ai1s: the bot of each bot env (names or objects named like the Java classes); a missing
         or short list is padded with PassiveAI (the JNIGridnetVecClient mirror raises instead, like
         Java).  mask_delta: `masks` is owned by this object and reused every call, so only changed rows are
         rewritten (the tensor must not be written by the caller).  source_bits: also keep mask slot 0
         as bits in `source` ([slots][ceil(H*W/32)] int32), which random_policy uses.  rfs: reward
-        function names (a_rfs); reward / done are [S] for one function, [S][R] otherwise."""
+        function names (a_rfs); reward / done are [S] for one function, [S][R] otherwise.  obs_delta:
+        `obs` is persistent too (mrts_set_obs_delta: partially observable views re-render only the chunks
+        that can have changed); an in-place torch write to `obs` (its version counter moves) makes the
+        next write a full one."""
         import torch
 
         if not torch.cuda.is_available():
@@ -366,6 +369,8 @@ class DeviceVecEnv:
             _lib.check(h.L.mrts_set_source_output(h.h, self._p(self.source)))
         self.mask_player = 0
         self._policy_out, self._policy_version = None, -1
+        _lib.check(h.L.mrts_set_obs_delta(h.h, int(bool(obs_delta))))
+        self._obs_version = -1
         torch.cuda.synchronize(dev)
 
     @staticmethod
@@ -376,16 +381,28 @@ class DeviceVecEnv:
         s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
         return ctypes.c_void_p(s.cuda_stream)
 
+    def _obs_guard(self):
+        """Before a call that writes `obs`: a torch in-place write since our last one voids the delta base."""
+        if self.obs._version != self._obs_version:
+            _lib.check(self._h.L.mrts_obs_invalidate(self._h.h))
+
+    def _obs_written(self):
+        self._obs_version = self.obs._version
+
     def reset(self, stream=None):
         h = self._h
+        self._obs_guard()
         _lib.check(h.L.mrts_reset_dev(h.h, self._p(self.players), self._p(self.obs), self._p(self.reward),
                                       self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
+        self._obs_written()
 
     def step(self, actions=None, stream=None):
         h = self._h
         a = self.actions if actions is None else actions
+        self._obs_guard()
         _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self.reward),
                                      self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
+        self._obs_written()
 
     def step_fused(self, seed, next_step, stream=None):
         """step() on env.actions, then env.actions := random_policy(seed, next_step) from the masks this
@@ -394,9 +411,11 @@ class DeviceVecEnv:
         assert self.masks is not None, "the fused policy samples from the masks"
         if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
             _lib.check(h.L.mrts_policy_invalidate(h.h))  # written by someone else since
+        self._obs_guard()
         _lib.check(h.L.mrts_step_fused_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
                                            self._p(self.reward), self._p(self.done), self._p(self.masks), self.mask_player,
                                            seed, next_step, self._s(stream)))
+        self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
     def rollout_fused(self, seed, first_next_step, n_steps, stream=None):
@@ -406,9 +425,11 @@ class DeviceVecEnv:
         assert self.masks is not None, "the fused policy samples from the masks"
         if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
             _lib.check(h.L.mrts_policy_invalidate(h.h))
+        self._obs_guard()
         _lib.check(h.L.mrts_rollout_fused_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
                                               self._p(self.reward), self._p(self.done), self._p(self.masks),
                                               self.mask_player, seed, first_next_step, n_steps, self._s(stream)))
+        self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
     def step_rows(self, rows, stream=None):
@@ -416,10 +437,12 @@ class DeviceVecEnv:
         h = self._h
         assert rows.dtype == self.torch.int32 and rows.is_contiguous() and rows.dim() == 3 and rows.shape[2] == 8
         assert rows.shape[0] == h.S and rows.device == self.device
+        self._obs_guard()
         _lib.check(h.L.mrts_step_rows_dev(h.h, self._p(rows), rows.shape[1], self._p(self.players), self._p(self.obs),
                                           self._p(self.reward), self._p(self.done),
                                           self._p(self.masks) if self.masks is not None else None, self.mask_player,
                                           self._s(stream)))
+        self._obs_written()
 
     def onehot_obs(self, obs=None, out=None, stream=None):
         """MicroRTS-Py's encoding of the observation (gym_microrts `_encode_obs`: clip + one-hot,

@@ -620,3 +620,69 @@ def test_native_rollout_matches_fused_steps(mp, n_sp):
     A.close()
     B.close()
     del torch
+
+
+@pytest.mark.parametrize("mp,n_sp,n_bot,rows,max_units", [
+    ("maps/BWDistantResources32x32.xml", 8, 4, False, 256),
+    ("maps/16x16/basesWorkers16x16.xml", 16, 4, False, 0),
+    ("maps/8x8/basesWorkers8x8.xml", 8, 4, True, 0),          # Java rows (shuffled, duplicates)
+    ("maps/24x24/basesWorkers24x24.xml", 8, 2, False, 0),
+    ("maps/10x10/basesWorkers10x10.xml", 8, 2, False, 0),     # W % 4 != 0: always full renders
+])
+def test_po_obs_delta_matches_full(mp, n_sp, n_bot, rows, max_units):
+    """Persistent-buffer partially observable observations (only the 4-cell chunks whose cells can have
+    changed are re-rendered: units whose view membership or rendered fields changed, units that died
+    in the last render, the XOR of old and new sight rows) stay byte-identical to full renders after
+    every step: self-play and agent-vs-RandomBiasedAI games (the agent's side flips every 7 steps),
+    auto-resets (max_steps 120), a caller's in-place edit of env.obs, a checkpoint restore and a
+    GameState.fromJSON injection."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    S = n_sp + n_bot
+    maps = [mp] * S
+    bots = ["RandomBiasedAI"] * n_bot if n_bot else None
+    mk = lambda d: DeviceVecEnv(n_sp, n_bot, 120, maps, seed=8, ai2s=bots, partial_obs=True, obs_delta=d,  # noqa: E731
+                                max_units=max_units)
+    a, b = mk(True), mk(False)
+    a.reset()
+    b.reset()
+    rng = np.random.default_rng(6)
+    ck = None
+    for step in range(320):
+        if n_bot and step % 7 == 3:
+            side = torch.tensor([(step // 7) % 2] * S, dtype=torch.int32, device=a.device)
+            a.players.copy_(side)
+            b.players.copy_(side)
+        a.random_policy(SEED, step)
+        b.random_policy(SEED, step)
+        if rows:
+            r = torch.as_tensor(_java_rows(rng, a.actions.cpu().numpy(), "shuffled_dups"), device=a.device)
+            a.step_rows(r)
+            b.step_rows(r)
+        else:
+            a.step()
+            b.step()
+        if step == 60:
+            a.obs[1, 6, 0, 0] += 3  # caller writes the buffer: the next write must be a full one
+        if step == 80:
+            ck = (a.checkpoint(), b.checkpoint())
+        if step == 150:
+            a.restore(ck[0])
+            b.restore(ck[1])
+            a.get_masks()
+            b.get_masks()
+        if step == 200:
+            j = b.state_json(2)
+            a.set_state_json(2, j)
+            b.set_state_json(2, j)
+            a.get_masks()
+            b.get_masks()
+        if step in (60, 150, 200):
+            continue  # the buffers differ / are stale until the next step
+        a.synchronize()
+        b.synchronize()
+        assert torch.equal(a.obs, b.obs), f"delta PO observations differ after step {step}"
+    assert not a.error_flags().any()
+    a.close()
+    b.close()

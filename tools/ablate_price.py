@@ -21,7 +21,9 @@ L.mrts_set_ablate.argtypes = [ctypes.c_uint]
 from microrts_amd import DeviceVecEnv  # noqa: E402
 
 NAMES = ["load", "obs", "store", "maskbits", "record", "policy", "accept", "legality", "outcome+rewards", "index",
-         "gone", "tables", "rank", "decode", "(issue)", "(cyclerank)", "SKIP obs", "SKIP records"]
+         "gone", "tables", "rank", "decode", "(issue)", "(cyclerank)", "SKIP obs", "SKIP records",
+         "PO obs without stores", "PO obs stores of zeros only", "SKIP PO disk painting", "SKIP PO cell map",
+         "SKIP PO render record", "(snapshot)"]
 SEED = 0x5EEDC0DE
 
 
@@ -32,7 +34,9 @@ def main():
     MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
     burn = int(os.environ.get("BURNIN", 1000))
     K = 100
-    env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=SEED)
+    PO = os.environ.get("PO", "0") == "1"
+    env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=SEED, partial_obs=PO,
+                       max_units=int(os.environ.get("MAXU", 0)))
     env.reset()
     env.random_policy(SEED, 0)
     env.rollout_fused(SEED, 1, burn)
