@@ -84,8 +84,10 @@ static void finishUtt(UttInfo& I) {
     for (int t = 0; t < u.ntypes; t++) maxRange = std::max(maxRange, u.range[t]);
     u.maxAttackRadius = 2 * maxRange + 1;
     u.K = 1 + 6 + 4 + 4 + 4 + 4 + u.ntypes + u.maxAttackRadius * u.maxAttackRadius;
+    u.maxSight = 0;
     for (int t = 0; t < u.ntypes; t++) {  // integer floor(sqrt(r^2 - dy^2)): the cells dx^2 + dy^2 <= r^2
         const int r = u.sight[t];
+        u.maxSight = std::max(u.maxSight, r);
         u.diskLo[t] = u.diskHi[t] = 0;
         if (r > 15) continue;  // painted with the sqrt form
         for (int dy = 0; dy <= r; dy++) {

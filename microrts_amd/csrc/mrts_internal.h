@@ -27,6 +27,7 @@ struct DevUtt {
     // sight disk half-widths floor(sqrt(r^2 - dy^2)) for r = sight[t] <= 15, 4 bits per |dy|:
     // dy 0..7 in diskLo, 8..15 in diskHi (PartiallyObservableGameState visibility, painted per row)
     uint32_t diskLo[MAX_TYPES], diskHi[MAX_TYPES];
+    int32_t maxSight;           // max sight[t] over the types
 };
 enum : uint32_t { F_RESOURCE = 1, F_STOCKPILE = 2, F_HARVEST = 4, F_MOVE = 8, F_ATTACK = 16,
                   // the type-name tests of the reward functions (src/ai/reward/*.java), set from the names

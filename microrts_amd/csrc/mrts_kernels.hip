@@ -366,7 +366,7 @@ struct Game {
         poVis = vis + 2 * H * ((W + 31) / 32);
         poPend = poVis + 4 * H;
         poDirty = poPend + 2 * poChunkWords(HW);
-        poList = (uint16_t*)(poDirty + poChunkWords(HW));
+        poList = (uint16_t*)(poDirty + 2 * poChunkWords(HW));  // poDirty: dirty + next pending bits
         ixValid = false;
     }
     // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
@@ -1640,6 +1640,20 @@ struct Game {
             }
         }
     }
+    // paintDisk for every lane with `act` at once, maps with W <= 32 (one row word) and sight <= 15:
+    // a uniform loop over dy up to the table's largest sight, one predicated atomicOr per row
+    DEV void paintDisks(bool act, uint32_t u, uint32_t* rows) const {
+        const int t = utyp(u), x = ux(u), y = uy(u);
+        const int sr = act ? U.sight[t] : -1, SM = U.maxSight;
+        const uint32_t dlo = act ? U.diskLo[t] : 0u, dhi = act ? U.diskHi[t] : 0u;
+        for (int dy = -SM; dy <= SM; dy++) {
+            const int yy = y + dy, ady = dy < 0 ? -dy : dy;
+            const int w = (int)(((ady < 8 ? dlo : dhi) >> (4 * (ady & 7))) & 0xFu);
+            const int x0 = max(0, x - w), x1 = min(W - 1, x + w);
+            const uint32_t b = ((2u << (x1 - x0)) - 1u) << x0;  // columns x0..x1 (x1 - x0 = 31: 2u << 31 wraps to 0)
+            if (ady <= sr && yy >= 0 && yy < H) atomicOr(&rows[yy], b);
+        }
+    }
     DEV bool seen(const uint32_t* rows, int x, int y) const {
         const int WPR = (W + 31) >> 5;
         return (rows[y * WPR + (x >> 5)] >> (x & 31)) & 1u;
@@ -2155,7 +2169,160 @@ struct Game {
     // or rendered fields changed (before and after — slots keep their index until the compaction),
     // those of rendered units that died last step (gone from the list: poPend), and the exact XOR
     // of old and new sight rows.  Only the 4-cell chunks holding them are rendered and stored.
+    // writeObsPO for maps with W % 4 == 0, W <= 32 (one word per sight row), H <= 32, sight <= 15
+    // and every unit in one wave (lane = slot).  One unit pass paints the sight disks, marks the
+    // chunks of changed units (delta) and of the view's dead units (the next record's pending
+    // chunks).  A cell's last snapshot writer (list order) is the later of its live occupant (cell
+    // map), when that unit is in the view, and the view's dead units on it (a register list: few),
+    // so no per-cell scratch map is built.  Same output as the general form below.
+    DEV void writeObsPOFast(int slot, int p, bool delta) {
+        const int l = lane_id(), NCW = poChunkWords(HW), NC = HW >> 2;
+        uint32_t* mineRows = vis;
+        uint32_t* theirRows = vis + H;
+        uint32_t* dirty = poDirty;
+        uint32_t* nextPend = poDirty + NCW;
+        int32_t* pr = D.po_prev ? D.po_prev + (size_t)g * D.po_words : nullptr;
+        const int SW = poSnapWords(CAP);
+        const int nu0 = delta ? hget(H_NU) : 0;  // the header holds the loaded unit count until store()
+        if (l < 2 * H) vis[l] = 0;
+        if (l < NCW) {
+            dirty[l] = delta ? poPend[p * NCW + l] : 0u;
+            nextPend[l] = 0u;
+        }
+        const bool live = l < nu;
+        uint32_t cu = 0, sb = 0;
+        int hv = 0, rv = 0;
+        if (live) {
+            cu = uc[l];
+            sb = snap[l];
+            hv = hp[l];
+            rv = res[l];
+        }
+        const bool in = live && snap_in(sb, p);
+        const bool dead = in && (cu & UC_DEAD);
+        const int cc = uy(cu) * W + ux(cu);
+        wsync();
+        // visibility planes over the view's units at their current positions (dead ones included:
+        // the view's list still holds them): own / other player's sight disks
+        const bool painter = in && uplay(cu) >= 0;
+#ifdef MRTS_ABLATE
+        if (!ab(AB_PO_NOPAINT))
+#endif
+        if (ballot(painter)) paintDisks(painter, cu, uplay(cu) == p ? mineRows : theirRows);
+        const uint64_t deadM = ballot(dead);
+        if (pr && dead) atomicOr(&nextPend[cc >> 7], 1u << ((cc >> 2) & 31));
+        if (delta && (live || l < nu0)) {
+            const bool inP = l < nu0 && ((lsnap >> p) & 1u);
+            const int cp = uy(lcu) * W + ux(lcu);
+            bool chg = in != inP;
+            if (in && inP) {
+                const uint32_t key = (uint32_t)(uint16_t)hv | ((uint32_t)(uint16_t)rv << 16);
+                chg = cc != cp || key != lkey || snap_act(sb, p) != (int)((lsnap >> (2 + 3 * p)) & 7u);
+            }
+            if (chg && inP) atomicOr(&dirty[cp >> 7], 1u << ((cp >> 2) & 31));
+            if (chg && in) atomicOr(&dirty[cc >> 7], 1u << ((cc >> 2) & 31));
+        }
+        wsync();
+        if (l < 2 * H) {  // sight rows: changed columns -> chunk bits of that row; the record's copy
+            const uint32_t row = vis[l];
+            if (delta) {
+                const uint32_t d = row ^ poVis[p * 2 * H + l];
+                if (d) {
+                    const int y = l < H ? l : l - H;
+                    uint32_t gbits = 0;  // bit j = column group 4j..4j+3 changed
+#pragma unroll
+                    for (int j = 0; j < 8; j++) gbits |= ((d >> (4 * j)) & 0xFu) ? (1u << j) : 0u;
+                    const int k0 = y * (W >> 2);
+                    if ((k0 & 31) + (W >> 2) <= 32) {
+                        atomicOr(&dirty[k0 >> 5], gbits << (k0 & 31));
+                    } else {
+                        for (uint32_t gg = gbits; gg; gg &= gg - 1) {
+                            const int k = k0 + __builtin_ctz(gg);
+                            atomicOr(&dirty[k >> 5], 1u << (k & 31));
+                        }
+                    }
+                }
+            }
+            if (pr) pr[1 + SW + p * 2 * H + l] = (int32_t)row;
+        }
+        wsync();
+        int n = NC;  // chunks to render: all, or the dirty list
+        if (delta) {
+            n = 0;
+#pragma unroll
+            for (int c0 = 0; c0 < 256; c0 += 64) {  // NC <= 256 (H, W <= 32)
+                if (c0 < NC) {
+                    const int k = c0 + l;
+                    const bool dk = k < NC && ((dirty[k >> 5] >> (k & 31)) & 1u);
+                    const uint64_t m = ballot(dk);
+                    if (dk) poList[n + lanes_below(m)] = (uint16_t)k;
+                    n += __popcll(m);
+                }
+            }
+        }
+        if (pr && l < NCW) pr[1 + SW + 4 * H + p * NCW + l] = (int32_t)nextPend[l];
+        wsync();
+        int32_t* out = D.obs + (size_t)slot * D.C * HW;
+        for (int it = l; it < n; it += 64) {
+            const int c4 = delta ? (int)poList[it] : it;  // lane = 4 consecutive cells of one row
+            const int y = (4 * c4) / W, x0 = (4 * c4) % W;
+            int cs[4], sl[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) cs[j] = cell[4 * c4 + j];
+            const uint32_t mr = mineRows[y], tr = theirRows[y];
+            uint32_t ocu[4], osb[4];
+            int ohp[4], ors[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {  // the live occupant's fields (an empty cell reads slot 0, masked)
+                const int s = cs[j] < CAP ? cs[j] : 0;
+                ocu[j] = uc[s];
+                osb[j] = snap[s];
+                ohp[j] = hp[s];
+                ors[j] = res[s];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) sl[j] = (cs[j] < CAP && snap_in(osb[j], p)) ? cs[j] : -1;
+            for (uint64_t m = deadM; m; m &= m - 1) {  // the view's dead units: a later list position wins
+                const int ds = __builtin_ctzll(m);
+                const uint32_t dcu = uniu((uint32_t)rl((int)cu, ds));
+                const int dcell = uy(dcu) * W + ux(dcu);
+                const int dh = rl(hv, ds), dr = rl(rv, ds);
+                const uint32_t dsb = uniu((uint32_t)rl((int)sb, ds));
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (dcell == 4 * c4 + j && ds > sl[j]) {
+                        sl[j] = ds;
+                        ocu[j] = dcu;
+                        osb[j] = dsb;
+                        ohp[j] = dh;
+                        ors[j] = dr;
+                    }
+            }
+            int v[4][8];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool occ = sl[j] >= 0;
+                const int pl = uplay(ocu[j]);
+                const int sa = snap_act(osb[j], p);
+                v[j][0] = occ ? ohp[j] : 0;
+                v[j][1] = occ ? ors[j] : 0;
+                v[j][2] = (occ && pl >= 0) ? ((pl + p) % 2) + 1 : 0;
+                v[j][3] = occ ? utyp(ocu[j]) + 1 : 0;
+                v[j][4] = (occ && sa) ? sa - 1 : 0;
+                v[j][5] = cs[j] == WALL ? 1 : 0;
+                v[j][6] = (int)((mr >> (x0 + j)) & 1u);
+                v[j][7] = (int)((tr >> (x0 + j)) & 1u);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) st4<WT_POOBS>(out + k * HW + 4 * c4, v[0][k], v[1][k], v[2][k], v[3][k]);
+        }
+        wsync();
+    }
     DEV void writeObsPO(int slot, int p, bool delta = false) {
+        if ((W & 3) == 0 && W <= 32 && H <= 32 && nu <= 64 && U.maxSight <= 15) {
+            writeObsPOFast(slot, p, delta);
+            return;
+        }
 #ifdef MRTS_ABLATE
         if (!ab(AB_PO_NOSCELL))
 #endif
@@ -2165,20 +2332,29 @@ struct Game {
         uint32_t* theirRows = vis + NW;
         for (int i = lane_id(); i < 2 * NW; i += 64) vis[i] = 0;
         wsync();
+        const bool fastPaint = W <= 32 && U.maxSight <= 15;
         for (int o0 = 0; o0 < nu; o0 += 64) {
             const int o = o0 + lane_id();
-            if (o < nu && snap_in(snap[o], p)) {
-                const uint32_t cu = uc[o];
+            const bool in = o < nu && snap_in(snap[o], p);
+            const uint32_t cu = in ? uc[o] : 0u;
+            if (in) {
 #ifdef MRTS_ABLATE
                 if (!ab(AB_PO_NOSCELL))
 #endif
                 atomicMax(&scell[uy(cu) * W + ux(cu)], (uint32_t)(o + 1));
-                // visibility planes over the view's units at their current positions (dead ones
-                // included: the view's list still holds them): own / other player's sight disks
+            }
+            // visibility planes over the view's units at their current positions (dead ones
+            // included: the view's list still holds them): own / other player's sight disks
 #ifdef MRTS_ABLATE
-                if (!ab(AB_PO_NOPAINT))
+            if (!ab(AB_PO_NOPAINT))
 #endif
-                if (uplay(cu) >= 0) paintDisk(uplay(cu) == p ? mineRows : theirRows, cu);
+            {
+                const bool painter = in && uplay(cu) >= 0;
+                if (fastPaint) {
+                    if (ballot(painter)) paintDisks(painter, cu, uplay(cu) == p ? mineRows : theirRows);
+                } else if (painter) {
+                    paintDisk(uplay(cu) == p ? mineRows : theirRows, cu);
+                }
             }
         }
         wsync();
@@ -3400,7 +3576,7 @@ hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts, [n] ends
 size_t ldsBytes(int HW, int W, int CAP, int po) {
     return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 + 128 +
            (po ? 4 * (size_t)HW + 8 * (size_t)(HW / W) * (size_t)((W + 31) / 32) : 0) +
-           (po && poDeltaShape(HW / W, W) ? 4 * (4 * (size_t)(HW / W) + 3 * (size_t)poChunkWords(HW)) + 2 * (size_t)((HW / 4 + 1) & ~1) : 0) +
+           (po && poDeltaShape(HW / W, W) ? 4 * (4 * (size_t)(HW / W) + 4 * (size_t)poChunkWords(HW)) + 2 * (size_t)((HW / 4 + 1) & ~1) : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (((size_t)CAP + 3) & ~(size_t)3);
 }
 // MicroRTS-Py GridnetVecEnv observation encoding (gym_microrts `_encode_obs`: clip each plane to
