@@ -314,18 +314,28 @@ def main():
     HW = H * W
     MWB = 4 * ((HW + 31) // 32)
     dirty = rows
+    # partially observable views under the persistent-buffer contract (DeviceVecEnv obs_delta): only
+    # the (plane, 4-cell chunk) pieces that changed must be written — measured on the probe steps
+    po_delta = a.po and (HW % 4) == 0 and W <= 32 and H <= 32
+    obs_chunks = float(C * HW // 4)
     if env.source is not None and a.mask_mode == "delta":
         lut = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int64, device=env.device)
-        tot, n_probe = 0, 5
+        tot, otot, n_probe = 0, 0, 5
         for k in range(n_probe):  # untimed probe steps after the timed window
             before = env.source.clone()
+            obefore = env.obs.clone() if po_delta else None
             one_step(base + a.steps + k)  # after the timed (and kernel-timing) windows
             env.synchronize()
             tot += int(lut[(before | env.source).view(torch.uint8).long()].sum().item())
+            if po_delta:
+                otot += int((obefore != env.obs).view(S, C, HW // 4, 4).any(-1).sum().item())
         dirty = tot / (n_probe * S)
+        if po_delta:
+            obs_chunks = otot / (n_probe * S)
     n_games = S // 2
     m_bytes = dirty * K if a.mask_mode == "delta" else HW * K
-    contract = S * (rows * 28 + C * HW * 4 + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
+    o_bytes = obs_chunks * 16  # C * HW * 4 for a full write
+    contract = S * (rows * 28 + o_bytes + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
     if fused:  # the policy's action rows leave the step kernel too
         contract += S * (dirty if a.mask_mode == "delta" else HW) * 28
     survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16))
@@ -390,7 +400,9 @@ def main():
             "kernel": "k_env<MODE_STEP>" + (" + fused policy rows" if fused else ""),
             "alg_bytes_per_launch": contract,
             "alg_bytes_note": f"step contract bytes, {a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "
-                              f"changed mask rows per slot (DESIGN.md §5)",
+                              f"changed mask rows per slot" + (f", {obs_chunks:.1f} changed (plane, 4-cell chunk) "
+                              f"observation pieces per slot (persistent PO views)" if po_delta else "")
+                              + " (DESIGN.md §5)",
             "survey_8d_bytes_per_launch": survey,
             "survey_8d_equivalent_GBps": survey / (kern_ms * 1e-3) / 1e9,
         },
