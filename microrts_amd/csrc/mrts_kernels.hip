@@ -99,9 +99,13 @@ DEV int lane_id() { return (int)threadIdx.x; }
 // hazard passes must see the stores.  MRTS_WT bits (measured on c3 / c5 / --mask-mode full,
 // profiles/r12_summary.md): 1 full-observability planes (c3 +4.5 %, full masks +3 %: on),
 // 2 delta mask records + policy rows (c3 -1.3 %), 4 full-rewrite mask chunks (-15 %),
-// 8 state block (neutral), 16 partial-observability planes (c5 -18 %).
+// 8 state block (neutral), 16 partial-observability planes (c5 -18 %).  Round 2: write-through
+// (`sc1`) buffer stores leave no line in the XCD's L2, so the next step's state and action-row
+// reads (the same game runs on the same XCD every launch: tools/xcd_placement.py) keep theirs:
+// 32 full-observability planes (c3 +3.2 %), 128 partially observable planes (c5 +3.4 %), 64 delta
+// mask records (byte-granular partial lines: c3 -5 %, off).  profiles/round2_store_policy.md.
 #ifndef MRTS_WT
-#define MRTS_WT 1
+#define MRTS_WT 161
 #endif
 typedef int32_t i32x4v __attribute__((ext_vector_type(4)));
 typedef int32_t i32x4u __attribute__((ext_vector_type(4), aligned(4)));
@@ -131,6 +135,19 @@ DEV void st1(int32_t* p, int a) {
 }
 constexpr bool WT_OBS = (MRTS_WT & 1) != 0, WT_MASK = (MRTS_WT & 2) != 0, WT_FULLMASK = (MRTS_WT & 4) != 0,
                WT_STATE = (MRTS_WT & 8) != 0, WT_POOBS = (MRTS_WT & 16) != 0;
+// MRTS_WT bit 32: full-observability planes as write-through (`sc1`) buffer stores, which leave no
+// line in the XCD's L2 (MI355X_MICROARCH.md, store flavours), so the next step's state and action
+// reads keep their L2 lines; `rsrc` = a raw buffer over the stored region (gfx9 descriptor word 3)
+constexpr bool SC1_OBS = (MRTS_WT & 32) != 0;
+// MRTS_WT bit 64: delta mask records (and zero records) likewise; bit 128: partially observable planes
+constexpr bool SC1_MASK = (MRTS_WT & 64) != 0, SC1_POOBS = (MRTS_WT & 128) != 0;
+DEV __amdgpu_buffer_rsrc_t bufRsrc(void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)bytes, 0x00020000);
+}
+DEV void st4sc1(__amdgpu_buffer_rsrc_t r, uint32_t byteOff, int a, int b, int c, int d) {
+    const i32x4v v = {a, b, c, d};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)byteOff, 0, 16);
+}
 DEV int ux(uint32_t c) { return (int)(c & 0xFF); }
 DEV int uy(uint32_t c) { return (int)((c >> 8) & 0xFF); }
 DEV int utyp(uint32_t c) { return (int)((c >> 16) & 0xF); }
@@ -2129,9 +2146,12 @@ struct Game {
                     v[j][4] = (occ && (ca[j] & UA_PRESENT)) ? ua_type(ca[j]) : 0;
                     v[j][5] = sc[j] == WALL ? 1 : 0;
                 }
+                const __amdgpu_buffer_rsrc_t rs = bufRsrc(o0, (uint32_t)(nslots * D.C * HW * 4));
 #pragma unroll
-                for (int pl = 0; pl < 6; pl++)
-                    st4<WT_OBS>(o0 + (size_t)pl * HW + c4, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
+                for (int pl = 0; pl < 6; pl++) {
+                    if (SC1_OBS) st4sc1(rs, (uint32_t)(pl * HW + c4) * 4u, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
+                    else st4<WT_OBS>(o0 + (size_t)pl * HW + c4, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
+                }
                 if (nslots == 2) {  // the other player's view differs only in the owner plane
                     int32_t* o1 = o0 + (size_t)D.C * HW;
 #pragma unroll
@@ -2143,7 +2163,8 @@ struct Game {
                             w.z = w.z ? 3 - w.z : 0;
                             w.w = w.w ? 3 - w.w : 0;
                         }
-                        st4<WT_OBS>(o1 + (size_t)pl * HW + c4, w.x, w.y, w.z, w.w);
+                        if (SC1_OBS) st4sc1(rs, (uint32_t)((D.C + pl) * HW + c4) * 4u, w.x, w.y, w.z, w.w);
+                        else st4<WT_OBS>(o1 + (size_t)pl * HW + c4, w.x, w.y, w.z, w.w);
                     }
                 }
             }
@@ -2313,8 +2334,14 @@ struct Game {
                 v[j][6] = (int)((mr >> (x0 + j)) & 1u);
                 v[j][7] = (int)((tr >> (x0 + j)) & 1u);
             }
+            if (SC1_POOBS) {
+                const __amdgpu_buffer_rsrc_t rs = bufRsrc(out, (uint32_t)(D.C * HW * 4));
 #pragma unroll
-            for (int k = 0; k < 8; k++) st4<WT_POOBS>(out + k * HW + 4 * c4, v[0][k], v[1][k], v[2][k], v[3][k]);
+                for (int k = 0; k < 8; k++) st4sc1(rs, (uint32_t)(k * HW + 4 * c4) * 4u, v[0][k], v[1][k], v[2][k], v[3][k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; k++) st4<WT_POOBS>(out + k * HW + 4 * c4, v[0][k], v[1][k], v[2][k], v[3][k]);
+            }
         }
         wsync();
     }
@@ -2874,6 +2901,40 @@ struct Game {
     // One cell's K-byte mask record (byte k = bit k of lo:hi) at dst, byte-exact: up to 3 head bytes to
     // reach dword alignment, whole dwords (dwordx4 / dwordx3 stores, 4-byte aligned), then the tail
     // bytes — neighbouring records written by other lanes are never touched.
+    // storeRecord as write-through (`sc1`) buffer stores (SC1_MASK): byte offset `off` into the raw
+    // buffer `r` whose base address is `base`
+    DEV void storeRecordSc1(__amdgpu_buffer_rsrc_t r, const uint8_t* base, uint32_t off, uint64_t lo, uint32_t hi) const {
+        const int head = (int)((4u - (((uint32_t)(uintptr_t)base + off) & 3u)) & 3u);
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+            if (i < head) __builtin_amdgcn_raw_buffer_store_b8((char)((lo >> i) & 1u), r, (int)(off + i), 0, 16);
+        const uint64_t sl = (lo >> head) | (head ? ((uint64_t)hi << (64 - head)) : 0ull);
+        const uint32_t sh = hi >> head;
+        const uint32_t v[3] = {(uint32_t)sl, (uint32_t)(sl >> 32), sh};
+        const int nd = (K - head) >> 2;
+        const uint32_t dwo = off + (uint32_t)head;
+        auto nib = [&](int k) -> int { return (int)expand4(v[k >> 3] >> (4 * (k & 7))); };
+        if (K == 79) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const i32x4v w = {nib(4 * q), nib(4 * q + 1), nib(4 * q + 2), nib(4 * q + 3)};
+                __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)(dwo + 16 * q), 0, 16);
+            }
+            typedef int32_t i32x3v __attribute__((ext_vector_type(3)));
+            const i32x3v w3 = {nib(16), nib(17), nib(18)};
+            __builtin_amdgcn_raw_buffer_store_b96(w3, r, (int)(dwo + 64), 0, 16);
+        } else {
+            for (int k = 0; k < nd; k++) __builtin_amdgcn_raw_buffer_store_b32(nib(k), r, (int)(dwo + 4 * k), 0, 16);
+        }
+        const int t0 = head + 4 * nd;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const int b = t0 + i;
+            if (b < K)
+                __builtin_amdgcn_raw_buffer_store_b8((char)((b < 64 ? (lo >> b) : (uint64_t)(hi >> (b - 64))) & 1u), r,
+                                                     (int)(off + b), 0, 16);
+        }
+    }
     DEV void storeRecord(uint8_t* dst, uint64_t lo, uint32_t hi) const {
         const int head = (int)((4u - ((uint32_t)(uintptr_t)dst & 3u)) & 3u);
 #pragma unroll
@@ -2976,6 +3037,8 @@ struct Game {
             prevG()[(i ? pl1 : pl0) * MW + w] = cur;
         }
         const bool pol = D.pol_actions && D.pol_delta;
+        const uint8_t* mbase = D.masks + (size_t)slot0 * total;  // this game's records (SC1_MASK buffer)
+        const __amdgpu_buffer_rsrc_t mrs = bufRsrc((void*)mbase, (uint32_t)(nslots * total));
         // the kernel's full policy pass (writePolicyAll, no delta base) reads the parked bits
         if (si >= 0 && D.pol_actions && !(D.pol_delta && D.mask_delta && (total & 15) == 0)) {
             at[l] = (int32_t)w0;
@@ -2988,7 +3051,8 @@ struct Game {
 #ifdef MRTS_ABLATE
             if (!ab(AB_SKIP_RECORD))
 #endif
-            storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, lo, w2);
+            if (SC1_MASK) storeRecordSc1(mrs, mbase, (uint32_t)(si * total + c * K), lo, w2);
+            else storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, lo, w2);
 #ifdef MRTS_ABLATE
             if (ab(AB_RECORD)) storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, launder(lo), launder(w2));
 #endif
@@ -3032,7 +3096,8 @@ struct Game {
             if (b0 + l < ngone) {
                 const uint32_t e = rslot[l];
                 const int slot = slot0 + (int)(e >> 15), cz = (int)(e & 0x7FFFu);
-                storeRecord(D.masks + (size_t)slot * total + (size_t)cz * K, 0ull, 0u);
+                if (SC1_MASK) storeRecordSc1(mrs, mbase, (uint32_t)((slot - slot0) * total + cz * K), 0ull, 0u);
+                else storeRecord(D.masks + (size_t)slot * total + (size_t)cz * K, 0ull, 0u);
                 if (pol) {
                     int32_t* dst = D.pol_actions + ((size_t)slot * HW + cz) * 7;
                     st4u<WT_MASK>(dst, 0, 0, 0, 0);
