@@ -985,6 +985,31 @@ struct Game {
     DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB,
                                 bool keepBits, int& irank) {
         const int l = lane_id();
+        {
+            // Parallel form for the common case: when no candidate's used position is reserved already,
+            // no two candidates use the same position, and the base reservations plus every candidate's
+            // cost fit the player's resources, each sequential consistentWith test below passes (the
+            // running sum only grows by accepted costs, so every prefix fits too) — accept them all.
+            const int runQ = p == 0 ? run1 : run0, presQ = p == 0 ? pres1 : pres0, presP = p == 0 ? pres0 : pres1;
+            const int runP = p == 0 ? run0 : run1;
+            const bool cand = rank >= 0, up = cand && usesPos;
+            if (!(runQ != 0 && runQ > 0 && runQ > presQ)) {
+                bool conf = up && ((bits[tpos >> 5] >> (tpos & 31)) & 1u);
+                for (uint64_t mm = ballot(up); mm; mm &= mm - 1) {
+                    const int k = __builtin_ctzll(mm);
+                    if (up && k != l && rl(tpos, k) == tpos) conf = true;
+                }
+                const int sumc = ballot(cand && cost > 0) ? wave_sum(cand ? cost : 0) : 0;
+                if (!ballot(conf) && runP + sumc <= presP) {
+                    if (p == 0) run0 = runP + sumc;
+                    else run1 = runP + sumc;
+                    if (!keepBits && up) atomicOr(&bits[tpos >> 5], 1u << (tpos & 31));
+                    if (cand) irank = rank;
+                    wsync();
+                    return ballot(cand);
+                }
+            }
+        }
         uint32_t bv = l < NB ? bits[l] : 0u;
         if (rank >= 0) rseq[rank] = (int)(((uint32_t)usesPos << 31) | ((uint32_t)cost << 16) | ((uint32_t)tpos & 0xFFFFu));
         wsync();
