@@ -84,6 +84,20 @@ static void finishUtt(UttInfo& I) {
     for (int t = 0; t < u.ntypes; t++) maxRange = std::max(maxRange, u.range[t]);
     u.maxAttackRadius = 2 * maxRange + 1;
     u.K = 1 + 6 + 4 + 4 + 4 + 4 + u.ntypes + u.maxAttackRadius * u.maxAttackRadius;
+    u.mtAttack1 = u.mtAttackFar = u.mtHarvest = u.mtMove = u.mtResource = u.mtStockpile = 0;
+    uint64_t prod = 0;
+    for (int t = 0; t < u.ntypes; t++) {  // the mask tables (Game::maskTables)
+        const uint32_t f = u.flags[t], b = 1u << t;
+        if ((f & F_ATTACK) && u.range[t] == 1) u.mtAttack1 |= b;
+        if ((f & F_ATTACK) && u.range[t] > 1) u.mtAttackFar |= b;
+        if (f & F_HARVEST) u.mtHarvest |= b;
+        if (f & F_MOVE) u.mtMove |= b;
+        if (f & F_RESOURCE) u.mtResource |= b;
+        if (f & F_STOCKPILE) u.mtStockpile |= b;
+        for (int i = 0; i < u.nprod[t]; i++) prod |= (uint64_t)1 << (8 * t + u.prod[t][i]);
+    }
+    u.mtProdLo = (uint32_t)prod;
+    u.mtProdHi = (uint32_t)(prod >> 32);
     u.maxSight = 0;
     for (int t = 0; t < u.ntypes; t++) {  // integer floor(sqrt(r^2 - dy^2)): the cells dx^2 + dy^2 <= r^2
         const int r = u.sight[t];

@@ -28,6 +28,10 @@ struct DevUtt {
     // dy 0..7 in diskLo, 8..15 in diskHi (PartiallyObservableGameState visibility, painted per row)
     uint32_t diskLo[MAX_TYPES], diskHi[MAX_TYPES];
     int32_t maxSight;           // max sight[t] over the types
+    // per-type bit sets of the mask tables (bit t = type t has the property; host-computed) and the
+    // produce lists as 8-bit type sets (type t's set in bits 8t..8t+7 of mtProd)
+    uint32_t mtAttack1, mtAttackFar, mtHarvest, mtMove, mtResource, mtStockpile;
+    uint32_t mtProdLo, mtProdHi;
 };
 enum : uint32_t { F_RESOURCE = 1, F_STOCKPILE = 2, F_HARVEST = 4, F_MOVE = 8, F_ATTACK = 16,
                   // the type-name tests of the reward functions (src/ai/reward/*.java), set from the names

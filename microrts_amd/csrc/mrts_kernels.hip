@@ -2623,26 +2623,21 @@ struct Game {
         uint64_t prod;
     };
     DEV MaskTables maskTables() const {
+        // the constant sets come with the unit-type table (host-computed, DevUtt::mt*); only the
+        // affordability sets depend on the step (the players' resources now)
         const int t = lane_id();
         const bool ok = t < NT;
-        const uint32_t fl = ok ? U.flags[t] : 0u;
-        const int r = ok ? U.range[t] : 0, cost = ok ? U.cost[t] : 0, np = ok ? U.nprod[t] : 0;
-        uint32_t pm = 0;
-#pragma unroll
-        for (int i = 0; i < MAX_PRODUCES; i++)
-            if (i < np) pm |= 1u << U.prod[t][i];
+        const int cost = ok ? U.cost[t] : 0;
         MaskTables T;
-        T.attack1 = (uint32_t)ballot(ok && (fl & F_ATTACK) && r == 1);
-        T.attackFar = (uint32_t)ballot(ok && (fl & F_ATTACK) && r > 1);
-        T.harvest = (uint32_t)ballot(ok && (fl & F_HARVEST));
-        T.move = (uint32_t)ballot(ok && (fl & F_MOVE));
-        T.resource = (uint32_t)ballot(ok && (fl & F_RESOURCE));
-        T.stockpile = (uint32_t)ballot(ok && (fl & F_STOCKPILE));
+        T.attack1 = uniu(U.mtAttack1);
+        T.attackFar = uniu(U.mtAttackFar);
+        T.harvest = uniu(U.mtHarvest);
+        T.move = uniu(U.mtMove);
+        T.resource = uniu(U.mtResource);
+        T.stockpile = uniu(U.mtStockpile);
+        T.prod = (uint64_t)uniu(U.mtProdLo) | ((uint64_t)uniu(U.mtProdHi) << 32);
         T.aff0 = (uint32_t)ballot(ok && pres0 >= cost);
         T.aff1 = (uint32_t)ballot(ok && pres1 >= cost);
-        T.prod = 0;
-#pragma unroll
-        for (int k = 0; k < MAX_TYPES; k++) T.prod |= (uint64_t)(uniu((uint32_t)rl((int)pm, k)) & 0xFFu) << (8 * k);
         return T;
     }
     // unitMask's bits for range <= 1 units (the range > 1 attack window: farAttackBits) from the
