@@ -94,6 +94,11 @@ enum : uint32_t {
 };
 
 DEV int lane_id() { return (int)threadIdx.x; }
+// branch-probability hints: cold paths (more than 64 units, auto-reset, conflict resolution, the
+// general mask writer, reward bookkeeping the benchmark does not request) are laid out away from the
+// hot straight-line code, which then packs into fewer instruction-cache lines
+#define MRTS_LIKELY(x) __builtin_expect(!!(x), 1)
+#define MRTS_UNLIKELY(x) __builtin_expect(!!(x), 0)
 // Output stores.  WT = streaming (`nt`) stores, so output lines do not sit dirty in the XCD's L2
 // until the end-of-kernel write-back.  Builtins, not inline asm: the wait-count and store-data
 // hazard passes must see the stores.  MRTS_WT bits (measured on c3 / c5 / --mask-mode full,
@@ -900,7 +905,7 @@ struct Game {
             baseReservations(p, run0, run1);
         }
         MPHASE(13);
-        if (nu <= 64) {
+        if (MRTS_LIKELY(nu <= 64)) {
             decodeUnits(p, run0, run1, useIx, issueNow);
             return;
         }
@@ -1321,7 +1326,7 @@ struct Game {
                         const uint32_t* cuKnown = nullptr) {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
-        if (D.reward_need & RN_COUNTS) {  // the pairs as the TraceEntry records them (legality applied)
+        if (MRTS_UNLIKELY(D.reward_need & RN_COUNTS)) {  // the pairs as the TraceEntry records them (legality applied)
             const int pc = np ? prodCategory(U.flags[ut]) : -1;
             auto cnt = [](bool b) { return (int)__popcll(ballot(b)); };
             const int c[RC_N] = {cnt(act && t == T_HARVEST), cnt(act && t == T_RETURN), cnt(act && t == T_ATTACK),
@@ -1367,7 +1372,7 @@ struct Game {
                 }
             }
         }
-        if (ballot(conf) == 0) {
+        if (MRTS_LIKELY(ballot(conf) == 0)) {
             if (act) {
                 ua[s] = pack_ua(t, ut, tx, ty) | UA_PRESENT;
                 par[s] = (int16_t)prm;
@@ -1853,7 +1858,7 @@ struct Game {
     DEV void cycle() {
         time++;
         ixValid = false;
-        if (nu <= 64) {
+        if (MRTS_LIKELY(nu <= 64)) {
             cycleLanes();
             return;
         }
@@ -2080,7 +2085,7 @@ struct Game {
     DEV bool writeRewards(int slot0, int nslots, int pl0, int pl1, bool gameover, int winner) {
         const int R = D.n_rewards;
         int newSq0 = INF, newSq1 = INF;
-        if (D.reward_need & RN_CLOSER) closerMin(newSq0, newSq1);
+        if (MRTS_UNLIKELY(D.reward_need & RN_CLOSER)) closerMin(newSq0, newSq1);
         bool resLeft = false;
         if (D.reward_need & RN_RESOURCES)
             for (int o0 = 0; o0 < nu; o0 += 64) {
@@ -3276,9 +3281,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
-        if (D.reward_need & RN_COUNTS)
+        if (MRTS_UNLIKELY(D.reward_need & RN_COUNTS))
             if (lane_id() < 2 * RC_N) G.rwc[lane_id()] = 0;
-        if (D.reward_need & RN_CLOSER) G.closerBefore();
+        if (MRTS_UNLIKELY(D.reward_need & RN_CLOSER)) G.closerBefore();
         const bool rowsMode = FIX ? false : D.rows != nullptr;
         if (rowsMode && gtype == GT_SELFPLAY) {
             for (int p = 0; p < 2; p++) {
@@ -3297,7 +3302,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
             G.issuePlayer(1 - side, 10, true);
         } else if (gtype == GT_SELFPLAY) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
-            if (!G.po && G.nu <= 64) {
+            if (MRTS_LIKELY(!G.po && G.nu <= 64)) {
                 G.selfPlayFast(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride);
             } else {
             G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1);
@@ -3352,7 +3357,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         const bool done0 = G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner);
         const bool reset = done0 || steps >= D.max_steps;
         if (reset && D.done && lane_id() < nslots) D.done[(size_t)(slot0 + lane_id()) * D.n_rewards] = 1;
-        if (reset) {
+        if (MRTS_UNLIKELY(reset)) {
             G.hset(H_STEPS, 0);  // envSteps[i] = 0 (JNIGridnetVecClient.java:229,264-265,285)
             G.resetFromTemplate();
             if (G.po) G.clearSnap();
@@ -3393,7 +3398,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     PHASE(7);
     if (D.masks && external) {
         const int nsl = selfplay ? 2 : 1;
-        if (D.mask_delta && G.nu <= 64 && nsl * maskWords(G.HW) <= 64 && G.K <= 96) {
+        if (MRTS_LIKELY(D.mask_delta && G.nu <= 64 && nsl * maskWords(G.HW) <= 64 && G.K <= 96)) {
             PHASE(8);
             if (selfplay) G.writeMasksLanes(slot0, 2, 0, 1);
             else G.writeMasksLanes(slot0, 1, D.mask_player, D.mask_player);
