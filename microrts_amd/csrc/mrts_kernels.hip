@@ -35,14 +35,28 @@ enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2, MODE_PLAYOUT = 3 };
 constexpr int PH_GAMES = 1 << 16;
 constexpr int NPH = 32;  // phase slots
 __device__ unsigned long long g_phase[NPH * PH_GAMES];  // [phase][game], no contention
-__device__ unsigned long long g_span[3 * PH_GAMES];    // last launch: [game] start / end, s_memrealtime (100 MHz),
+__device__ unsigned long long g_span[11 * PH_GAMES];    // last launch: [game] start / end, s_memrealtime (100 MHz),
                                                        // placement: HW_ID | XCC_ID << 32 | nu at start << 40 | nu at end << 48
+#ifdef MRTS_SPAN_ONLY
+// per-game start / end / placement plus 8 milestones (lane 0 stores s_memrealtime to g_span block
+// 3 + mileOf(phase id)); no per-phase accumulation.  Each stamp costs an lgkmcnt drain and a store.
+constexpr int NMILE = 8;
+constexpr int mileOf(int ph) {
+    return ph == 20 ? 0 : ph == 21 ? 1 : ph == 1 ? 2 : ph == 3 ? 3 : ph == 4 ? 4 : ph == 5 ? 5 : ph == 6 ? 6 : ph == 9 ? 7 : -1;
+}
+#define PHASE_IN(acc, tt, i)                                                                      \
+    do {                                                                                          \
+        if (mileOf(i) >= 0 && threadIdx.x == 0 && (int)blockIdx.x < PH_GAMES)                      \
+            g_span[(3 + mileOf(i)) * PH_GAMES + blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
 #define PHASE_IN(acc, tt, i)                          \
     do {                                              \
         const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
         (acc)[i] += t_ - (tt);                        \
         (tt) = t_;                                    \
     } while (0)
+#endif
 #define PHASE(i) PHASE_IN(G.phAcc, G.tph_, i)  // in the kernel body
 #define MPHASE(i) PHASE_IN(phAcc, tph_, i)     // inside Game methods
 #else
@@ -344,7 +358,9 @@ struct Game {
     // the sum of present PRODUCE costs
 #ifdef MRTS_PHASE_TIMING
     uint64_t tph_;
+#ifndef MRTS_SPAN_ONLY
     uint64_t phAcc[NPH];  // per-phase cycles (registers: constant indices), flushed at kernel end
+#endif
 #endif
 #ifdef MRTS_ABLATE
     uint32_t G_AB = 0;
@@ -1274,7 +1290,9 @@ struct Game {
     // full observability it is also every view's base ResourceUsage (PlayerAction.java:497-505).
     DEV void buildIndex() {
 #ifdef MRTS_PHASE_TIMING
+#ifndef MRTS_SPAN_ONLY
         phAcc[15] += 1000;  // call counter (x1000 so the per-step mean shows)
+#endif
 #endif
         const int NB = (HW + 2 * W + 31) / 32;
         for (int i = lane_id(); i < NB; i += 64) bits[i] = 0;
@@ -1393,7 +1411,9 @@ struct Game {
             wsync();
         } else {
 #ifdef MRTS_PHASE_TIMING
+#ifndef MRTS_SPAN_ONLY
             phAcc[11] += 1000;  // slow-path batches
+#endif
 #endif
             for (int r = 0; r < n; r++) {
                 const int k = __builtin_ctzll(ballot(act && rank == r));
@@ -3206,7 +3226,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     const int side = selfplay ? 0 : (D.players ? uni(D.players[slot0]) : 0);
     bool freshObs = true;  // observation comes from the current (post-step or fresh) state
 #ifdef MRTS_PHASE_TIMING
+#ifndef MRTS_SPAN_ONLY
     for (int i = 0; i < NPH; i++) G.phAcc[i] = 0;
+#endif
     G.tph_ = __builtin_amdgcn_s_memtime();
     const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -3429,7 +3451,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     PHASE(10);
 #ifdef MRTS_PHASE_TIMING
     if (lane_id() == 0 && G.g < PH_GAMES) {
+#ifndef MRTS_SPAN_ONLY
         for (int i = 0; i < NPH; i++) g_phase[i * PH_GAMES + G.g] += G.phAcc[i];
+#endif
         g_span[G.g] = rt0_;
         g_span[PH_GAMES + G.g] = __builtin_amdgcn_s_memrealtime();
         g_span[2 * PH_GAMES + G.g] = (unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
@@ -3651,15 +3675,12 @@ hipError_t phaseTimes(unsigned long long* out, int reset) {
     }
     return e;
 }
-hipError_t phaseSpans(unsigned long long* out, int n) {  // [n] starts, [n] ends, [n] placements of the last launch
-    std::vector<unsigned long long> h((size_t)3 * PH_GAMES);
+hipError_t phaseSpans(unsigned long long* out, int n) {  // [11][n]: starts, ends, placements, milestones of the last launch
+    std::vector<unsigned long long> h((size_t)11 * PH_GAMES);
     hipError_t e = hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_span), h.size() * sizeof(h[0]));
     if (e != hipSuccess) return e;
-    for (int i = 0; i < n && i < PH_GAMES; i++) {
-        out[i] = h[i];
-        out[n + i] = h[PH_GAMES + i];
-        out[2 * n + i] = h[2 * PH_GAMES + i];
-    }
+    for (int b = 0; b < 11; b++)  // starts, ends, placements, then the span build's 8 milestones
+        for (int i = 0; i < n && i < PH_GAMES; i++) out[(size_t)b * n + i] = h[(size_t)b * PH_GAMES + i];
     return e;
 }
 #endif

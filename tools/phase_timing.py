@@ -13,7 +13,7 @@ import torch  # noqa: E402,F401
 
 from microrts_amd import _lib  # noqa: E402
 
-L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_timing.so"))
+L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_span.so" if os.environ.get("LIB") == "span" else "libmrts_timing.so"))
 L.mrts_phase_times.argtypes = [ctypes.c_void_p, ctypes.c_int]
 L.mrts_phase_spans.argtypes = [ctypes.c_void_p, ctypes.c_int]
 from microrts_amd import DeviceVecEnv  # noqa: E402
@@ -104,7 +104,7 @@ for delta in (True, False):
         e.synchronize()
         ms += s.elapsed_time(e)
     ph = read(1)
-    sp = (ctypes.c_ulonglong * (3 * E))()
+    sp = (ctypes.c_ulonglong * (11 * E))()
     _lib.check(L.mrts_phase_spans(sp, E))
     import numpy as np
     st = np.array(sp[:E], dtype=np.float64)
@@ -112,6 +112,24 @@ for delta in (True, False):
     place = np.array(sp[2 * E:3 * E], dtype=np.uint64)
     if os.environ.get("TAIL", "0") == "1" and delta:
         tail_report(st, en, place)
+    if os.environ.get("LIB") == "span" and delta:
+        # milestones (span build): us from the game's start, mean / p50 / p90 / max over games
+        mnames = ["header", "loaded", "rows", "issued", "cycled", "outcome", "obs", "masks"]
+        rep = {}
+        prev = st
+        for b, nm in enumerate(mnames):
+            m = np.array(sp[(3 + b) * E:(4 + b) * E], dtype=np.float64)
+            ok = m >= st
+            if not ok.any():
+                continue
+            d = (m - st)[ok] / 100.0
+            seg = (m - prev)[ok] / 100.0
+            rep[nm] = {"from_start_mean": round(float(d.mean()), 2), "p90": round(float(np.percentile(d, 90)), 2),
+                       "segment_mean": round(float(seg.mean()), 2)}
+            prev = np.where(ok, m, prev)
+        d = (en - prev) / 100.0
+        rep["end"] = {"from_start_mean": round(float(((en - st) / 100.0).mean()), 2), "segment_mean": round(float(d.mean()), 2)}
+        print(json.dumps({"milestones": rep}), flush=True)
     t0 = st.min()
     spans = {"dispatch_spread_us": (st.max() - t0) / 100.0, "kernel_span_us": (en.max() - t0) / 100.0,
              "game_us_mean": float((en - st).mean()) / 100.0, "game_us_p99": float(np.percentile(en - st, 99)) / 100.0,
