@@ -305,7 +305,8 @@ def main():
 
     # Roofline bytes per step-kernel launch.  The step's HBM contract under the persistent-buffer
     # (delta) mask mode — what any implementation must move:
-    #   A = idle-unit action rows read (28 B each; other rows are ignored by the Java decode),
+    #   A = idle-unit action rows read (28 B each; other rows are ignored by the Java decode; 4 B when
+    #       the fused policy forwards them),
     #   O = C*HW*4 observation written per slot,
     #   M = K bytes per mask row that changed (delta) or HW*K per slot (full rewrite),
     #   S = per game: header 64 B + 28 B/unit, read and written; terrain HW B read; previous row sets
@@ -335,9 +336,12 @@ def main():
     n_games = S // 2
     m_bytes = dirty * K if a.mask_mode == "delta" else HW * K
     o_bytes = obs_chunks * 16  # C * HW * 4 for a full write
-    contract = S * (rows * 28 + o_bytes + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
-    if fused:  # the policy's action rows leave the step kernel too
-        contract += S * (dirty if a.mask_mode == "delta" else HW) * 28
+    # fused policy: the idle units' rows arrive as one forwarded 4-B word each (KDyn.fwd_read), and the
+    # step writes that word next to the 28-B row it leaves in the action tensor
+    row_in = 4 if fused else 28
+    contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
+    if fused:  # the policy's action rows (and their forwarded words) leave the step kernel too
+        contract += S * (dirty if a.mask_mode == "delta" else HW) * 28 + S * rows * 4
     survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16))
     achieved = contract / (kern_ms * 1e-3) / 1e9
     # roofline.traffic: HBM bytes per k_env launch from the rocprofv3 --pmc passes of this same command

@@ -491,6 +491,7 @@ struct mrts_env {
     const int32_t* lastPolicyActions = nullptr;
     bool polValid = false;
     const int32_t* fusedActions = nullptr;  // buffer the last fused-policy step wrote (delta base), or null
+    mutable uint32_t launchStamp = 0;       // KDyn.fwd_stamp of the last k_env launch (never 0)
     int polParity = 0;
     // the kernels store observations and mask chunks as 16-byte vectors
     static void checkAlign(const KDyn& D) {
@@ -556,6 +557,8 @@ struct mrts_env {
         D.reward_need = hstatic.reward_need;
         D.reward_kinds4 = 0;
         for (int j = 0; j < hstatic.n_rewards; j++) D.reward_kinds4 |= (uint32_t)hstatic.reward_kinds[j] << (4 * j);
+        if (++launchStamp == 0) ++launchStamp;  // H_FWD = 0 means "no forwarded rows"
+        D.fwd_stamp = launchStamp;
         return launchEnv(mode, hstatic, d_static, D, s);
     }
     int gameOfSlot(int slot, int* player) const {
@@ -873,6 +876,7 @@ int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_play
         D.pol_step = next_step;
         D.pol_slot_base = env->slotIdBase;
         D.pol_delta = (D.mask_delta && env->fusedActions == d_actions) ? 1 : 0;
+        D.fwd_read = env->fusedActions == d_actions ? 1 : 0;  // games check H_FWD == this stamp - 1
         HIPCHK(env->launch(0, D, pickStream(env, stream)));
         env->fusedActions = d_actions;
         if (env->lastPolicyActions == d_actions) env->polValid = false;  // the standalone policy's delta base is stale
@@ -1475,7 +1479,7 @@ int mrts_checkpoint(mrts_env* env, void* buf, int64_t cap) {
         CkptHeader h;
         std::memset(&h, 0, sizeof(h));
         std::memcpy(h.magic, "MRTSCKP1", 8);
-        h.version = 2;
+        h.version = 3;
         h.H = env->H;
         h.W = env->W;
         h.CAP = env->CAP;
@@ -1499,7 +1503,7 @@ int mrts_restore(mrts_env* env, const void* buf, int64_t size) {
         CkptHeader h;
         if (size < (int64_t)sizeof(h)) throw Fail{-EINVAL, "checkpoint too short"};
         std::memcpy(&h, buf, sizeof(h));
-        if (std::memcmp(h.magic, "MRTSCKP1", 8) != 0 || h.version != 2) throw Fail{-EINVAL, "not a checkpoint"};
+        if (std::memcmp(h.magic, "MRTSCKP1", 8) != 0 || h.version != 3) throw Fail{-EINVAL, "not a checkpoint"};
         if (h.H != env->H || h.W != env->W || h.CAP != env->CAP || h.nGames != env->nGames || h.nSpGames != env->nSpGames ||
             h.words != stateWords(env->CAP, env->HW) || h.uttHash != uttHash(env->utt))
             throw Fail{-EINVAL, "checkpoint of a different configuration"};

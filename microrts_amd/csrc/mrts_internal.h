@@ -56,6 +56,7 @@ enum {
     H_RNG_DAMAGE = 10,// 2 words: java.util.Random for non-deterministic damage (UnitAction.r)
     H_RNG_SAMPLER = 12,// 2 words: java.util.Random for RandomBiasedAI (Sampler.generator)
     H_KIND = 14,      // game kind (KStatic.game_kind), copied here so a step needs no dependent load
+    H_FWD = 15,       // launch stamp of the fused policy's forwarded action rows (0 = none; see stateFwdOff)
     H_WORDS = 16
 };
 // followed by 7 SoA arrays of CAP int32: UC, HP, RES, UA, PAR, AT, AS (see mrts_kernels.hip)
@@ -66,7 +67,14 @@ constexpr int maskWords(int hw) { return (hw + 31) / 32; }
 // after the arrays: the previous mask row sets (2 x maskWords), then the map's terrain bytes (copied
 // from the template at reset, so a step's first memory round needs nothing but the state block)
 constexpr int stateTerrOff(int cap, int hw) { return H_WORDS + N_ARRAYS * cap + 2 * maskWords(hw); }
-constexpr int stateWords(int cap, int hw) { return stateTerrOff(cap, hw) + (hw + 3) / 4; }  // host + device
+// then FWD_WORDS words: the fused random policy's action rows of the idle units in slots 0..63, one
+// packed word per slot (packFwd in mrts_kernels.hip), written by the launch whose stamp is in H_FWD.
+// The next launch of a self-play game reads them in its first memory round instead of fetching the
+// rows from the action tensor the same launch wrote them to (KDyn.fwd_read), which removes the
+// step's second dependent global round trip.
+constexpr int FWD_WORDS = 64;
+constexpr int stateFwdOff(int cap, int hw) { return stateTerrOff(cap, hw) + (hw + 3) / 4; }
+constexpr int stateWords(int cap, int hw) { return stateFwdOff(cap, hw) + FWD_WORDS; }  // host + device
 
 // unit core word
 constexpr uint32_t UC_DEAD = 1u << 31;
@@ -122,6 +130,12 @@ struct KDyn {
     uint64_t pol_seed;
     uint32_t pol_step, pol_slot_base;
     int32_t pol_delta;             // 1: pol_actions holds the policy rows of the previous mask write's candidates
+    // forwarded action rows: fwd_read = 1 when `actions` is the buffer the previous launch on this
+    // handle wrote as pol_actions and nothing has written it since (the host's fusedActions); a game
+    // uses its forwarded words iff its H_FWD == fwd_stamp - 1 (this launch's stamp minus one, i.e.
+    // the previous launch wrote them).  Every launch that stores a state writes H_FWD.
+    int32_t fwd_read;
+    uint32_t fwd_stamp;
     // copies of the KStatic fields the step reads after its first memory round (kernel arguments sit
     // in SGPRs from the kernel's start; a KStatic load there is a dependent round trip on the chain)
     int32_t n_rewards, max_steps, C;

@@ -317,6 +317,24 @@ DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes
     }
 }
 
+// Forwarded action word (H_FWD / stateFwdOff): the 7 values of a fused-policy row, which the sampler
+// draws as type 0..5 and parameters -1..(field size - 1): type 3 bits, the four directions 3 bits
+// each, produce type 4 bits, attack index 7 bits, each parameter stored + 1.
+DEV uint32_t packFwd(const int32_t a[7]) {
+    return ((uint32_t)a[0] & 7u) | (((uint32_t)(a[1] + 1) & 7u) << 3) | (((uint32_t)(a[2] + 1) & 7u) << 6) |
+           (((uint32_t)(a[3] + 1) & 7u) << 9) | (((uint32_t)(a[4] + 1) & 7u) << 12) | (((uint32_t)(a[5] + 1) & 15u) << 15) |
+           (((uint32_t)(a[6] + 1) & 127u) << 19);
+}
+DEV void unpackFwd(uint32_t w, int32_t a[7]) {
+    a[0] = (int32_t)(w & 7u);
+    a[1] = (int32_t)((w >> 3) & 7u) - 1;
+    a[2] = (int32_t)((w >> 6) & 7u) - 1;
+    a[3] = (int32_t)((w >> 9) & 7u) - 1;
+    a[4] = (int32_t)((w >> 12) & 7u) - 1;
+    a[5] = (int32_t)((w >> 15) & 15u) - 1;
+    a[6] = (int32_t)((w >> 19) & 127u) - 1;
+}
+
 struct Game {
     const KStatic& P;
     const KDyn& D;  // the kernel argument itself (kernarg memory): fields load on demand
@@ -369,6 +387,9 @@ struct Game {
     bool ixValid;
     bool anyMP;
     uint32_t lcu, lua;     // load(): lane l's unit core / assignment words (units 0..63) as loaded
+    uint32_t lfwd;         // load(): lane l's forwarded action word (KDyn.fwd_read)
+    bool fwdOn;            // this game's forwarded action words are current (H_FWD == fwd_stamp - 1)
+    bool fwdWritten;       // this launch wrote the forwarded action words (store() stamps H_FWD)
     uint32_t lkey, lsnap;  // PO delta: lane l's hp | resources << 16 as loaded, its previous render's snapshot byte
     uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
     int curP;              // player whose pa is being issued
@@ -406,6 +427,9 @@ struct Game {
         poDirty = poPend + 2 * poChunkWords(HW);
         poList = (uint16_t*)(poDirty + 2 * poChunkWords(HW));  // poDirty: dirty + next pending bits
         ixValid = false;
+        fwdOn = false;
+        fwdWritten = false;
+        lfwd = 0;
     }
     // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
     enum { HX_SNAP = 16, HX_BASE = 18, HX_OLDSQ = 20, HX_POVALID = 22 };
@@ -511,6 +535,8 @@ struct Game {
         for (int a = 0; a < N_ARRAYS; a++) r[a] = arr[a * CAP + l];
         const uint32_t tw = l < TW ? (uint32_t)terr[l] : 0u;
         const uint32_t pv = (wantPrev && l < PW) ? (uint32_t)arr[N_ARRAYS * CAP + l] : 0u;
+        // forwarded action words (speculative: used only if H_FWD, in this same round, matches)
+        const uint32_t fw = D.fwd_read ? (uint32_t)s[stateFwdOff(CAP, HW) + l] : 0u;
         // PO delta: the previous render's record, in the same memory round
         const bool poRec = po && D.obs_delta && D.po_prev && poDeltaShape(H, W);
         const int32_t* pr = poRec ? D.po_prev + (size_t)g * D.po_words : nullptr;
@@ -527,6 +553,8 @@ struct Game {
         MPHASE(20);
         lcu = (uint32_t)r[A_UC];
         lua = (uint32_t)r[A_UA];
+        lfwd = fw;
+        fwdOn = D.fwd_read && (uint32_t)rl(hv, H_FWD) == D.fwd_stamp - 1u;
         if (poRec) {
             lkey = (uint32_t)(uint16_t)r[A_HP] | ((uint32_t)(uint16_t)r[A_RES] << 16);
             lsnap = ((uint32_t)prsb >> (8 * (l & 3))) & 0xFFu;
@@ -579,6 +607,7 @@ struct Game {
             case H_RES0: hv = pres0; break;
             case H_RES1: hv = pres1; break;
             case H_SEQ: hv = seq; break;
+            case H_FWD: hv = fwdWritten ? (int)D.fwd_stamp : 0; break;
         }
         if (l < H_WORDS) st1<WT_STATE>(s + l, hv);
         int32_t* arr = s + H_WORDS;
@@ -638,7 +667,11 @@ struct Game {
         const int pl = l < nu ? uplay(cu) : -1;
         const bool idle = pl >= 0 && !(lua & UA_PRESENT);
         int32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
-        if (idle) {
+        if (fwdOn) {
+            // the previous launch's fused policy sampled this unit's row (the values it wrote to the
+            // action tensor at this cell) and forwarded it in the state block
+            if (idle) unpackFwd(lfwd, a);
+        } else if (idle) {
             const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)(uy(cu) * W + ux(cu)) * 7;
 #pragma unroll
             for (int k = 0; k < 7; k++) a[k] = r[k];
@@ -3082,6 +3115,9 @@ struct Game {
             prevG()[(i ? pl1 : pl0) * MW + w] = cur;
         }
         const bool pol = D.pol_actions && D.pol_delta;
+        // forward the sampled rows of a self-play game (read by selfPlayFast next launch); K - 23 - NT
+        // attack slots fit packFwd's 7-bit field
+        const bool fwdW = pol && nslots == 2 && K - 23 - NT <= 126;
         const uint8_t* mbase = D.masks + (size_t)slot0 * total;  // this game's records (SC1_MASK buffer)
         const __amdgpu_buffer_rsrc_t mrs = bufRsrc((void*)mbase, (uint32_t)(nslots * total));
         // the kernel's full policy pass (writePolicyAll, no delta base) reads the parked bits
@@ -3117,8 +3153,10 @@ struct Game {
                 int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
                 st4u<WT_MASK>(dst, a[0], a[1], a[2], a[3]);
                 st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
+                if (fwdW) st1<WT_STATE>(st() + stateFwdOff(CAP, HW) + l, (int32_t)packFwd(a));
             }
         }
+        fwdWritten = fwdW;
         MPHASE(14);
         // cells whose idle unit is gone: zero record + zero row
         const uint32_t gone = old & ~cur;

@@ -592,6 +592,46 @@ def test_fused_policy_matches_separate_kernels(mp, n_sp, n_bot, po, delta):
     del torch
 
 
+@pytest.mark.parametrize("mp", ["maps/16x16/basesWorkers16x16.xml", "maps/8x8/basesWorkers8x8.xml"])
+def test_fused_forwarding_respects_action_writes(mp):
+    """A fused step forwards its sampled rows to the next launch in the state block (KDyn.fwd_read):
+    when the caller overwrites the action tensor in between (uniform random rows, every 7th step), or
+    runs a plain step or a mask write on the handle, the next fused step must read the tensor.  Twin A
+    always reads the tensor (step + standalone policy kernel)."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n_sp = 16
+    mk = lambda: DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=5)  # noqa: E731
+    A, B = mk(), mk()
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+    g = torch.Generator(device="cpu").manual_seed(11)
+    hi = torch.tensor([6, 4, 4, 4, 4, 7, 49], dtype=torch.int32)
+    for k in range(200):
+        if k % 7 == 3:
+            alt = (torch.rand(tuple(A.actions.shape), generator=g) * hi).to(torch.int32)
+            for e in (A, B):
+                e.actions.copy_(alt.to(e.actions.device))
+        if k % 29 == 11:  # a plain step on the fused handle, then a fresh policy write
+            B.step()
+            A.step()
+            for e in (A, B):
+                e.random_policy(SEED, 1000 + k)
+        if k % 31 == 17:
+            B.get_masks()
+        A.step()
+        A.random_policy(SEED, k + 1)
+        B.step_fused(SEED, k + 1)
+        for name in ("obs", "reward", "done", "masks", "actions"):
+            assert np.array_equal(getattr(A, name).cpu().numpy(), getattr(B, name).cpu().numpy()), f"{name} after {k}"
+    for s in range(0, n_sp, 2):
+        assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s}"
+    A.close()
+    B.close()
+
+
 @pytest.mark.parametrize("mp,n_sp", [("maps/16x16/basesWorkers16x16.xml", 64), ("maps/8x8/basesWorkers8x8.xml", 16)])
 def test_native_rollout_matches_fused_steps(mp, n_sp):
     """mrts_rollout_fused_dev(n) = n mrts_step_fused_dev calls (the bench's timed launch form), bit for
