@@ -356,6 +356,7 @@ struct Game {
     uint32_t* poVis;
     uint32_t* poPend;
     uint32_t* poDirty;
+    uint32_t* vis2;  // writeObsPOFast2: view 1's sight rows [2][H]
     uint16_t* poList;
     int32_t* rseq;   // ready-list scratch (64)
     uint32_t* mprev; // previous mask row sets, [2][maskWords(HW)] (delta mask writes)
@@ -424,8 +425,9 @@ struct Game {
         vis = scell + HW;
         poVis = vis + 2 * H * ((W + 31) / 32);
         poPend = poVis + 4 * H;
-        poDirty = poPend + 2 * poChunkWords(HW);
-        poList = (uint16_t*)(poDirty + 2 * poChunkWords(HW));  // poDirty: dirty + next pending bits
+        poDirty = poPend + 2 * poChunkWords(HW);  // [view][dirty, next pending bits] (view 1: writeObsPOFast2)
+        vis2 = poDirty + 4 * poChunkWords(HW);
+        poList = (uint16_t*)(vis2 + 2 * H);  // up to 2 x HW / 4 entries
         ixValid = false;
         fwdOn = false;
         fwdWritten = false;
@@ -1754,6 +1756,23 @@ struct Game {
             if (ady <= sr && yy >= 0 && yy < H) atomicOr(&rows[yy], b);
         }
     }
+    // paintDisks into two views at once: the same disk (same unit) ORed into view 0's rows when act0
+    // and into view 1's when act1 (row buffers rows0 / rows1 chosen per lane)
+    DEV void paintDisks2(bool act0, uint32_t* rows0, bool act1, uint32_t* rows1, uint32_t u) const {
+        const bool act = act0 || act1;
+        const int t = utyp(u), x = ux(u), y = uy(u);
+        const int sr = act ? U.sight[t] : -1, SM = U.maxSight;
+        const uint32_t dlo = act ? U.diskLo[t] : 0u, dhi = act ? U.diskHi[t] : 0u;
+        for (int dy = -SM; dy <= SM; dy++) {
+            const int yy = y + dy, ady = dy < 0 ? -dy : dy;
+            const int w = (int)(((ady < 8 ? dlo : dhi) >> (4 * (ady & 7))) & 0xFu);
+            const int x0 = max(0, x - w), x1 = min(W - 1, x + w);
+            const uint32_t b = ((2u << (x1 - x0)) - 1u) << x0;
+            const bool row = ady <= sr && yy >= 0 && yy < H;
+            if (row && act0) atomicOr(&rows0[yy], b);
+            if (row && act1) atomicOr(&rows1[yy], b);
+        }
+    }
     DEV bool seen(const uint32_t* rows, int x, int y) const {
         const int WPR = (W + 31) >> 5;
         return (rows[y * WPR + (x >> 5)] >> (x & 31)) & 1u;
@@ -2428,6 +2447,189 @@ struct Game {
         }
         wsync();
     }
+    // writeObsPOFast for both views of a self-play game in one pass (slot0 + v renders player v's
+    // view v): the unit pass reads each unit once and paints its disk into both views' rows, the
+    // dirty chunks of both views go into one list, and each render lane takes one (view, chunk)
+    // item — half the dependent LDS rounds of two writeObsPOFast calls.  delta: bit v = view v's
+    // buffer holds its previous render (writeObsPOFast's delta).  Same output as
+    // writeObsPOFast(slot0, 0, delta & 1) followed by writeObsPOFast(slot0 + 1, 1, delta >> 1 & 1).
+    DEV void writeObsPOFast2(int slot0, uint32_t delta) {
+        const int l = lane_id(), NCW = poChunkWords(HW), NC = HW >> 2;
+        uint32_t* const rowsV0 = vis;   // [mine H][theirs H]
+        uint32_t* const rowsV1 = vis2;
+        int32_t* pr = D.po_prev ? D.po_prev + (size_t)g * D.po_words : nullptr;
+        const int SW = poSnapWords(CAP);
+        const bool d0 = delta & 1u, d1 = (delta >> 1) & 1u;
+        const int nu0 = delta ? hget(H_NU) : 0;  // the header holds the loaded unit count until store()
+        if (l < 2 * H) {
+            rowsV0[l] = 0;
+            rowsV1[l] = 0;
+        }
+        if (l < NCW) {  // [view][dirty, next pending]
+            poDirty[l] = d0 ? poPend[l] : 0u;
+            poDirty[NCW + l] = 0u;
+            poDirty[2 * NCW + l] = d1 ? poPend[NCW + l] : 0u;
+            poDirty[3 * NCW + l] = 0u;
+        }
+        const bool live = l < nu;
+        uint32_t cu = 0, sb = 0;
+        int hv = 0, rv = 0;
+        if (live) {
+            cu = uc[l];
+            sb = snap[l];
+            hv = hp[l];
+            rv = res[l];
+        }
+        const bool in0 = live && snap_in(sb, 0), in1 = live && snap_in(sb, 1);
+        const bool isDead = (cu & UC_DEAD) != 0;
+        const bool dead0 = in0 && isDead, dead1 = in1 && isDead;
+        const int cc = uy(cu) * W + ux(cu);
+        const int own = uplay(cu);
+        wsync();
+        {
+            const bool pt0 = in0 && own >= 0, pt1 = in1 && own >= 0;
+            if (ballot(pt0 || pt1))
+                paintDisks2(pt0, own == 0 ? rowsV0 : rowsV0 + H, pt1, own == 1 ? rowsV1 : rowsV1 + H, cu);
+        }
+        const uint64_t deadM0 = ballot(dead0), deadM1 = ballot(dead1);
+        if (pr && dead0) atomicOr(&poDirty[NCW + (cc >> 7)], 1u << ((cc >> 2) & 31));
+        if (pr && dead1) atomicOr(&poDirty[3 * NCW + (cc >> 7)], 1u << ((cc >> 2) & 31));
+        if (delta && (live || l < nu0)) {
+            const int cp = uy(lcu) * W + ux(lcu);
+            const uint32_t key = (uint32_t)(uint16_t)hv | ((uint32_t)(uint16_t)rv << 16);
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                if (!(v ? d1 : d0)) continue;
+                const bool in = v ? in1 : in0;
+                const bool inP = l < nu0 && ((lsnap >> v) & 1u);
+                bool chg = in != inP;
+                if (in && inP)
+                    chg = cc != cp || key != lkey || snap_act(sb, v) != (int)((lsnap >> (2 + 3 * v)) & 7u);
+                uint32_t* dirty = poDirty + 2 * v * NCW;
+                if (chg && inP) atomicOr(&dirty[cp >> 7], 1u << ((cp >> 2) & 31));
+                if (chg && in) atomicOr(&dirty[cc >> 7], 1u << ((cc >> 2) & 31));
+            }
+        }
+        wsync();
+        if (l < 2 * H) {  // sight rows: changed columns -> chunk bits of that row; the record's copies
+            const int y = l < H ? l : l - H;
+            const int k0 = y * (W >> 2);
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const uint32_t row = (v ? rowsV1 : rowsV0)[l];
+                if (v ? d1 : d0) {
+                    const uint32_t d = row ^ poVis[v * 2 * H + l];
+                    if (d) {
+                        uint32_t gbits = 0;  // bit j = column group 4j..4j+3 changed
+#pragma unroll
+                        for (int j = 0; j < 8; j++) gbits |= ((d >> (4 * j)) & 0xFu) ? (1u << j) : 0u;
+                        uint32_t* dirty = poDirty + 2 * v * NCW;
+                        if ((k0 & 31) + (W >> 2) <= 32) {
+                            atomicOr(&dirty[k0 >> 5], gbits << (k0 & 31));
+                        } else {
+                            for (uint32_t gg = gbits; gg; gg &= gg - 1) {
+                                const int k = k0 + __builtin_ctz(gg);
+                                atomicOr(&dirty[k >> 5], 1u << (k & 31));
+                            }
+                        }
+                    }
+                }
+                if (pr) pr[1 + SW + v * 2 * H + l] = (int32_t)row;
+            }
+        }
+        wsync();
+        // one list of (view << 15 | chunk) items: view 0's dirty chunks (all, without delta), then view 1's
+        int n = 0;
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const bool dv = v ? d1 : d0;
+            const uint32_t* dirty = poDirty + 2 * v * NCW;
+#pragma unroll
+            for (int c0 = 0; c0 < 256; c0 += 64) {  // NC <= 256 (H, W <= 32)
+                if (c0 < NC) {
+                    const int k = c0 + l;
+                    const bool dk = k < NC && (!dv || ((dirty[k >> 5] >> (k & 31)) & 1u));
+                    const uint64_t m = ballot(dk);
+                    if (dk) poList[n + lanes_below(m)] = (uint16_t)((v << 15) | k);
+                    n += __popcll(m);
+                }
+            }
+        }
+        if (pr && l < NCW) {
+            pr[1 + SW + 4 * H + l] = (int32_t)poDirty[NCW + l];
+            pr[1 + SW + 4 * H + NCW + l] = (int32_t)poDirty[3 * NCW + l];
+        }
+        wsync();
+        int32_t* out = D.obs + (size_t)slot0 * D.C * HW;
+        const __amdgpu_buffer_rsrc_t rs = bufRsrc(out, (uint32_t)(2 * D.C * HW * 4));
+        const uint64_t deadAny = deadM0 | deadM1;
+        for (int it = l; it < n; it += 64) {
+            const uint32_t e = poList[it];
+            const int v = (int)(e >> 15), c4 = (int)(e & 0x7FFFu);  // lane = 4 consecutive cells of one row
+            const uint64_t deadM = v ? deadM1 : deadM0;
+            const int y = (4 * c4) / W, x0 = (4 * c4) % W;
+            const uint32_t* rows = v ? rowsV1 : rowsV0;
+            int cs[4], sl[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) cs[j] = cell[4 * c4 + j];
+            const uint32_t mr = rows[y], tr = rows[H + y];
+            uint32_t ocu[4], osb[4];
+            int ohp[4], ors[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {  // the live occupant's fields (an empty cell reads slot 0, masked)
+                const int s = cs[j] < CAP ? cs[j] : 0;
+                ocu[j] = uc[s];
+                osb[j] = snap[s];
+                ohp[j] = hp[s];
+                ors[j] = res[s];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) sl[j] = (cs[j] < CAP && snap_in(osb[j], v)) ? cs[j] : -1;
+            for (uint64_t m = deadAny; m; m &= m - 1) {  // the view's dead units: a later list position wins
+                const int ds = __builtin_ctzll(m);
+                const uint32_t dcu = uniu((uint32_t)rl((int)cu, ds));
+                const int dcell = uy(dcu) * W + ux(dcu);
+                const int dh = rl(hv, ds), dr = rl(rv, ds);
+                const uint32_t dsb = uniu((uint32_t)rl((int)sb, ds));
+                const bool mine = (deadM >> ds) & 1ull;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (mine && dcell == 4 * c4 + j && ds > sl[j]) {
+                        sl[j] = ds;
+                        ocu[j] = dcu;
+                        osb[j] = dsb;
+                        ohp[j] = dh;
+                        ors[j] = dr;
+                    }
+            }
+            int vv[4][8];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool occ = sl[j] >= 0;
+                const int pl = uplay(ocu[j]);
+                const int sa = snap_act(osb[j], v);
+                vv[j][0] = occ ? ohp[j] : 0;
+                vv[j][1] = occ ? ors[j] : 0;
+                vv[j][2] = (occ && pl >= 0) ? ((pl + v) % 2) + 1 : 0;
+                vv[j][3] = occ ? utyp(ocu[j]) + 1 : 0;
+                vv[j][4] = (occ && sa) ? sa - 1 : 0;
+                vv[j][5] = cs[j] == WALL ? 1 : 0;
+                vv[j][6] = (int)((mr >> (x0 + j)) & 1u);
+                vv[j][7] = (int)((tr >> (x0 + j)) & 1u);
+            }
+            const uint32_t base = (uint32_t)(v * D.C * HW + 4 * c4) * 4u;
+            if (SC1_POOBS) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) st4sc1(rs, base + (uint32_t)(k * HW) * 4u, vv[0][k], vv[1][k], vv[2][k], vv[3][k]);
+            } else {
+                int32_t* o = out + base / 4;
+#pragma unroll
+                for (int k = 0; k < 8; k++) st4<WT_POOBS>(o + k * HW, vv[0][k], vv[1][k], vv[2][k], vv[3][k]);
+            }
+        }
+        wsync();
+    }
+    DEV bool poFast2() const { return (W & 3) == 0 && W <= 32 && H <= 32 && nu <= 64 && U.maxSight <= 15; }
     DEV void writeObsPO(int slot, int p, bool delta = false) {
         if ((W & 3) == 0 && W <= 32 && H <= 32 && nu <= 64 && U.maxSight <= 15) {
             writeObsPOFast(slot, p, delta);
@@ -3435,6 +3637,16 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
             const bool canDelta = MODE == MODE_STEP && !freshObs && D.obs_delta && D.po_prev && poDeltaShape(G.H, G.W) &&
                                   G.nu <= 64 && G.hget(H_NU) <= 64;
             const uint32_t valid = canDelta ? (uint32_t)G.hget(Game::HX_POVALID) : 0u;
+            if (selfplay && G.poFast2()) {
+                if (freshObs) {  // PO views of the reset state (snapshot(p) touches only view p's bits)
+                    G.snapshot(0);
+                    G.snapshot(1);
+                }
+#ifdef MRTS_ABLATE
+                if (!G.ab(AB_SKIP_OBS))
+#endif
+                G.writeObsPOFast2(slot0, valid & 3u);
+            } else
             for (int i = 0; i < nslots; i++) {
                 const int p = selfplay ? i : side;
                 if (freshObs) G.snapshot(p);  // PO view of the reset state
@@ -3725,7 +3937,7 @@ hipError_t phaseSpans(unsigned long long* out, int n) {  // [11][n]: starts, end
 size_t ldsBytes(int HW, int W, int CAP, int po) {
     return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 + 128 +
            (po ? 4 * (size_t)HW + 8 * (size_t)(HW / W) * (size_t)((W + 31) / 32) : 0) +
-           (po && poDeltaShape(HW / W, W) ? 4 * (4 * (size_t)(HW / W) + 4 * (size_t)poChunkWords(HW)) + 2 * (size_t)((HW / 4 + 1) & ~1) : 0) +
+           (po && poDeltaShape(HW / W, W) ? 4 * (6 * (size_t)(HW / W) + 6 * (size_t)poChunkWords(HW)) + 4 * (size_t)((HW / 4 + 1) & ~1) : 0) +
            6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (((size_t)CAP + 3) & ~(size_t)3);
 }
 // MicroRTS-Py GridnetVecEnv observation encoding (gym_microrts `_encode_obs`: clip each plane to
