@@ -44,11 +44,17 @@ constexpr int NMILE = 8;
 constexpr int mileOf(int ph) {
     return ph == 20 ? 0 : ph == 21 ? 1 : ph == 1 ? 2 : ph == 3 ? 3 : ph == 4 ? 4 : ph == 5 ? 5 : ph == 6 ? 6 : ph == 9 ? 7 : -1;
 }
+#ifdef MRTS_NO_MILESTONES  // start / end / placement only (tools/launch_gap.py)
+#define PHASE_IN(acc, tt, i) \
+    do {                     \
+    } while (0)
+#else
 #define PHASE_IN(acc, tt, i)                                                                      \
     do {                                                                                          \
         if (mileOf(i) >= 0 && threadIdx.x == 0 && (int)blockIdx.x < PH_GAMES)                      \
             g_span[(3 + mileOf(i)) * PH_GAMES + blockIdx.x] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#endif
 #else
 #define PHASE_IN(acc, tt, i)                          \
     do {                                              \
@@ -3704,8 +3710,15 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
 #ifndef MRTS_SPAN_ONLY
         for (int i = 0; i < NPH; i++) g_phase[i * PH_GAMES + G.g] += G.phAcc[i];
 #endif
-        g_span[G.g] = rt0_;
-        g_span[PH_GAMES + G.g] = __builtin_amdgcn_s_memrealtime();
+#ifdef MRTS_NO_MILESTONES
+        // odd launch stamps go to blocks 3 / 4 (free without milestones): two back-to-back launches
+        // can be compared (tools/launch_gap.py)
+        const int sb_ = (D.fwd_stamp & 1u) ? 3 : 0;
+#else
+        const int sb_ = 0;
+#endif
+        g_span[sb_ * PH_GAMES + G.g] = rt0_;
+        g_span[(sb_ + 1) * PH_GAMES + G.g] = __builtin_amdgcn_s_memrealtime();
         g_span[2 * PH_GAMES + G.g] = (unsigned long long)(uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
                                      ((unsigned long long)(__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 15) << 32) |
                                      ((unsigned long long)(nu0_ & 255) << 40) | ((unsigned long long)(G.nu & 255) << 48);
