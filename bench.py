@@ -66,10 +66,12 @@ def parse():
     ap.add_argument("--gather-obs", nargs="?", const="allgather", choices=["allgather", "learner"], default=None,
                     help="per-step RCCL exchange of the observation tensor (int16 transport, on its own stream, "
                          "overlapped with the next step): all-gather to every rank, or gather to rank 0")
-    ap.add_argument("--policy", choices=["kernel", "fused"], default="fused",
-                    help="kernel: the random policy is its own launch before each step; fused: the step kernel "
-                         "samples the next step's actions from the masks it writes (mrts_step_fused_dev, same "
-                         "Philox stream, bit-identical actions)")
+    ap.add_argument("--policy", choices=["kernel", "fused", "uniform"], default=None,
+                    help="kernel: the masked random policy is its own launch before each step; fused: the step "
+                         "kernel samples the next step's actions from the masks it writes (mrts_step_fused_dev, "
+                         "same Philox stream, bit-identical actions); uniform: SURVEY.md §8(d)'s c2 workload, "
+                         "unmasked uniform rows for every cell (mrts_policy_uniform_dev) and no masks.  Default: "
+                         "uniform for c2, fused otherwise")
     ap.add_argument("--launch", choices=["native", "graph", "eager"], default=None,
                     help="how the K timed steps are enqueued: native = one mrts_rollout_fused_dev call (K launches "
                          "from C++; fused policy only, the default there), graph = replay of a captured hipGraph "
@@ -86,12 +88,14 @@ def parse():
     a.envs = a.envs or e
     a.po = po
     a.max_units = mu
+    if a.policy is None:
+        a.policy = "uniform" if a.config == "c2" else "fused"
     if a.no_graph:
         a.launch = "eager"
     if a.launch is None:
-        a.launch = "native" if a.policy == "fused" else "graph"
-    if a.launch == "native" and a.policy != "fused":
-        ap.error("--launch native needs --policy fused")
+        a.launch = "native" if a.policy in ("fused", "uniform") else "graph"
+    if a.launch == "native" and a.policy not in ("fused", "uniform"):
+        ap.error("--launch native needs --policy fused or uniform")
     return a
 
 
@@ -143,7 +147,7 @@ class _FenceFreeEvent:
         return ms.value
 
 
-def cpu_baseline(map_path, threads, burnin):
+def cpu_baseline(map_path, threads, burnin, uniform=False):
     """The CPU oracle (C++ restatement of the Java engine; the JVM is not available) running the
     same workload: VecClient self-play + getMasks + the same Philox policy, std::thread shards."""
     from tests import oracle_py
@@ -151,14 +155,14 @@ def cpu_baseline(map_path, threads, burnin):
     L = oracle_py.load()
     games_per_thread, steps = 48, 300
     games = games_per_thread * threads
-    secs = L.oref_bench(map_path.encode(), games, steps, threads, SEED, burnin)
-    one = L.oref_bench(map_path.encode(), games_per_thread, steps, 1, SEED, burnin)
+    secs = L.oref_bench2(map_path.encode(), games, steps, threads, SEED, burnin, int(uniform))
+    one = L.oref_bench2(map_path.encode(), games_per_thread, steps, 1, SEED, burnin, int(uniform))
     return {
         "value": games * steps / secs,
         "unit": "env-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{games} self-play games x {steps} timed steps after {burnin} untimed, {threads} threads (same map/policy/masks; "
+        "sample": f"{games} self-play games x {steps} timed steps after {burnin} untimed, {threads} threads (same map/policy/masks{'' if not uniform else ' (uniform rows, no masks)'}; "
                   f"1 thread: {games_per_thread * steps / one:.0f} env-steps/s)",
     }
 
@@ -196,16 +200,21 @@ def main():
         gather_buf = mdist.ObservationGather(env.obs.shape, env.device, mode=a.gather_obs)
 
     fused = a.policy == "fused"
+    uniform = a.policy == "uniform"
     mode = {"fused": fused}
 
     def one_step(k, ev=None):
         fused = mode["fused"]
-        if not fused:
+        if uniform:
+            env.uniform_policy(SEED, k)
+        elif not fused:
             env.random_policy(SEED, k)
         if ev is not None:
             ev[0].record(torch.cuda.current_stream(env.device))
         if fused:
             env.step_fused(SEED, k + 1)  # consumes the actions of step k, writes those of step k + 1
+        elif uniform:
+            env.step(masks=False)  # c2: no masks
         else:
             env.step()
         if ev is not None:
@@ -219,7 +228,9 @@ def main():
     native_path = a.launch == "native" and gather_buf is None
 
     def run_steps(first, n):  # steps first .. first + n - 1, through the timed window's own path
-        if native_path:
+        if native_path and uniform:
+            env.rollout_uniform(SEED, first, n)
+        elif native_path:
             env.rollout_fused(SEED, first + 1, n)
         else:
             for k in range(first, first + n):
@@ -230,6 +241,9 @@ def main():
     # rows decoded per step (sum of mask[...,0]) and live units, for the algorithmic-byte count —
     # taken after the burn-in, so that the warmup steps run right before the timed window (no host
     # work leaves the GPU idle in between)
+    if uniform:  # the steps write no masks: one untimed mask write to count the idle units
+        env.get_masks()
+        env.synchronize()
     rows = float(env.masks[..., 0].sum().item()) / S
     units = []
     for s in range(0, min(S, 64), 2):
@@ -273,7 +287,9 @@ def main():
     torch.cuda.synchronize(env.device)
     env.synchronize()
     t0 = time.perf_counter()
-    if native:
+    if native and uniform:
+        env.rollout_uniform(SEED, base, a.steps)
+    elif native:
         env.rollout_fused(SEED, base + 1, a.steps)
     elif graph is not None:
         graph.replay()
@@ -313,13 +329,13 @@ def main():
     #       (2 * maskWords * 4 B) read and written; per slot the source bits (maskWords * 4 B) written.
     # SURVEY.md §8(d)'s figure assumed a full mask rewrite and all rows read; it is reported next to it.
     HW = H * W
-    MWB = 4 * ((HW + 31) // 32)
+    MWB = 0 if uniform else 4 * ((HW + 31) // 32)  # mask row sets / source bits: only with masks
     dirty = rows
     # partially observable views under the persistent-buffer contract (DeviceVecEnv obs_delta): only
     # the (plane, 4-cell chunk) pieces that changed must be written — measured on the probe steps
     po_delta = a.po and (HW % 4) == 0 and W <= 32 and H <= 32
     obs_chunks = float(C * HW // 4)
-    if env.source is not None and a.mask_mode == "delta":
+    if env.source is not None and a.mask_mode == "delta" and not uniform:
         lut = torch.tensor([bin(i).count("1") for i in range(256)], dtype=torch.int64, device=env.device)
         tot, otot, n_probe = 0, 0, 5
         for k in range(n_probe):  # untimed probe steps after the timed window
@@ -334,7 +350,7 @@ def main():
         if po_delta:
             obs_chunks = otot / (n_probe * S)
     n_games = S // 2
-    m_bytes = dirty * K if a.mask_mode == "delta" else HW * K
+    m_bytes = 0 if uniform else (dirty * K if a.mask_mode == "delta" else HW * K)
     o_bytes = obs_chunks * 16  # C * HW * 4 for a full write
     # fused policy: the idle units' rows arrive as one forwarded 4-B word each (KDyn.fwd_read), and the
     # step writes that word next to the 28-B row it leaves in the action tensor
@@ -342,7 +358,7 @@ def main():
     contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
     if fused:  # the policy's action rows (and their forwarded words) leave the step kernel too
         contract += S * (dirty if a.mask_mode == "delta" else HW) * 28 + S * rows * 4
-    survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * mean_units + 2 * HW + 16))
+    survey = S * (HW * 7 * 4 + C * HW * 4 + (0 if uniform else HW * K) + (16 * mean_units + 2 * HW + 16))
     achieved = contract / (kern_ms * 1e-3) / 1e9
     # roofline.traffic: HBM bytes per k_env launch from the rocprofv3 --pmc passes of this same command
     # (tools/gpu_profile.sh + tools/summarize_profile.py -> profiles/pmc_latest.json), when they exist
@@ -367,22 +383,27 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic (masked uniform random policy, Philox seed 0x5EEDC0DE)",
+        "data": ("synthetic (unmasked uniform random rows for every cell, Philox seed 0x5EEDC0DE)" if uniform
+                 else "synthetic (masked uniform random policy, Philox seed 0x5EEDC0DE)"),
         "parity": "bit-exact vs the C++ oracle (trace-pinned: all 280 reference traces replay exactly; Java itself "
                   "cannot run in this image) — tests/test_gpu_parity.py, tests/test_kats.py; value over the K timed "
                   "steps above",
         "config": {
-            "workload": f"{a.config}: {a.map} self-play, {E} games/GPU ({2 * E} player slots), masks+obs every step"
+            "workload": f"{a.config}: {a.map} self-play, {E} games/GPU ({2 * E} player slots), "
+                        + ("obs every step, no masks (SURVEY §8(d) c2)" if uniform else "masks+obs every step")
                         + (", partial observability" if a.po else "")
                         + (f", max_units {a.max_units} (capacity errors checked)" if a.max_units else ""),
             "envs_per_gpu": E,
             "utt": "VERSION_ORIGINAL, CANCEL_BOTH",
             "max_steps": 2000,
             "burnin_steps": a.burnin,
-            "mask_mode": a.mask_mode,
-            "launch": ("one mrts_rollout_fused_dev call (K step launches from C++)" if native
+            "mask_mode": "off" if uniform else a.mask_mode,
+            "launch": ("one mrts_rollout_uniform_dev call (K policy + K step launches from C++)" if native and uniform
+                       else "one mrts_rollout_fused_dev call (K step launches from C++)" if native
                        else "hipGraph replay of the K timed steps" if graph is not None else "eager"),
-            "policy": ("fused into the step kernel (mrts_step_fused_dev)" if fused
+            "policy": ("unmasked uniform rows, separate kernel before each step (mrts_policy_uniform_dev, inside the "
+                       "timed window)" if uniform
+                       else "fused into the step kernel (mrts_step_fused_dev)" if fused
                        else "separate masked-uniform policy kernel before each step (mrts_policy_dev)"),
             "kernel_timing": (f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
                               if (native or graph is not None) else f"{event_kind} around each step-kernel launch in the timed window"),
@@ -403,7 +424,7 @@ def main():
             "traffic_source": traffic_src,
             "kernel": "k_env<MODE_STEP>" + (" + fused policy rows" if fused else ""),
             "alg_bytes_per_launch": contract,
-            "alg_bytes_note": f"step contract bytes, {a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "
+            "alg_bytes_note": f"step contract bytes, {'no' if uniform else a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "
                               f"changed mask rows per slot" + (f", {obs_chunks:.1f} changed (plane, 4-cell chunk) "
                               f"observation pieces per slot (persistent PO views)" if po_delta else "")
                               + " (DESIGN.md §5)",
@@ -411,7 +432,7 @@ def main():
             "survey_8d_equivalent_GBps": survey / (kern_ms * 1e-3) / 1e9,
         },
     }
-    if world == 1 and (native or graph is not None) and gather_buf is None and not a.no_compare:
+    if world == 1 and (native or graph is not None) and gather_buf is None and not a.no_compare and not uniform:
         # the other policy form over the next K steps, for comparison (same contract otherwise)
         mode["fused"] = not fused
         base2 = base + a.steps + 5
@@ -433,7 +454,7 @@ def main():
         mode["fused"] = fused
         assert not env.error_flags().any()
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.po:
-        out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin)
+        out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin, uniform)
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

@@ -22,6 +22,8 @@ using namespace mrts;
 namespace mrts {
 size_t ldsBytes(int HW, int W, int CAP, int po);
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream);
+hipError_t launchPolicyUniform(int32_t* actions, int n_slots, int HW, int ntypes, int natt, uint64_t seed, uint32_t step,
+                               uint32_t slot_base, hipStream_t stream);
 #ifdef MRTS_ABLATE
 hipError_t setAblate(uint32_t v);
 #endif
@@ -978,6 +980,33 @@ int mrts_get_masks_dev(mrts_env* env, int32_t player, uint8_t* d_out, void* stre
     } catch (const Fail& f) {
         return fail(f);
     }
+}
+
+int mrts_policy_uniform_dev(mrts_env* env, uint64_t seed, uint32_t step, int32_t* d_actions, void* stream) {
+    try {
+        if (!env || !d_actions) throw Fail{-EINVAL, "null argument"};
+        if ((uintptr_t)d_actions & 3) throw Fail{-EINVAL, "misaligned buffer"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(launchPolicyUniform(d_actions, env->nSlots, env->HW, env->utt.ntypes, env->K - 23 - env->utt.ntypes, seed, step,
+                                   (uint32_t)env->slotIdBase, pickStream(env, stream)));
+        // the tensor no longer holds what a masked policy or a fused step wrote there
+        if (env->fusedActions == d_actions) env->fusedActions = nullptr;
+        if (env->lastPolicyActions == d_actions) env->polValid = false;
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                             uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps, void* stream) {
+    if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
+    for (int32_t k = 0; k < n_steps; k++) {
+        int r = mrts_policy_uniform_dev(env, seed, first_step + (uint32_t)k, d_actions, stream);
+        if (!r) r = mrts_step_dev(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, stream);
+        if (r) return r;
+    }
+    return 0;
 }
 
 int mrts_policy_invalidate(mrts_env* env) {

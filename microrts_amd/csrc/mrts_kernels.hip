@@ -4135,6 +4135,31 @@ hipError_t prepareLds(size_t bytes) {
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_PLAYOUT, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     return e;
 }
+// Unmasked uniform random policy (BASELINE config c2): every cell of every slot gets
+// type in [0, 6), the four directions in [0, 4), produce type in [0, ntypes) and attack window index
+// in [0, natt) — rows that reach every illegal -> NONE path of issueSafe.  Philox4x32-10, key = seed,
+// counter = (slot id, step, cell, UNIFORM_TAG); ranges by multiply-shift of the 32-bit words.  One
+// thread per (slot, cell): the whole action tensor, dwordx4 + dwordx3 per row.
+constexpr uint32_t UNIFORM_TAG = 0x554E4946u;  // "UNIF": a stream apart from the masked policy's (word 3 = 0)
+__global__ __launch_bounds__(64) void k_policy_uniform(int32_t* __restrict__ actions, int HW, int ntypes, int natt,
+                                                        uint64_t seed, uint32_t step, uint32_t slot_base) {
+    const int slot = (int)blockIdx.y, c = (int)(blockIdx.x * 64 + threadIdx.x);
+    if (c >= HW) return;
+    uint32_t ctr[4] = {slot_base + (uint32_t)slot, step, (uint32_t)c, UNIFORM_TAG};
+    philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    auto below = [](uint32_t r, int n) { return (int)(((uint64_t)r * (uint32_t)n) >> 32); };
+    int32_t* dst = actions + ((size_t)slot * HW + c) * 7;
+    st4u<false>(dst, below(ctr[0], 6), (int)(ctr[1] & 3u), (int)((ctr[1] >> 2) & 3u), (int)((ctr[1] >> 4) & 3u));
+    st3u<false>(dst + 4, (int)((ctr[1] >> 6) & 3u), below(ctr[2], ntypes), below(ctr[3], natt));
+}
+hipError_t launchPolicyUniform(int32_t* actions, int n_slots, int HW, int ntypes, int natt, uint64_t seed, uint32_t step,
+                               uint32_t slot_base, hipStream_t stream) {
+    if (n_slots <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_policy_uniform, dim3((unsigned)((HW + 63) / 64), (unsigned)n_slots), dim3(64), 0, stream, actions, HW,
+                       ntypes, natt, seed, step, slot_base);
+    return hipGetLastError();
+}
+
 // *prevWritten: the launch recorded its candidate set in Q.prev (a later call may use the delta form)
 hipError_t launchPolicy(const PolicyParams& Q, hipStream_t stream, bool* prevWritten) {
     dim3 grid((unsigned)((Q.HW + 63) / 64), (unsigned)Q.n_slots), block(64);

@@ -396,12 +396,32 @@ class DeviceVecEnv:
                                       self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
         self._obs_written()
 
-    def step(self, actions=None, stream=None):
+    def step(self, actions=None, stream=None, masks=True):
+        """masks=False: this step writes no masks (the masks tensor keeps its previous contents)."""
         h = self._h
         a = self.actions if actions is None else actions
         self._obs_guard()
         _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self.reward),
-                                     self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
+                                     self._p(self.done), self._p(self.masks) if masks else None, self.mask_player,
+                                     self._s(stream)))
+        self._obs_written()
+
+    def uniform_policy(self, seed, step, out=None, stream=None):
+        """Unmasked uniform random rows for every cell (BASELINE config c2; mrts_policy_uniform_dev):
+        type in [0,6), directions in [0,4), produce type in [0,ntypes), attack index in [0,K-23-ntypes)."""
+        h = self._h
+        out = self.actions if out is None else out
+        _lib.check(h.L.mrts_policy_uniform_dev(h.h, seed, step, self._p(out), self._s(stream)))
+        return out
+
+    def rollout_uniform(self, seed, first_step, n_steps, stream=None):
+        """n_steps x (uniform_policy(seed, first_step + k), then a step without masks), enqueued by
+        native code (mrts_rollout_uniform_dev): the c2 random-policy rollout."""
+        h = self._h
+        self._obs_guard()
+        _lib.check(h.L.mrts_rollout_uniform_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
+                                                self._p(self.reward), self._p(self.done), seed, first_step, n_steps,
+                                                self._s(stream)))
         self._obs_written()
 
     def step_fused(self, seed, next_step, stream=None):

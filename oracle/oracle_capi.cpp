@@ -419,6 +419,26 @@ extern "C" void oref_policy(const uint8_t* mask, int HW, int K, int n_types, uin
     }
 }
 
+// Unmasked uniform random policy (BASELINE config c2; include/mrts.h
+// mrts_policy_uniform_dev): per cell, Philox4x32-10 with counter (slot id, step, cell, "UNIF"),
+// type = 6 * w0 >> 32, directions = 2-bit fields of w1, produce type = ntypes * w2 >> 32, attack
+// index = natt * w3 >> 32 (natt = K - 23 - ntypes).
+extern "C" void oref_policy_uniform(int HW, int K, int n_types, uint64_t seed, uint32_t slot_id, uint32_t step, int32_t* out) {
+    const int natt = K - 23 - n_types;
+    for (int c = 0; c < HW; c++) {
+        uint32_t ctr[4] = {slot_id, step, (uint32_t)c, 0x554E4946u};
+        Philox::gen(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        int32_t* a = out + (size_t)c * 7;
+        a[0] = (int32_t)(((uint64_t)ctr[0] * 6u) >> 32);
+        a[1] = (int32_t)(ctr[1] & 3u);
+        a[2] = (int32_t)((ctr[1] >> 2) & 3u);
+        a[3] = (int32_t)((ctr[1] >> 4) & 3u);
+        a[4] = (int32_t)((ctr[1] >> 6) & 3u);
+        a[5] = (int32_t)(((uint64_t)ctr[2] * (uint32_t)n_types) >> 32);
+        a[6] = (int32_t)(((uint64_t)ctr[3] * (uint32_t)natt) >> 32);
+    }
+}
+
 extern "C" {
 
 const char* oref_last_error() { return g_err.c_str(); }
@@ -862,7 +882,12 @@ int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int 
 // ------------------------------------------------ CPU baseline: VecClient + random policy,
 // `threads` std::threads each stepping a disjoint shard of games (cores = threads).
 // Returns env-steps executed; *seconds = wall time of the timed region.
+double oref_bench2(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin, int uniform);
 double oref_bench(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin) {
+    return oref_bench2(map_path, n_games, steps, threads, seed, burnin, 0);
+}
+// uniform = 1: the c2 workload (unmasked uniform rows, no masks) instead of masks + masked policy
+double oref_bench2(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin, int uniform) {
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
@@ -892,6 +917,13 @@ double oref_bench(const char* map_path, int n_games, int steps, int threads, uin
                 } else {
                     cv.wait(lk, [&] { return arrived == threads; });
                 }
+            }
+            if (uniform) {
+                for (int s = 0; s < S; s++)
+                    oref_policy_uniform(H * W, K, 7, seed, (uint32_t)(t * 100000 + s), (uint32_t)(k + burnin),
+                                        acts.data() + (size_t)s * H * W * 7);
+                oref_step(h, acts.data(), nullptr, obs.data(), rew.data(), done.data());
+                continue;
             }
             oref_get_masks(h, 0, masks.data());
             for (int s = 0; s < S; s++)

@@ -65,6 +65,9 @@ def load():
         L.oref_fm_errors.argtypes = [P, I]
         L.oref_bench.restype = ctypes.c_double
         L.oref_bench.argtypes = [ctypes.c_char_p, I, I, I, U64, I]
+        L.oref_bench2.restype = ctypes.c_double
+        L.oref_bench2.argtypes = [ctypes.c_char_p, I, I, I, U64, I, I]
+        L.oref_policy_uniform.argtypes = [I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, P]
         _lib = L
     return _lib
 
@@ -172,6 +175,14 @@ def policy(mask, seed, env_id, step, player, n_types=7):
     m = np.ascontiguousarray(mask, np.uint8)
     out = np.zeros((H * W, 7), np.int32)
     L.oref_policy(_ptr(m), H * W, K, n_types, seed, env_id, step, player, _ptr(out))
+    return out
+
+
+def policy_uniform(H, W, K, seed, slot_id, step, n_types=7):
+    """Unmasked uniform random rows of one slot (bit-identical to mrts_policy_uniform_dev)."""
+    L = load()
+    out = np.zeros((H * W, 7), np.int32)
+    L.oref_policy_uniform(H * W, K, n_types, seed, slot_id, step, _ptr(out))
     return out
 
 

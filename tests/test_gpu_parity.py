@@ -726,3 +726,44 @@ def test_po_obs_delta_matches_full(mp, n_sp, n_bot, rows, max_units):
     assert not a.error_flags().any()
     a.close()
     b.close()
+
+
+def test_uniform_policy_matches_oracle():
+    """mrts_policy_uniform_dev (BASELINE config c2's unmasked uniform rows) = the oracle's restatement,
+    for every slot, several steps, with a non-zero slot_id_base."""
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    env = DeviceVecEnv(12, 0, 300, ["maps/8x8/basesWorkers8x8.xml"] * 12, seed=2, slot_id_base=40)
+    S, H, W, C, K = env.dims
+    for step in (0, 1, 7, 123456):
+        env.uniform_policy(SEED, step)
+        acts = env.actions.cpu().numpy().reshape(S, H * W, 7)
+        for s in range(S):
+            assert np.array_equal(acts[s], oracle_py.policy_uniform(H, W, K, SEED, 40 + s, step)), f"slot {s} step {step}"
+    env.close()
+
+
+@pytest.mark.parametrize("mp", ["maps/8x8/basesWorkers8x8.xml", "maps/16x16/basesWorkers16x16.xml"])
+def test_uniform_rollout_matches_oracle(mp):
+    """The c2 workload: rollout_uniform (uniform rows + a step without masks, native loop) against the
+    oracle VecClient stepped with the oracle's uniform rows — observations, rewards and dones every
+    step, the canonical state every 20 steps, and across auto-resets (max_steps 150)."""
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n = 16
+    env = DeviceVecEnv(n, 0, 150, [mp] * n, seed=4, with_masks=False)
+    ref = oracle_py.OracleVecClient(n, 0, 150, [mp] * n, seed=4)
+    S, H, W, C, K = env.dims
+    env.reset()
+    ref.reset(None)
+    _compare_step(env, ref, 0, 1, "reset")
+    for step in range(260):
+        env.rollout_uniform(SEED, step, 1)
+        acts = np.stack([oracle_py.policy_uniform(H, W, K, SEED, s, step) for s in range(S)])
+        ref.step(acts, None)
+        _compare_step(env, ref, step + 1, 20, "uniform")
+    assert not env.error_flags().any()
+    env.close()
+    ref.close()
