@@ -1,5 +1,5 @@
 set -o pipefail
-# round-2 evidence: parity suite, smoke, headline bench + rocprofv3 stats + PMC passes, c2 / c5 / full-mask lines
+# Round evidence (run through gpurun: bash tools/round_evidence.sh <tag>): parity suite, smoke, headline bench + rocprofv3 stats + PMC passes, c2 / c5 / full-mask lines
 TAG=${1:-round2_a}
 mkdir -p gpurun_out/$TAG
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$TAG/tests.log 2>&1 || exit $?
