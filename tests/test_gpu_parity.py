@@ -232,6 +232,58 @@ def test_full_size_properties():
     env.close()
 
 
+def test_full_size_c5_fused():
+    """BASELINE config c5 as bench.py runs it (2048 games, 32x32 partially observable, max_units 256,
+    the fused random policy with forwarded rows, delta masks, persistent PO views): picked games are
+    replayed by the oracle from the actions each launch consumed — observations and masks equal."""
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    E = 2048
+    mp = "maps/BWDistantResources32x32.xml"
+    env = DeviceVecEnv(2 * E, 0, 2000, [mp] * (2 * E), seed=7, partial_obs=True, max_units=256)
+    picks = [0, 1, 2 * 777, 2 * 777 + 1, 2 * E - 2, 2 * E - 1]
+    ref = oracle_py.OracleVecClient(len(picks), 0, 2000, [mp] * len(picks), seed=7, partial_obs=True)
+    env.reset()
+    ref.reset()
+    env.random_policy(SEED, 0)
+    for step in range(80):
+        acts = env.actions.cpu().numpy()[picks]  # what this launch consumes (a read: no invalidation)
+        env.step_fused(SEED, step + 1)
+        env.synchronize()
+        o, _, _ = ref.step(acts)
+        assert np.array_equal(env.obs.cpu().numpy()[picks], o), f"c5 observations diverged at step {step}"
+        assert np.array_equal(env.masks.cpu().numpy()[picks], ref.get_masks(0)), f"c5 masks diverged at step {step}"
+    assert not env.error_flags().any()
+    env.close()
+    ref.close()
+
+
+def test_full_size_c2_uniform():
+    """BASELINE config c2 as bench.py runs it (1024 games, 8x8, unmasked uniform rows, no masks, the
+    native policy + step loop): picked games replayed by the oracle with the oracle's uniform rows."""
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    E = 1024
+    mp = "maps/8x8/basesWorkers8x8.xml"
+    env = DeviceVecEnv(2 * E, 0, 2000, [mp] * (2 * E), seed=8)
+    S, H, W, C, K = env.dims
+    picks = [0, 1, 2 * 500, 2 * 500 + 1, 2 * E - 2, 2 * E - 1]
+    ref = oracle_py.OracleVecClient(len(picks), 0, 2000, [mp] * len(picks), seed=8)
+    env.reset()
+    ref.reset()
+    for step in range(120):
+        env.rollout_uniform(SEED, step, 1)
+        env.synchronize()
+        acts = np.stack([oracle_py.policy_uniform(H, W, K, SEED, s, step) for s in picks])
+        o, _, _ = ref.step(acts)
+        assert np.array_equal(env.obs.cpu().numpy()[picks], o), f"c2 observations diverged at step {step}"
+    assert not env.error_flags().any()
+    env.close()
+    ref.close()
+
+
 @pytest.mark.parametrize("mp,po,n_bot", [("maps/16x16/basesWorkers16x16.xml", False, 0),
                                           ("maps/10x10/basesWorkers10x10.xml", True, 6),
                                           ("maps/4x4/base4x4.xml", False, 4)])
