@@ -113,6 +113,11 @@ int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out /* [n_slots][H][W
 int mrts_step_rows(mrts_env* env, const int32_t* rows, int32_t n_rows, const int32_t* players, mrts_responses* out);
 /* getMasks in the Java element type: int32 [n_slots][H][W][K] (int[][][][], :307-316) */
 int mrts_get_masks_i32(mrts_env* env, int32_t player, int32_t* out);
+/* getMasks into a library-owned pinned host array, *out valid until the next call on the handle
+ * (the Java client reuses its mask array the same way, JNIGridnetClient.java:211-215); the copy runs
+ * at pinned rate instead of staging through a pageable caller buffer */
+int mrts_get_masks_host(mrts_env* env, int32_t player, const uint8_t** out);
+int mrts_get_masks_i32_host(mrts_env* env, int32_t player, const int32_t** out);
 
 /* Device-pointer API: same semantics, caller-owned HBM buffers, stream-ordered on `stream`
  * (a hipStream_t; NULL = HIP's default stream, as everywhere in HIP; mrts_stream() gives the handle's

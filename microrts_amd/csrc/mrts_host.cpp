@@ -460,6 +460,8 @@ struct mrts_env {
     uint8_t* d_done = nullptr;
     uint8_t* d_masks = nullptr;
     int32_t* h_obs = nullptr;
+    uint8_t* h_masks = nullptr;    // mrts_get_masks_host: pinned, library-owned (Java reuses its mask array)
+    int32_t* h_masks32 = nullptr;  // mrts_get_masks_i32_host
     double* h_reward = nullptr;
     uint8_t* h_done = nullptr;
     std::vector<int32_t> h_stateScratch;
@@ -1174,6 +1176,37 @@ int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out) {
     }
 }
 
+// getMasks into a library-owned pinned buffer (valid until the next call on the handle, like the Java
+// client's reused mask array, JNIGridnetClient.java:211-215): the D2H copy runs at pinned-memory rate
+// instead of staging through a pageable caller buffer
+int mrts_get_masks_host(mrts_env* env, int32_t player, const uint8_t** out) {
+    try {
+        if (!out) throw Fail{-EINVAL, "out is null"};
+        const size_t n = (size_t)env->nSlots * env->HW * env->K;
+        if (!env->h_masks) HIPCHK(hipHostMalloc(&env->h_masks, n, hipHostMallocDefault));
+        int r = mrts_get_masks(env, player, env->h_masks);
+        if (r) return r;
+        *out = env->h_masks;
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_get_masks_i32_host(mrts_env* env, int32_t player, const int32_t** out) {
+    try {
+        if (!out) throw Fail{-EINVAL, "out is null"};
+        const size_t n = (size_t)env->nSlots * env->HW * env->K;
+        if (!env->h_masks32) HIPCHK(hipHostMalloc(&env->h_masks32, n * 4, hipHostMallocDefault));
+        int r = mrts_get_masks_i32(env, player, env->h_masks32);
+        if (r) return r;
+        *out = env->h_masks32;
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
 int mrts_get_state(mrts_env* env, int32_t slot, int32_t* buf, int32_t cap) {
     try {
         if (slot < 0 || slot >= env->nSlots) throw Fail{-EINVAL, "slot out of range"};
@@ -1287,6 +1320,8 @@ void mrts_destroy(mrts_env* env) {
     (void)hipFree(env->d_done);
     (void)hipFree(env->d_masks);
     (void)hipHostFree(env->h_obs);
+    (void)hipHostFree(env->h_masks);
+    (void)hipHostFree(env->h_masks32);
     (void)hipHostFree(env->h_reward);
     (void)hipHostFree(env->h_done);
     if (env->stream) (void)hipStreamDestroy(env->stream);

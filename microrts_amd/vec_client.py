@@ -293,10 +293,19 @@ class JNIGridnetVecClient:
             _lib.check(h.L.mrts_step(h.h, a.ctypes.data_as(ctypes.c_void_p), pp, ctypes.byref(self._resp)))
         return self._responses()
 
-    def getMasks(self, player=0, dtype=np.uint8):
+    def getMasks(self, player=0, dtype=np.uint8, copy=True):
         """getMasks(int player) (:307-316) → [slots][H][W][79]; dtype np.int32 gives the Java int[][][][]
-        element type."""
+        element type.  copy=False returns a view of a library-owned pinned array that the next call
+        refills (the Java client reuses its mask array the same way, JNIGridnetClient.java:211-215) —
+        the fast form: the device-to-host copy runs at pinned-memory rate."""
         h = self._h
+        if not copy:
+            i32 = np.dtype(dtype) == np.int32
+            ptr = ctypes.c_void_p()
+            fn = h.L.mrts_get_masks_i32_host if i32 else h.L.mrts_get_masks_host
+            _lib.check(fn(h.h, player, ctypes.byref(ptr)))
+            ct = ctypes.c_int32 if i32 else ctypes.c_uint8
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), shape=(h.S, h.H, h.W, h.K))
         if np.dtype(dtype) == np.int32:
             m = np.empty((h.S, h.H, h.W, h.K), np.int32)
             _lib.check(h.L.mrts_get_masks_i32(h.h, player, m.ctypes.data_as(ctypes.c_void_p)))

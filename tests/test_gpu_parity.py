@@ -819,3 +819,25 @@ def test_uniform_rollout_matches_oracle(mp):
     assert not env.error_flags().any()
     env.close()
     ref.close()
+
+
+def test_host_mask_views_match_copies():
+    """getMasks(copy=False): views of the library-owned pinned arrays (mrts_get_masks_host /
+    mrts_get_masks_i32_host) hold the same masks as the copying form, and the next call refills them."""
+    _torch()
+    from microrts_amd import JNIGridnetVecClient, UnitTypeTable
+
+    mp = "maps/8x8/basesWorkers8x8.xml"
+    vc = JNIGridnetVecClient(8, 0, 100, ["WinLossRewardFunction"], ".", [mp] * 8, [], UnitTypeTable(), False)
+    vc.reset([0] * 8)
+    rng = np.random.default_rng(1)
+    for step in range(30):
+        a = np.stack([rng.integers(0, 6, (8, 64)), rng.integers(0, 4, (8, 64)), rng.integers(0, 4, (8, 64)),
+                      rng.integers(0, 4, (8, 64)), rng.integers(0, 4, (8, 64)), rng.integers(0, 7, (8, 64)),
+                      rng.integers(0, 49, (8, 64))], axis=-1).astype(np.int32)
+        vc.gameStep(a)
+        for dt in (np.uint8, np.int32):
+            v = vc.getMasks(0, dtype=dt, copy=False)
+            c = vc.getMasks(0, dtype=dt)
+            assert v.dtype == dt and v.shape == c.shape and np.array_equal(v, c), f"step {step} {dt}"
+    vc.close()
