@@ -66,12 +66,13 @@ def parse():
     ap.add_argument("--gather-obs", nargs="?", const="allgather", choices=["allgather", "learner"], default=None,
                     help="per-step RCCL exchange of the observation tensor (int16 transport, on its own stream, "
                          "overlapped with the next step): all-gather to every rank, or gather to rank 0")
-    ap.add_argument("--policy", choices=["kernel", "fused", "uniform"], default=None,
+    ap.add_argument("--policy", choices=["kernel", "fused", "uniform", "uniform-split"], default=None,
                     help="kernel: the masked random policy is its own launch before each step; fused: the step "
                          "kernel samples the next step's actions from the masks it writes (mrts_step_fused_dev, "
                          "same Philox stream, bit-identical actions); uniform: SURVEY.md §8(d)'s c2 workload, "
-                         "unmasked uniform rows for every cell (mrts_policy_uniform_dev) and no masks.  Default: "
-                         "uniform for c2, fused otherwise")
+                         "unmasked uniform rows for every cell and no masks, drawn and written by the step kernel "
+                         "itself (mrts_step_uniform_dev); uniform-split: the same rows from their own kernel launch "
+                         "before each step (mrts_policy_uniform_dev).  Default: uniform for c2, fused otherwise")
     ap.add_argument("--launch", choices=["native", "graph", "eager"], default=None,
                     help="how the K timed steps are enqueued: native = one mrts_rollout_fused_dev call (K launches "
                          "from C++; fused policy only, the default there), graph = replay of a captured hipGraph "
@@ -93,8 +94,8 @@ def parse():
     if a.no_graph:
         a.launch = "eager"
     if a.launch is None:
-        a.launch = "native" if a.policy in ("fused", "uniform") else "graph"
-    if a.launch == "native" and a.policy not in ("fused", "uniform"):
+        a.launch = "native" if a.policy in ("fused", "uniform", "uniform-split") else "graph"
+    if a.launch == "native" and a.policy not in ("fused", "uniform", "uniform-split"):
         ap.error("--launch native needs --policy fused or uniform")
     return a
 
@@ -200,11 +201,20 @@ def main():
         gather_buf = mdist.ObservationGather(env.obs.shape, env.device, mode=a.gather_obs)
 
     fused = a.policy == "fused"
-    uniform = a.policy == "uniform"
-    mode = {"fused": fused}
+    uniform = a.policy in ("uniform", "uniform-split")
+    mode = {"fused": fused, "uni_fused": a.policy == "uniform"}
 
     def one_step(k, ev=None):
         fused = mode["fused"]
+        if uniform and mode["uni_fused"]:  # one launch: rows drawn and written by the step kernel
+            if ev is not None:
+                ev[0].record(torch.cuda.current_stream(env.device))
+            env.step_uniform(SEED, k)
+            if ev is not None:
+                ev[1].record(torch.cuda.current_stream(env.device))
+            if gather_buf is not None:
+                gather_buf.push(env.obs)
+            return
         if uniform:
             env.uniform_policy(SEED, k)
         elif not fused:
@@ -229,7 +239,7 @@ def main():
 
     def run_steps(first, n):  # steps first .. first + n - 1, through the timed window's own path
         if native_path and uniform:
-            env.rollout_uniform(SEED, first, n)
+            env.rollout_uniform(SEED, first, n, fused=mode["uni_fused"])
         elif native_path:
             env.rollout_fused(SEED, first + 1, n)
         else:
@@ -288,7 +298,7 @@ def main():
     env.synchronize()
     t0 = time.perf_counter()
     if native and uniform:
-        env.rollout_uniform(SEED, base, a.steps)
+        env.rollout_uniform(SEED, base, a.steps, fused=mode["uni_fused"])
     elif native:
         env.rollout_fused(SEED, base + 1, a.steps)
     elif graph is not None:
@@ -354,10 +364,15 @@ def main():
     o_bytes = obs_chunks * 16  # C * HW * 4 for a full write
     # fused policy: the idle units' rows arrive as one forwarded 4-B word each (KDyn.fwd_read), and the
     # step writes that word next to the 28-B row it leaves in the action tensor
-    row_in = 4 if fused else 28
+    # fused uniform policy: no row is read (the idle units' rows are drawn in registers), and every row
+    # of the action tensor is written by the step kernel
+    uni_fused = uniform and mode["uni_fused"]
+    row_in = 4 if fused else 0 if uni_fused else 28
     contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
     if fused:  # the policy's action rows (and their forwarded words) leave the step kernel too
         contract += S * (dirty if a.mask_mode == "delta" else HW) * 28 + S * rows * 4
+    if uni_fused:
+        contract += S * HW * 28
     survey = S * (HW * 7 * 4 + C * HW * 4 + (0 if uniform else HW * K) + (16 * mean_units + 2 * HW + 16))
     achieved = contract / (kern_ms * 1e-3) / 1e9
     # roofline.traffic: HBM bytes per k_env launch from the rocprofv3 --pmc passes of this same command
@@ -398,10 +413,13 @@ def main():
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": "off" if uniform else a.mask_mode,
-            "launch": ("one mrts_rollout_uniform_dev call (K policy + K step launches from C++)" if native and uniform
+            "launch": ("one mrts_rollout_uniform_dev call (K fused policy+step launches from C++)" if native and uni_fused
+                       else "one mrts_rollout_uniform_dev call (K policy + K step launches from C++)" if native and uniform
                        else "one mrts_rollout_fused_dev call (K step launches from C++)" if native
                        else "hipGraph replay of the K timed steps" if graph is not None else "eager"),
-            "policy": ("unmasked uniform rows, separate kernel before each step (mrts_policy_uniform_dev, inside the "
+            "policy": ("unmasked uniform rows drawn and written by the step kernel (mrts_step_uniform_dev, "
+                       "bit-identical to a policy launch + a step launch)" if uni_fused
+                       else "unmasked uniform rows, separate kernel before each step (mrts_policy_uniform_dev, inside the "
                        "timed window)" if uniform
                        else "fused into the step kernel (mrts_step_fused_dev)" if fused
                        else "separate masked-uniform policy kernel before each step (mrts_policy_dev)"),
@@ -422,7 +440,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "k_env<MODE_STEP>" + (" + fused policy rows" if fused else ""),
+            "kernel": "k_env<MODE_STEP>" + (" + fused policy rows" if fused else " + fused uniform rows" if uni_fused else ""),
             "alg_bytes_per_launch": contract,
             "alg_bytes_note": f"step contract bytes, {'no' if uniform else a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "
                               f"changed mask rows per slot" + (f", {obs_chunks:.1f} changed (plane, 4-cell chunk) "
@@ -452,6 +470,18 @@ def main():
         out["other_policy_form"] = {"policy": "fused" if mode["fused"] else "kernel", "value": total_games * a.steps / t2,
                                     "ms_per_step": 1e3 * t2 / a.steps}
         mode["fused"] = fused
+        assert not env.error_flags().any()
+    if world == 1 and native and uniform and gather_buf is None and not a.no_compare:
+        # the other uniform form (fused <-> split) over the next K steps, native launches both
+        base2 = base + a.steps + 5
+        env.rollout_uniform(SEED, base2 - 5, 5, fused=not mode["uni_fused"])
+        torch.cuda.synchronize(env.device)
+        t1 = time.perf_counter()
+        env.rollout_uniform(SEED, base2, a.steps, fused=not mode["uni_fused"])
+        torch.cuda.synchronize(env.device)
+        t2 = time.perf_counter() - t1
+        out["other_policy_form"] = {"policy": "uniform-split" if mode["uni_fused"] else "uniform",
+                                    "value": total_games * a.steps / t2, "ms_per_step": 1e3 * t2 / a.steps}
         assert not env.error_flags().any()
     if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.po:
         out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin, uniform)

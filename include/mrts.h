@@ -163,10 +163,19 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
  * and attack index in [0, K-23-ntypes) — no masks needed; illegal rows become NONE in issueSafe
  * like Java's (Philox4x32-10, key = seed, counter = (slot_id_base + slot, step, cell, 0x554E4946)). */
 int mrts_policy_uniform_dev(mrts_env* env, uint64_t seed, uint32_t step, int32_t* d_actions, void* stream);
+/* mrts_policy_uniform_dev(seed, step, d_actions) followed by mrts_step_dev(d_actions, ...) in ONE
+ * launch: the step kernel writes every row of d_actions (the same values) and draws the rows of the
+ * idle units it decodes itself instead of reading them back.  Bit-identical to the two calls; one
+ * kernel launch (and one launch gap) per step instead of two. */
+int mrts_step_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
+                          uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t step,
+                          void* stream);
 /* n_steps x (mrts_policy_uniform_dev(step = first_step + k) then mrts_step_dev without masks),
- * enqueued from native code: the c2 random-policy rollout.  n_steps >= 0. */
+ * enqueued from native code: the c2 random-policy rollout.  fused != 0: each step as one
+ * mrts_step_uniform_dev launch (same results).  n_steps >= 0. */
 int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
-                             uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps, void* stream);
+                             uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps, int32_t fused,
+                             void* stream);
 /* Persistent-buffer observations (default off; always on for the library-owned buffer of the
  * host-pointer API).  When a call writes observations into the same buffer as this handle's previous
  * call did, partially observable views re-render only the 4-cell chunks whose cells can have changed

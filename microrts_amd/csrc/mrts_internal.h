@@ -147,6 +147,12 @@ struct KDyn {
     int32_t obs_delta;
     int32_t po_words;
     int32_t* po_prev;
+    // fused unmasked uniform policy (mrts_step_uniform_dev, BASELINE config c2): this launch draws
+    // its own rows (the values k_policy_uniform would write for uni_step) for the idle units it
+    // decodes and writes every row of its slots to uni_actions; null = off (rows come from `actions`)
+    int32_t* uni_actions;
+    uint64_t uni_seed;
+    uint32_t uni_step, uni_slot_base;
 };
 // PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);
 // snapshot bytes of the unit slots (after the end-of-step compaction); per view p the sight rows

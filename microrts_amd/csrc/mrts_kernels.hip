@@ -323,6 +323,24 @@ DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes
     }
 }
 
+// Unmasked uniform random row (BASELINE config c2) of cell c of slot id slotId:
+// type in [0, 6), the four directions in [0, 4), produce type in [0, ntypes), attack window index
+// in [0, natt) — rows that reach every illegal -> NONE path of issueSafe.  Philox4x32-10, key =
+// seed, counter = (slot id, step, cell, UNIFORM_TAG); ranges by multiply-shift of the 32-bit words.
+constexpr uint32_t UNIFORM_TAG = 0x554E4946u;  // "UNIF": a stream apart from the masked policy's (word 3 = 0)
+DEV void uniformRow(uint64_t seed, uint32_t step, uint32_t slotId, int c, int ntypes, int natt, int32_t a[7]) {
+    uint32_t ctr[4] = {slotId, step, (uint32_t)c, UNIFORM_TAG};
+    philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    auto below = [](uint32_t r, int n) { return (int)(((uint64_t)r * (uint32_t)n) >> 32); };
+    a[0] = below(ctr[0], 6);
+    a[1] = (int)(ctr[1] & 3u);
+    a[2] = (int)((ctr[1] >> 2) & 3u);
+    a[3] = (int)((ctr[1] >> 4) & 3u);
+    a[4] = (int)((ctr[1] >> 6) & 3u);
+    a[5] = below(ctr[2], ntypes);
+    a[6] = below(ctr[3], natt);
+}
+
 // Forwarded action word (H_FWD / stateFwdOff): the 7 values of a fused-policy row, which the sampler
 // draws as type 0..5 and parameters -1..(field size - 1): type 3 bits, the four directions 3 bits
 // each, produce type 4 bits, attack index 7 bits, each parameter stored + 1.
@@ -669,7 +687,7 @@ struct Game {
     // issuePlayer, with each lane's own unit fields (load()'s registers) instead of LDS re-reads.
     // Between steps no unit is dead; decoded rows are never parked in LDS (every idle unit's
     // assignment is written by its issue or its fill).
-    DEV void selfPlayFast(const int32_t* rows0, const int32_t* rows1) {
+    DEV void selfPlayFast(const int32_t* rows0, const int32_t* rows1, int s0) {
         const int l = lane_id();
         const uint32_t cu = lcu;
         const int pl = l < nu ? uplay(cu) : -1;
@@ -680,9 +698,7 @@ struct Game {
             // action tensor at this cell) and forwarded it in the state block
             if (idle) unpackFwd(lfwd, a);
         } else if (idle) {
-            const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)(uy(cu) * W + ux(cu)) * 7;
-#pragma unroll
-            for (int k = 0; k < 7; k++) a[k] = r[k];
+            fetchRow(pl == 0 ? rows0 : rows1, s0 + pl, uy(cu) * W + ux(cu), a);
         }
         const bool useIx = (HW + 2 * W + 31) / 32 <= 64;
         if (useIx) buildIndex();  // while the rows are in flight
@@ -770,7 +786,30 @@ struct Game {
             MPHASE(3);
         }
     }
-    DEV void predecode(const int32_t* rows0, const int32_t* rows1, int only) {
+    // Row of cell c of slot `slot` (rows = that slot's rows): the action tensor's, or, in a fused
+    // uniform-policy step (KDyn.uni_actions), the Philox row the launch also writes there
+    // (writeUniformRows) — drawn again in registers instead of read back.
+    DEV void fetchRow(const int32_t* rows, int slot, int c, int32_t a[7]) const {
+        if (D.uni_actions) {
+            uniformRow(D.uni_seed, D.uni_step, D.uni_slot_base + (uint32_t)slot, c, NT, K - 23 - NT, a);
+            return;
+        }
+        const int32_t* r = rows + (size_t)c * 7;
+#pragma unroll
+        for (int k = 0; k < 7; k++) a[k] = r[k];
+    }
+    // the fused uniform policy's output: every row of this game's slots, as k_policy_uniform writes them
+    DEV void writeUniformRows(int slot0, int nslots) const {
+        for (int i = 0; i < nslots; i++)
+            for (int c = lane_id(); c < HW; c += 64) {
+                int32_t a[7];
+                uniformRow(D.uni_seed, D.uni_step, D.uni_slot_base + (uint32_t)(slot0 + i), c, NT, K - 23 - NT, a);
+                int32_t* dst = D.uni_actions + ((size_t)(slot0 + i) * HW + c) * 7;
+                st4u<false>(dst, a[0], a[1], a[2], a[3]);
+                st3u<false>(dst + 4, a[4], a[5], a[6]);
+            }
+    }
+    DEV void predecode(const int32_t* rows0, const int32_t* rows1, int only, int s0, int s1) {
         bool bad_any = false;
         const int l = lane_id();
         // units 0..63: rows requested first, the issue index (LDS only) is built while they are in
@@ -781,11 +820,7 @@ struct Game {
             const uint32_t cu = uc[l];
             const int pl = uplay(cu);
             act = !(pl < 0 || (ua[l] & UA_PRESENT) || (only >= 0 && pl != only));
-            if (act) {
-                const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)(uy(cu) * W + ux(cu)) * 7;
-#pragma unroll
-                for (int k = 0; k < 7; k++) a[k] = r[k];
-            }
+            if (act) fetchRow(pl == 0 ? rows0 : rows1, pl == 0 ? s0 : s1, uy(cu) * W + ux(cu), a);
         }
         if (!po && (HW + 2 * W + 31) / 32 <= 64) buildIndex();
         if (act) bad_any |= decodeRow(l, a);
@@ -793,10 +828,8 @@ struct Game {
             const uint32_t cu = uc[o];
             const int pl = uplay(cu);
             if (pl < 0 || (ua[o] & UA_PRESENT) || (only >= 0 && pl != only)) continue;
-            const int32_t* r = (pl == 0 ? rows0 : rows1) + (size_t)(uy(cu) * W + ux(cu)) * 7;
             int32_t b[7];
-#pragma unroll
-            for (int k = 0; k < 7; k++) b[k] = r[k];
+            fetchRow(pl == 0 ? rows0 : rows1, pl == 0 ? s0 : s1, uy(cu) * W + ux(cu), b);
             bad_any |= decodeRow(o, b);
         }
         if (ballot(bad_any)) addErr(E_PRODUCE_TYPE);
@@ -3549,6 +3582,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
 
     if (MODE == MODE_STEP) {
         const size_t rowStride = (size_t)G.HW * 7;
+        // fused uniform policy: this step's rows go out first (fire-and-forget stores, nothing in the
+        // launch reads them back: fetchRow draws the idle units' rows again)
+        if (D.uni_actions) G.writeUniformRows(slot0, nslots);
         if (MRTS_UNLIKELY(D.reward_need & RN_COUNTS))
             if (lane_id() < 2 * RC_N) G.rwc[lane_id()] = 0;
         if (MRTS_UNLIKELY(D.reward_need & RN_CLOSER)) G.closerBefore();
@@ -3571,9 +3607,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         } else if (gtype == GT_SELFPLAY) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
             if (MRTS_LIKELY(!G.po && G.nu <= 64)) {
-                G.selfPlayFast(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride);
+                G.selfPlayFast(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, slot0);
             } else {
-            G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1);
+            G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1, slot0, slot0 + 1);
             PHASE(1);
             for (int p = 0; p < 2; p++) {
                 if (G.po) G.snapshot(p);
@@ -3591,7 +3627,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
             // JNIGridnetClient.gameStep (tests/JNIGridnetClient.java:163-203): both views are taken and
             // both actions computed before either issueSafe
             const int32_t* rows = D.actions + (size_t)slot0 * rowStride;
-            G.predecode(rows, rows, side);
+            G.predecode(rows, rows, side, slot0, slot0);
             if (G.po) {
                 G.snapshot(side);
                 G.snapshot(1 - side);
@@ -4135,22 +4171,17 @@ hipError_t prepareLds(size_t bytes) {
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_PLAYOUT, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     return e;
 }
-// Unmasked uniform random policy (BASELINE config c2): every cell of every slot gets
-// type in [0, 6), the four directions in [0, 4), produce type in [0, ntypes) and attack window index
-// in [0, natt) — rows that reach every illegal -> NONE path of issueSafe.  Philox4x32-10, key = seed,
-// counter = (slot id, step, cell, UNIFORM_TAG); ranges by multiply-shift of the 32-bit words.  One
-// thread per (slot, cell): the whole action tensor, dwordx4 + dwordx3 per row.
-constexpr uint32_t UNIFORM_TAG = 0x554E4946u;  // "UNIF": a stream apart from the masked policy's (word 3 = 0)
+// Unmasked uniform random policy (BASELINE config c2), uniformRow for every cell of
+// every slot.  One thread per (slot, cell): the whole action tensor, dwordx4 + dwordx3 per row.
 __global__ __launch_bounds__(64) void k_policy_uniform(int32_t* __restrict__ actions, int HW, int ntypes, int natt,
                                                         uint64_t seed, uint32_t step, uint32_t slot_base) {
     const int slot = (int)blockIdx.y, c = (int)(blockIdx.x * 64 + threadIdx.x);
     if (c >= HW) return;
-    uint32_t ctr[4] = {slot_base + (uint32_t)slot, step, (uint32_t)c, UNIFORM_TAG};
-    philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-    auto below = [](uint32_t r, int n) { return (int)(((uint64_t)r * (uint32_t)n) >> 32); };
+    int32_t a[7];
+    uniformRow(seed, step, slot_base + (uint32_t)slot, c, ntypes, natt, a);
     int32_t* dst = actions + ((size_t)slot * HW + c) * 7;
-    st4u<false>(dst, below(ctr[0], 6), (int)(ctr[1] & 3u), (int)((ctr[1] >> 2) & 3u), (int)((ctr[1] >> 4) & 3u));
-    st3u<false>(dst + 4, (int)((ctr[1] >> 6) & 3u), below(ctr[2], ntypes), below(ctr[3], natt));
+    st4u<false>(dst, a[0], a[1], a[2], a[3]);
+    st3u<false>(dst + 4, a[4], a[5], a[6]);
 }
 hipError_t launchPolicyUniform(int32_t* actions, int n_slots, int HW, int ntypes, int natt, uint64_t seed, uint32_t step,
                                uint32_t slot_base, hipStream_t stream) {

@@ -423,14 +423,26 @@ class DeviceVecEnv:
         _lib.check(h.L.mrts_policy_uniform_dev(h.h, seed, step, self._p(out), self._s(stream)))
         return out
 
-    def rollout_uniform(self, seed, first_step, n_steps, stream=None):
+    def step_uniform(self, seed, step, masks=False, stream=None):
+        """uniform_policy(seed, step) into env.actions, then step() on it — in one launch
+        (mrts_step_uniform_dev: the step kernel writes the rows and draws its idle units' rows itself)."""
+        h = self._h
+        self._obs_guard()
+        _lib.check(h.L.mrts_step_uniform_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
+                                             self._p(self.reward), self._p(self.done),
+                                             self._p(self.masks) if masks else None, self.mask_player, seed, step,
+                                             self._s(stream)))
+        self._obs_written()
+
+    def rollout_uniform(self, seed, first_step, n_steps, fused=True, stream=None):
         """n_steps x (uniform_policy(seed, first_step + k), then a step without masks), enqueued by
-        native code (mrts_rollout_uniform_dev): the c2 random-policy rollout."""
+        native code (mrts_rollout_uniform_dev): the c2 random-policy rollout.  fused: one
+        step_uniform launch per step (same results) instead of a policy launch + a step launch."""
         h = self._h
         self._obs_guard()
         _lib.check(h.L.mrts_rollout_uniform_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
                                                 self._p(self.reward), self._p(self.done), seed, first_step, n_steps,
-                                                self._s(stream)))
+                                                1 if fused else 0, self._s(stream)))
         self._obs_written()
 
     def step_fused(self, seed, next_step, stream=None):

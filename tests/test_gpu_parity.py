@@ -821,6 +821,51 @@ def test_uniform_rollout_matches_oracle(mp):
     ref.close()
 
 
+@pytest.mark.parametrize("mp,n_sp,n_bot,po,masks", [("maps/16x16/basesWorkers16x16.xml", 24, 0, False, False),
+                                                     ("maps/8x8/basesWorkers8x8.xml", 32, 0, False, False),
+                                                     ("maps/8x8/basesWorkers8x8.xml", 16, 6, False, True),
+                                                     ("maps/10x10/basesWorkers10x10.xml", 12, 6, True, False)])
+def test_uniform_fused_matches_split(mp, n_sp, n_bot, po, masks):
+    """mrts_step_uniform_dev (the step kernel writes the uniform rows and draws its idle units' rows
+    itself, one launch) = mrts_policy_uniform_dev + mrts_step_dev (two launches): the action tensor,
+    observations, rewards, dones (and masks) after every step, every slot's canonical state every 25
+    steps — specialised 16x16 / 8x8 kernels, the generic kernel with agent-vs-RandomBiasedAI games and
+    partially observable views, across auto-resets (max_steps 120)."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    maps = [mp] * (n_sp + n_bot)
+    bots = ["RandomBiasedAI"] * n_bot if n_bot else None
+    mk = lambda: DeviceVecEnv(n_sp, n_bot, 120, maps, seed=9, partial_obs=po, ai2s=bots, with_masks=masks,
+                              slot_id_base=7)
+    a, b = mk(), mk()
+    a.reset()
+    b.reset()
+    for step in range(300):
+        a.uniform_policy(SEED, step)
+        a.step(masks=masks)
+        b.step_uniform(SEED, step, masks=masks)
+        a.synchronize()
+        b.synchronize()
+        assert torch.equal(a.actions, b.actions), f"actions differ at step {step}"
+        assert torch.equal(a.obs, b.obs), f"observations differ at step {step}"
+        assert torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done), f"rewards / dones differ at step {step}"
+        if masks:
+            assert torch.equal(a.masks, b.masks), f"masks differ at step {step}"
+        if step % 25 == 0:
+            for s in range(a.dims[0]):
+                assert np.array_equal(a.dump_state(s), b.dump_state(s)), f"state of slot {s} differs at step {step}"
+    assert not a.error_flags().any() and not b.error_flags().any()
+    # the native rollout's fused and split forms agree too
+    a.rollout_uniform(SEED, 300, 40, fused=False)
+    b.rollout_uniform(SEED, 300, 40, fused=True)
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.actions, b.actions)
+    a.close()
+    b.close()
+
+
 def test_host_mask_views_match_copies():
     """getMasks(copy=False): views of the library-owned pinned arrays (mrts_get_masks_host /
     mrts_get_masks_i32_host) hold the same masks as the copying form, and the next call refills them."""
