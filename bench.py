@@ -291,6 +291,11 @@ def main():
         print(f"bench: fence-free events unavailable ({ex!r}); torch.cuda.Event", file=sys.stderr)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
         event_kind = "torch.cuda.Event"
+    # multi-step launches: the native fused rollout runs the K steps of every game in one k_env launch
+    # (state in LDS between steps; mrts_rollout_fused_dev), so the launch's own duration is the
+    # kernel time — fence-free events around it inside the timed window
+    multi = native and fused and env.multi_step_capable
+    roll_ev = (_FenceFreeEvent(), _FenceFreeEvent()) if multi and event_kind.startswith("hipEvent") else None
     run_steps(a.burnin, a.warmup)  # the W untimed warmup steps, immediately before the window
     if world > 1:
         dist.barrier()
@@ -300,7 +305,11 @@ def main():
     if native and uniform:
         env.rollout_uniform(SEED, base, a.steps, fused=mode["uni_fused"])
     elif native:
+        if roll_ev is not None:
+            roll_ev[0].record(stream)
         env.rollout_fused(SEED, base + 1, a.steps)
+        if roll_ev is not None:
+            roll_ev[1].record(stream)
     elif graph is not None:
         graph.replay()
     else:
@@ -326,6 +335,11 @@ def main():
     t = mdist.max_over_ranks(t, env.device)
     step_ms = [s.elapsed_time(e) for s, e in evs]
     kern_ms = float(np.mean(step_ms))
+    single_kern_ms = kern_ms  # one step per launch (the eager event pass)
+    launch_ms = None
+    if roll_ev is not None:  # the multi-step launch: its duration / K is the per-step kernel time
+        launch_ms = roll_ev[0].elapsed_time(roll_ev[1])
+        kern_ms = launch_ms / a.steps
     flags = env.error_flags()
     assert not flags.any(), f"engine error flags set: {np.unique(flags)}"
 
@@ -413,7 +427,10 @@ def main():
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": "off" if uniform else a.mask_mode,
-            "launch": ("one mrts_rollout_uniform_dev call (K fused policy+step launches from C++)" if native and uni_fused
+            "launch": ("one mrts_rollout_fused_dev call: ONE k_env launch runs the K steps of every game (multi-step "
+                       "launch, each game's state kept in LDS between its steps; every step's observation, masks, "
+                       "rewards, dones and next action rows written to HBM)" if multi
+                       else "one mrts_rollout_uniform_dev call (K fused policy+step launches from C++)" if native and uni_fused
                        else "one mrts_rollout_uniform_dev call (K policy + K step launches from C++)" if native and uniform
                        else "one mrts_rollout_fused_dev call (K step launches from C++)" if native
                        else "hipGraph replay of the K timed steps" if graph is not None else "eager"),
@@ -423,13 +440,16 @@ def main():
                        "timed window)" if uniform
                        else "fused into the step kernel (mrts_step_fused_dev)" if fused
                        else "separate masked-uniform policy kernel before each step (mrts_policy_dev)"),
-            "kernel_timing": (f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
+            "kernel_timing": (f"{event_kind} around the multi-step launch in the timed window, / K" if launch_ms is not None
+                              else f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
                               if (native or graph is not None) else f"{event_kind} around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (
                 f", per-step RCCL int16 observation {a.gather_obs} overlapped on a comm stream" if gather_buf is not None
                 else ", no collective in the step"),
         },
         "step_kernel_ms": kern_ms,
+        "launch_ms": launch_ms,
+        "single_step_launch_kernel_ms": single_kern_ms,
         "mean_units": mean_units,
         "decoded_rows_per_slot": rows,
         "roofline": {
@@ -470,6 +490,21 @@ def main():
         out["other_policy_form"] = {"policy": "fused" if mode["fused"] else "kernel", "value": total_games * a.steps / t2,
                                     "ms_per_step": 1e3 * t2 / a.steps}
         mode["fused"] = fused
+        assert not env.error_flags().any()
+    if world == 1 and multi and not a.no_compare:
+        # the same native rollout with one launch per step (mrts_set_multi_step(0)), next K steps
+        base3 = base + 2 * a.steps + 10
+        env.set_multi_step(False)
+        env.rollout_fused(SEED, base3 - 4, 5)
+        torch.cuda.synchronize(env.device)
+        t1 = time.perf_counter()
+        env.rollout_fused(SEED, base3 + 1, a.steps)
+        torch.cuda.synchronize(env.device)
+        t2 = time.perf_counter() - t1
+        env.set_multi_step(True)
+        out["single_step_launches"] = {"value": total_games * a.steps / t2, "ms_per_step": 1e3 * t2 / a.steps,
+                                       "step_kernel_ms": single_kern_ms,
+                                       "launch": "one mrts_rollout_fused_dev call issuing K single-step launches"}
         assert not env.error_flags().any()
     if world == 1 and native and uniform and gather_buf is None and not a.no_compare:
         # the other uniform form (fused <-> split) over the next K steps, native launches both

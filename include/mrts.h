@@ -152,12 +152,22 @@ int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_play
                         uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step,
                         void* stream);
 /* n_steps consecutive mrts_step_fused_dev calls (next_step = first_next_step, first_next_step + 1,
- * ...) enqueued from native code: the same launches with the same arguments, without a host
- * language's per-call overhead between them (a random-policy rollout; the outputs of the last step
- * remain in the buffers).  n_steps >= 0. */
+ * ...) enqueued from native code, without a host language's per-call overhead between them (a
+ * random-policy rollout; the outputs of the last step remain in the buffers).  n_steps >= 0.
+ * Multi-step launches (default on, mrts_set_multi_step): on full-observability self-play handles of
+ * the specialised shapes (16x16 / 8x8 maps, the built-in unit-type tables), once the handle is in the
+ * steady fused state (the previous launch was a fused step on these buffers), one launch runs up to
+ * MRTS_MAX_ITER of the steps: each game's wave keeps its state in LDS between steps and performs
+ * every step in full (decode, issue, cycle, rewards, auto-reset, observation, masks and the next
+ * action rows, all written to the buffers).  Results are bit-identical to one launch per step. */
 int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                            uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
                            int32_t n_steps, void* stream);
+#define MRTS_MAX_ITER 1024
+/* on = 0: mrts_rollout_fused_dev issues one launch per step (for comparison / debugging). */
+int mrts_set_multi_step(mrts_env* env, int32_t on);
+/* 1 when mrts_rollout_fused_dev on this handle runs several steps per launch (shape + switch), else 0. */
+int mrts_multi_step_capable(const mrts_env* env);
 /* Unmasked uniform random policy (BASELINE config c2): every row of d_actions
  * [n_slots][H*W][7] gets type in [0,6), the four directions in [0,4), produce type in [0,ntypes)
  * and attack index in [0, K-23-ntypes) — no masks needed; illegal rows become NONE in issueSafe

@@ -22,6 +22,7 @@ using namespace mrts;
 namespace mrts {
 size_t ldsBytes(int HW, int W, int CAP, int po);
 hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream);
+bool envIterable(const KStatic& hs);
 hipError_t launchPolicyUniform(int32_t* actions, int n_slots, int HW, int ntypes, int natt, uint64_t seed, uint32_t step,
                                uint32_t slot_base, hipStream_t stream);
 #ifdef MRTS_ABLATE
@@ -472,6 +473,7 @@ struct mrts_env {
     // last launch wrote observations to (null after a launch that changed the state without one, or
     // after an invalidation) and the per-game render records (PO handles on delta-capable maps)
     int obsDelta = 0;
+    int multiStep = 1;  // mrts_rollout_fused_dev may run several steps per launch (mrts_set_multi_step)
     const int32_t* lastObsPtr = nullptr;
     int32_t* d_poPrev = nullptr;
     int poWords = 0;
@@ -857,33 +859,47 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
     }
 }
 
+namespace {
+// n_iter consecutive fused steps (next_step, next_step + 1, ...) as ONE launch when the handle runs a
+// specialised full-observability self-play kernel and is in the steady fused state (the previous
+// launch was a fused step on these buffers: delta masks and policy rows, forwarded action words);
+// else one step.  Returns the number of steps enqueued.
+int stepFused(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
+              uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step, int32_t n_iter, void* stream) {
+    if (!d_actions || !d_masks) throw Fail{-EINVAL, "actions and masks are required"};
+    if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
+    HIPCHK(hipSetDevice(env->device));
+    KDyn D;
+    std::memset(&D, 0, sizeof(D));
+    D.actions = d_actions;
+    D.players = d_players;
+    D.obs = d_obs;
+    D.reward = d_reward;
+    D.done = d_done;
+    D.masks = d_masks;
+    D.mask_player = mask_player;
+    env->prepMasks(D);
+    env->prepObs(D);
+    D.pol_actions = d_actions;
+    D.pol_seed = seed;
+    D.pol_step = next_step;
+    D.pol_slot_base = env->slotIdBase;
+    D.pol_delta = (D.mask_delta && env->fusedActions == d_actions) ? 1 : 0;
+    D.fwd_read = env->fusedActions == d_actions ? 1 : 0;  // games check H_FWD == this stamp - 1
+    const bool steady = D.pol_delta && D.fwd_read && D.mask_delta && envIterable(env->hstatic);
+    D.n_iter = (steady && n_iter > 1) ? n_iter : 1;
+    HIPCHK(env->launch(0, D, pickStream(env, stream)));
+    env->fusedActions = d_actions;
+    if (env->lastPolicyActions == d_actions) env->polValid = false;  // the standalone policy's delta base is stale
+    return D.n_iter;
+}
+}  // namespace
+
 int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                         uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step,
                         void* stream) {
     try {
-        if (!d_actions || !d_masks) throw Fail{-EINVAL, "actions and masks are required"};
-        if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
-        HIPCHK(hipSetDevice(env->device));
-        KDyn D;
-        std::memset(&D, 0, sizeof(D));
-        D.actions = d_actions;
-        D.players = d_players;
-        D.obs = d_obs;
-        D.reward = d_reward;
-        D.done = d_done;
-        D.masks = d_masks;
-        D.mask_player = mask_player;
-        env->prepMasks(D);
-        env->prepObs(D);
-        D.pol_actions = d_actions;
-        D.pol_seed = seed;
-        D.pol_step = next_step;
-        D.pol_slot_base = env->slotIdBase;
-        D.pol_delta = (D.mask_delta && env->fusedActions == d_actions) ? 1 : 0;
-        D.fwd_read = env->fusedActions == d_actions ? 1 : 0;  // games check H_FWD == this stamp - 1
-        HIPCHK(env->launch(0, D, pickStream(env, stream)));
-        env->fusedActions = d_actions;
-        if (env->lastPolicyActions == d_actions) env->polValid = false;  // the standalone policy's delta base is stale
+        stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed, next_step, 1, stream);
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -894,13 +910,25 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
                            uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
                            int32_t n_steps, void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
-    for (int32_t k = 0; k < n_steps; k++) {
-        const int r = mrts_step_fused_dev(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
-                                          first_next_step + (uint32_t)k, stream);
-        if (r) return r;
+    try {
+        for (int32_t k = 0; k < n_steps;) {
+            const int32_t n = std::min<int32_t>(n_steps - k, env->multiStep ? MRTS_MAX_ITER : 1);
+            k += stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
+                           first_next_step + (uint32_t)k, n, stream);
+        }
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
     }
+}
+
+int mrts_set_multi_step(mrts_env* env, int32_t on) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    env->multiStep = on ? 1 : 0;
     return 0;
 }
+
+int mrts_multi_step_capable(const mrts_env* env) { return (env && env->multiStep && envIterable(env->hstatic)) ? 1 : 0; }
 
 int mrts_step_rows_dev(mrts_env* env, const int32_t* d_rows, int32_t n_rows, const int32_t* d_players, int32_t* d_obs,
                        double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, void* stream) {

@@ -153,6 +153,11 @@ struct KDyn {
     int32_t* uni_actions;
     uint64_t uni_seed;
     uint32_t uni_step, uni_slot_base;
+    // multi-step launch (mrts_rollout_fused_dev): > 1 = this launch runs n_iter consecutive fused steps
+    // per game (pol_step, pol_step + 1, ...), the state kept in LDS in between (specialised
+    // full-observability self-play kernels; the host issues it only in the steady fused state:
+    // pol_delta = fwd_read = mask_delta = 1)
+    int32_t n_iter;
 };
 // PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);
 // snapshot bytes of the unit slots (after the end-of-step compaction); per view p the sight rows

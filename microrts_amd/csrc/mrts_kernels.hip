@@ -366,6 +366,7 @@ struct Game {
     int g, H, W, HW, CAP;
     int K, NT, R;  // mask slots per cell, unit types, attack window (2 * max range + 1): table values or constants
     bool po;
+    bool iter;        // a multi-step kernel (KDyn.n_iter iterations per launch)
     int32_t* stBase;  // the state blocks (a leading kernel argument: preloaded into SGPRs)
     int stWords;      // words per state block (a constant in a specialised kernel)
     uint32_t* uc;    // unit core: x | y<<8 | type<<16 | (player+1)<<20 | dead<<31
@@ -409,6 +410,20 @@ struct Game {
     uint32_t G_AB = 0;
     DEV bool ab(int b) const { return (G_AB >> b) & 1u; }
 #endif
+    // lane id for the step code: threadIdx.x passed through an opaque (volatile asm) copy at the start
+    // of every iteration of a multi-step launch, so that lane-derived values are recomputed per
+    // iteration instead of being hoisted out of the loop and held in VGPRs across it (the loop alone
+    // took k_env from 67 to 166 VGPRs: 3 waves per SIMD instead of the 4 the benchmark needs)
+    // Only the multi-step kernels (iter, a compile-time constant after inlining) pay for it.
+    int lidv;
+    DEV int lid() const {
+        if (!iter) return (int)threadIdx.x;
+        __builtin_assume(lidv >= 0 && lidv < 64);
+        return lidv;
+    }
+    DEV void freshLane() {
+        if (iter) asm volatile("" : "=v"(lidv) : "0"((int)threadIdx.x));
+    }
     bool ixValid;
     bool anyMP;
     uint32_t lcu, lua;     // load(): lane l's unit core / assignment words (units 0..63) as loaded
@@ -420,15 +435,16 @@ struct Game {
     int curP;              // player whose pa is being issued
     // CloserToEnemyBase/Unit: each player's first Base before the step (x | y << 8, -1 = none) and
     // the smallest squared distance from the OTHER player's mobile units to it, before the step
-    int readySlot;         // per lane: the unit slot of ready item lane_id() (-1 outside cycle)
+    int readySlot;         // per lane: the unit slot of ready item lid() (-1 outside cycle)
+    uint32_t polStep;      // the fused policy's Philox step (D.pol_step, + 1 per iteration of a multi-step launch)
     int maxProd0, maxProd1, sumProd0, sumProd1;
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
     // array offset then folds to an immediate), else the kernel arguments
     DEV Game(const KStatic& p, const KDyn& d, int32_t* stb, int stw, uint8_t* smem, int h, int w, int hw, int cap, bool partial,
-             int k, int nt, int r)
+             int k, int nt, int r, bool iterating = false)
         : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
-          po(partial), stBase(stb), stWords(stw) {
+          po(partial), iter(iterating), stBase(stb), stWords(stw) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
         ua = (uint32_t*)q; q += 4 * CAP;
@@ -456,15 +472,17 @@ struct Game {
         fwdOn = false;
         fwdWritten = false;
         lfwd = 0;
+        polStep = d.pol_step;
+        freshLane();
     }
     // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
     enum { HX_SNAP = 16, HX_BASE = 18, HX_OLDSQ = 20, HX_POVALID = 22 };
     DEV int hget(int i) const { return uni(hdr[i]); }
     DEV void hset(int i, int v) const {
-        if (lane_id() == 0) hdr[i] = v;
+        if (lid() == 0) hdr[i] = v;
     }
     DEV void addErr(uint32_t bits) const {
-        if (lane_id() == 0) hdr[H_ERR] |= (int32_t)bits;
+        if (lid() == 0) hdr[H_ERR] |= (int32_t)bits;
     }
     DEV uint32_t errFlags() const { return (uint32_t)hget(H_ERR); }
     DEV JRand rngLoad(int i) const { return JRand{rng_of(hget(i), hget(i + 1))}; }
@@ -506,42 +524,42 @@ struct Game {
     }
     DEV void initCells() {  // terrain walls from the map template
         const int32_t* t = tmpl() + T_TERR;
-        for (int w = lane_id(); w < (HW + 3) / 4; w += 64) setTerrainWord(w, (uint32_t)t[w]);
+        for (int w = lid(); w < (HW + 3) / 4; w += 64) setTerrainWord(w, (uint32_t)t[w]);
         wsync();
     }
     DEV void copyUtt() {  // the LDS copy of the unit-type table, when load() does not fetch it
         const int32_t* ug = (const int32_t*)&P.utt;
         int32_t* ul = (int32_t*)&U;
-        for (int i = lane_id(); i < UTT_WORDS; i += 64) ul[i] = ug[i];
+        for (int i = lid(); i < UTT_WORDS; i += 64) ul[i] = ug[i];
         wsync();
     }
     DEV void storeTerrain() {  // the template's terrain words into the state block (at reset)
         const int32_t* t = tmpl() + T_TERR;
         int32_t* d = st() + stateTerrOff(CAP, HW);
-        for (int w = lane_id(); w < (HW + 3) / 4; w += 64) d[w] = t[w];
+        for (int w = lid(); w < (HW + 3) / 4; w += 64) d[w] = t[w];
     }
     DEV uint32_t* prevG() const { return (uint32_t*)(st() + H_WORDS + N_ARRAYS * CAP); }
     DEV void loadPrev() {  // previous mask row sets (delta mask writes), when not fetched by load()
         const uint32_t* pg = prevG();
-        for (int i = lane_id(); i < 2 * maskWords(HW); i += 64) mprev[i] = pg[i];
+        for (int i = lid(); i < 2 * maskWords(HW); i += 64) mprev[i] = pg[i];
         wsync();
     }
     DEV void placeUnits() {
-        for (int i = lane_id(); i < nu; i += 64) {
+        for (int i = lid(); i < nu; i += 64) {
             const uint32_t c = uc[i];
             if (!(c & UC_DEAD)) cell[uy(c) * W + ux(c)] = (uint16_t)i;
         }
         wsync();
     }
-    DEV void loadHeader(const int32_t* s) { loadHeader(lane_id() < H_WORDS ? s[lane_id()] : 0); }
-    DEV void loadHeader(int hv) {  // hv = header word lane_id() (lanes < H_WORDS)
+    DEV void loadHeader(const int32_t* s) { loadHeader(lid() < H_WORDS ? s[lid()] : 0); }
+    DEV void loadHeader(int hv) {  // hv = header word lid() (lanes < H_WORDS)
         time = rl(hv, H_TIME);
         nu = rl(hv, H_NU);
         pres0 = rl(hv, H_RES0);
         pres1 = rl(hv, H_RES1);
         seq = rl(hv, H_SEQ);
         deaths = 0;
-        const int l = lane_id();
+        const int l = lid();
         if (l < H_WORDS) hdr[l] = hv;
         else if (l < 32) hdr[l] = (l >= HX_BASE && l < HX_BASE + 2) ? -1 : (l >= HX_OLDSQ && l < HX_OLDSQ + 2) ? INF : 0;
     }
@@ -551,7 +569,7 @@ struct Game {
         const int32_t* s = st();
         const int32_t* arr = s + H_WORDS;
         const int32_t* terr = s + stateTerrOff(CAP, HW);
-        const int l = lane_id();
+        const int l = lid();
         const int TW = (HW + 3) / 4, PW = 2 * maskWords(HW);
         const int hv = l < H_WORDS ? s[l] : 0;
         const int32_t* ug = (const int32_t*)&P.utt;
@@ -625,7 +643,7 @@ struct Game {
     }
     DEV void store() {
         int32_t* s = st();
-        const int l = lane_id();
+        const int l = lid();
         int hv = l < H_WORDS ? hdr[l] : 0;
         switch (l) {
             case H_TIME: hv = time; break;
@@ -647,6 +665,26 @@ struct Game {
             st1<WT_STATE>(arr + A_AS * CAP + i, as[i]);
         }
     }
+    // Between two iterations of a multi-step launch (KDyn.n_iter): the state stays in LDS, so the
+    // registers load() would set are re-derived from it — lane l's unit words, the forwarded action
+    // word the previous iteration sampled (lfwd, kept in its register), the per-step header extras.
+    DEV void nextStep() {
+        freshLane();
+        const int l = lid();
+        wsync();
+        lcu = uc[l];  // l < 64 <= CAP; selfPlayFast ignores lanes >= nu
+        lua = ua[l];
+        fwdOn = fwdWritten;
+        // without forwarded words the next decode reads the rows the previous iteration's policy
+        // stored to the action tensor: make this wave's stores visible to its own loads first
+        if (!fwdWritten) __threadfence();
+        fwdWritten = false;
+        ixValid = false;
+        deaths = 0;
+        polStep++;
+        if (l >= H_WORDS && l < 32) hdr[l] = (l >= HX_BASE && l < HX_BASE + 2) ? -1 : (l >= HX_OLDSQ && l < HX_OLDSQ + 2) ? INF : 0;
+        wsync();
+    }
     // new GameState(PhysicalGameState.load(map)) — JNIGridnetClient.reset (tests/JNIGridnetClient.java:239-241).
     // envSteps is NOT part of it: VecClient.reset (tests/JNIGridnetVecClient.java:179-211) never touches
     // envSteps[]; only the auto-reset path zeroes it (:229,264-265,285).
@@ -660,7 +698,7 @@ struct Game {
         pres1 = t[T_RES1];
         nu = nu_t;
         const int32_t* tu = t + tmplUnits(HW);
-        for (int i = lane_id(); i < nu_t; i += 64) {
+        for (int i = lid(); i < nu_t; i += 64) {
             uc[i] = (uint32_t)tu[i];
             hp[i] = (int16_t)tu[nu_t + i];
             res[i] = (int16_t)tu[2 * nu_t + i];
@@ -670,7 +708,7 @@ struct Game {
             as[i] = 0;
         }
         wsync();
-        for (int c = lane_id(); c < HW; c += 64)
+        for (int c = lid(); c < HW; c += 64)
             if (cell[c] != WALL) cell[c] = EMPTY;
         wsync();
         placeUnits();
@@ -688,7 +726,7 @@ struct Game {
     // Between steps no unit is dead; decoded rows are never parked in LDS (every idle unit's
     // assignment is written by its issue or its fill).
     DEV void selfPlayFast(const int32_t* rows0, const int32_t* rows1, int s0) {
-        const int l = lane_id();
+        const int l = lid();
         const uint32_t cu = lcu;
         const int pl = l < nu ? uplay(cu) : -1;
         const bool idle = pl >= 0 && !(lua & UA_PRESENT);
@@ -801,7 +839,7 @@ struct Game {
     // the fused uniform policy's output: every row of this game's slots, as k_policy_uniform writes them
     DEV void writeUniformRows(int slot0, int nslots) const {
         for (int i = 0; i < nslots; i++)
-            for (int c = lane_id(); c < HW; c += 64) {
+            for (int c = lid(); c < HW; c += 64) {
                 int32_t a[7];
                 uniformRow(D.uni_seed, D.uni_step, D.uni_slot_base + (uint32_t)(slot0 + i), c, NT, K - 23 - NT, a);
                 int32_t* dst = D.uni_actions + ((size_t)(slot0 + i) * HW + c) * 7;
@@ -811,7 +849,7 @@ struct Game {
     }
     DEV void predecode(const int32_t* rows0, const int32_t* rows1, int only, int s0, int s1) {
         bool bad_any = false;
-        const int l = lane_id();
+        const int l = lid();
         // units 0..63: rows requested first, the issue index (LDS only) is built while they are in
         // flight, then decoded
         int32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -882,7 +920,7 @@ struct Game {
     DEV int rowsDecode(int p, const int32_t* rows) {
         int run0, run1;
         baseReservations(p, run0, run1);
-        const int l = lane_id();
+        const int l = lid();
         uint32_t* pairs = D.pairs + (size_t)g * D.n_rows * 2;
         int npairs = 0;
         bool badAny = false;
@@ -929,7 +967,7 @@ struct Game {
         curP = p;
         const uint32_t* pairs = D.pairs + (size_t)g * D.n_rows * 2;
         for (int b0 = 0; b0 < npairs; b0 += 64) {
-            const int k = b0 + lane_id();
+            const int k = b0 + lid();
             const bool act = k < npairs;
             int s = 0, t = 0, prm = 0, tx = 0, ty = 0, ut = 0;
             if (act) {
@@ -943,7 +981,7 @@ struct Game {
                 legality(s, t, prm, tx, ty, ut);
             }
             wsync();
-            issueBatch(act, lane_id(), min(64, npairs - b0), s, t, prm, tx, ty, ut, true);
+            issueBatch(act, lid(), min(64, npairs - b0), s, t, prm, tx, ty, ut, true);
         }
         issueFills(p, fillDur);
     }
@@ -953,10 +991,10 @@ struct Game {
     DEV void baseReservations(int p, int& r0, int& r1) {
         const int NB = (HW + 2 * W + 31) / 32;
         ixValid = false;  // `bits` now holds this view's set
-        for (int i = lane_id(); i < NB; i += 64) bits[i] = 0;
+        for (int i = lid(); i < NB; i += 64) bits[i] = 0;
         wsync();
         int s0 = 0, s1 = 0;
-        for (int o = lane_id(); o < nu; o += 64) {
+        for (int o = lid(); o < nu; o += 64) {
             const uint32_t a = ua[o];
             if (!(a & UA_PRESENT)) continue;
             if (po && !snap_in(snap[o], p)) continue;
@@ -1001,7 +1039,7 @@ struct Game {
         }
         ixValid = false;  // the chain below adds to `bits`
         for (int c0 = 0; c0 < HW; c0 += 64) {
-            const int c = c0 + lane_id();
+            const int c = c0 + lid();
             const int s = c < HW ? cell[c] : EMPTY;
             uint32_t a = 0;
             bool cand = false;
@@ -1014,14 +1052,14 @@ struct Game {
             const int t = ua_type(a), pr = par[s < CAP ? s : 0];
             int irank = 0;
             const uint64_t acc = acceptChain(p, run0, run1, cand, cand ? lanes_below(m) : -1, __popcll(m), t, pr, c, a, false, irank);
-            if ((acc >> lane_id()) & 1ull) ua[s] = a | UA_PA;
+            if ((acc >> lid()) & 1ull) ua[s] = a | UA_PA;
             wsync();
         }
     }
     // Unit-parallel form (all units in one wave): the candidates' ascending-cell order is a rank
     // computed in registers, so the serial part is the acceptance chain alone.
     DEV void decodeUnits(int p, int& run0, int& run1, bool keepBits, bool issueNow) {
-        const int o = lane_id();
+        const int o = lid();
         uint32_t a = 0, cu = 0;
         bool cand = false;
         if (o < nu) {
@@ -1079,7 +1117,7 @@ struct Game {
     // every candidate is rejected.
     DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB,
                                 bool keepBits, int& irank) {
-        const int l = lane_id();
+        const int l = lid();
         {
             // Parallel form for the common case: when no candidate's used position is reserved already,
             // no two candidates use the same position, and the base reservations plus every candidate's
@@ -1166,11 +1204,11 @@ struct Game {
                 if (sum > 0 && sum > pres1) ok = false;
             }
             if (ok) {
-                if (up && lane_id() == 0) bits[bi >> 5] |= 1u << (bi & 31);
+                if (up && lid() == 0) bits[bi >> 5] |= 1u << (bi & 31);
                 if (p == 0) run0 += cst;
                 else run1 += cst;
                 acc |= 1ull << k;
-                if (lane_id() == k) irank = nacc;
+                if (lid() == k) irank = nacc;
                 nacc++;
             }
         }
@@ -1277,7 +1315,7 @@ struct Game {
             const int ncost = nProduce ? U.cost[ut] : 0;
             bool any = false;
             for (int o0 = 0; o0 < nu; o0 += 64) {
-                const int o = o0 + lane_id();
+                const int o = o0 + lid();
                 any |= ballot(o < nu && conflicts(o, ntgt, nProduce, ncost, pl)) != 0;
             }
             int lastSeq = -1;
@@ -1285,12 +1323,12 @@ struct Game {
             const int tIn = t, utIn = ut;
             while (any) {  // rare: resolve the conflicting assignments in insertion order
                 int best = INF;
-                for (int o = lane_id(); o < nu; o += 64)
+                for (int o = lid(); o < nu; o += 64)
                     if (as[o] > lastSeq && conflicts(o, ntgt, nProduce, ncost, pl)) best = min(best, as[o]);
                 best = wave_min(best);
                 if (best == INF) break;
                 int os = INF;
-                for (int o = lane_id(); o < nu; o += 64)
+                for (int o = lid(); o < nu; o += 64)
                     if ((ua[o] & UA_PRESENT) && as[o] == best) os = o;
                 os = wave_min(os);
                 lastSeq = best;
@@ -1313,7 +1351,7 @@ struct Game {
                     const int d2 = eta(t, prm, ut, typ);
                     const int md = min(d1, d2);
                     if (cold) {
-                        if (lane_id() == 0) {
+                        if (lid() == 0) {
                             ua[os] = pack_ua(T_NONE, 0, 0, 0) | UA_PRESENT;
                             par[os] = (int16_t)md;
                             if (po) {  // the mutated UAA object is shared with the PO snapshots holding it
@@ -1335,7 +1373,7 @@ struct Game {
                 } else {  // older assignment: only the new one is cancelled (:298-317)
                     // p.m_b = NONE mutates pa's own Pair unless a cancel already replaced p: the
                     // TraceEntry (pa.clone() after issueSafe) then records NONE, not the PRODUCE
-                    if (orig && tIn == T_PRODUCE && (D.reward_need & RN_COUNTS) && lane_id() == 0) {
+                    if (orig && tIn == T_PRODUCE && (D.reward_need & RN_COUNTS) && lid() == 0) {
                         const int pc = prodCategory(U.flags[utIn]);
                         if (pc >= 0) rwc[curP * RC_N + pc] -= 1;
                     }
@@ -1350,7 +1388,7 @@ struct Game {
         // a unit with an assignment here got it from an earlier pair of this pa (Java rows may name a
         // unit twice): LinkedHashMap.put replaces the value and keeps the entry's position
         const bool again = (uniu(ua[s]) & UA_PRESENT) != 0;
-        if (lane_id() == 0) {
+        if (lid() == 0) {
             ua[s] = pack_ua(t, ut, tx, ty) | UA_PRESENT;
             par[s] = (int16_t)prm;
             at[s] = time;
@@ -1369,11 +1407,11 @@ struct Game {
 #endif
 #endif
         const int NB = (HW + 2 * W + 31) / 32;
-        for (int i = lane_id(); i < NB; i += 64) bits[i] = 0;
+        for (int i = lid(); i < NB; i += 64) bits[i] = 0;
         wsync();
         bool mp = false;
         int mc0 = -1, mc1 = -1, s0 = 0, s1 = 0;
-        for (int o = lane_id(); o < nu; o += 64) {
+        for (int o = lid(); o < nu; o += 64) {
             const uint32_t a = ua[o];
             const int t = ua_type(a);
             if (!(a & UA_PRESENT) || (t != T_MOVE && t != T_PRODUCE)) continue;
@@ -1423,7 +1461,7 @@ struct Game {
             auto cnt = [](bool b) { return (int)__popcll(ballot(b)); };
             const int c[RC_N] = {cnt(act && t == T_HARVEST), cnt(act && t == T_RETURN), cnt(act && t == T_ATTACK),
                                  cnt(pc == RC_PROD_WORKER), cnt(pc == RC_PROD_BUILDING), cnt(pc == RC_PROD_COMBAT)};
-            if (lane_id() == 0)
+            if (lid() == 0)
 #pragma unroll
                 for (int k = 0; k < RC_N; k++) rwc[curP * RC_N + k] += c[k];
         }
@@ -1518,7 +1556,7 @@ struct Game {
     DEV void issuePlayer(int p, int fillDur, bool listOrder) {
         curP = p;
         if (!listOrder && nu <= 64) {
-            const int o = lane_id();
+            const int o = lid();
             uint32_t cu = 0;
             bool isPA = false;
             if (o < nu) {
@@ -1529,7 +1567,7 @@ struct Game {
             if (m) issuePA(o, isPA, cellRank(m, isPA, uy(cu) * W + ux(cu)), __popcll(m));
         } else if (!listOrder) {
             for (int c0 = 0; c0 < HW; c0 += 64) {
-                const int c = c0 + lane_id();
+                const int c = c0 + lid();
                 const int s = c < HW ? cell[c] : EMPTY;
                 const bool isPA = s < CAP && uplay(uc[s]) == p && (ua[s] & UA_PA);
                 const uint64_t m = ballot(isPA);
@@ -1537,7 +1575,7 @@ struct Game {
             }
         } else {
             for (int o0 = 0; o0 < nu; o0 += 64) {
-                const int o = o0 + lane_id();
+                const int o = o0 + lid();
                 const bool isPA = o < nu && !(uc[o] & UC_DEAD) && uplay(uc[o]) == p && (ua[o] & UA_PA);
                 const uint64_t m = ballot(isPA);
                 if (m) issuePA(o, isPA, lanes_below(m), __popcll(m));
@@ -1548,7 +1586,7 @@ struct Game {
     // the NONE fills never conflict (issue() checks MOVE/PRODUCE only): parallel, seq in list order
     DEV void issueFills(int p, int fillDur) {
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             bool fill = false;
             if (o < nu) {
                 const uint32_t c = uc[o];
@@ -1577,14 +1615,14 @@ struct Game {
     DEV void randomBiased(int b) {
         bool anyIdle = false;
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             anyIdle |= ballot(o < nu && !(uc[o] & UC_DEAD) && uplay(uc[o]) == b && !(ua[o] & UA_PRESENT)) != 0;
         }
         if (!anyIdle) return;  // canExecuteAnyAction (rts/GameState.java:416-423): empty pa, no draws
         int run0, run1;
         baseReservations(b, run0, run1);
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             uint64_t m = ballot(o < nu && !(uc[o] & UC_DEAD) && uplay(uc[o]) == b && !(ua[o] & UA_PRESENT));
             while (m) {
                 const int k = __builtin_ctzll(m);
@@ -1622,7 +1660,7 @@ struct Game {
                 nAtk = __popc(atkDirs);
             } else {
                 for (int q0 = 0; q0 < nu; q0 += 64) {
-                    const int q = q0 + lane_id();
+                    const int q = q0 + lid();
                     bool in = false;
                     if (q < nu) {
                         const uint32_t qc = uc[q];
@@ -1670,7 +1708,7 @@ struct Game {
             } else {  // idx-th enemy in list order inside the disk
                 int seen = 0;
                 for (int q0 = 0; q0 < nu; q0 += 64) {
-                    const int q = q0 + lane_id();
+                    const int q = q0 + lid();
                     uint32_t qc = 0;
                     bool in = false;
                     if (q < nu) {
@@ -1735,7 +1773,7 @@ struct Game {
             if (sum > 0 && sum > pres1) ok = false;
         }
         if (ok) {
-            if (up && lane_id() == 0) bits[bi >> 5] |= 1u << (bi & 31);
+            if (up && lid() == 0) bits[bi >> 5] |= 1u << (bi & 31);
             if (b == 0) run0 += cst;
             else run1 += cst;
         } else {
@@ -1743,7 +1781,7 @@ struct Game {
             prm = 10;
             ut = tx = ty = 0;
         }
-        if (lane_id() == 0) {
+        if (lid() == 0) {
             ua[s] = pack_ua(t, ut, tx, ty) | UA_PA;
             par[s] = (int16_t)prm;
         }
@@ -1821,7 +1859,7 @@ struct Game {
     // unit, a uniform loop over the observers (few; painting disks costs more here).
     DEV void snapshot(int p) {
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             uint32_t cu = 0;
             bool live = false;
             if (o < nu) {
@@ -1831,7 +1869,7 @@ struct Game {
             bool vis = live && uplay(cu) == p;
             const int x = ux(cu), y = uy(cu);
             for (int q0 = 0; q0 < nu; q0 += 64) {
-                const int q = q0 + lane_id();
+                const int q = q0 + lid();
                 uint32_t qc = q < nu ? uc[q] : UC_DEAD;
                 uint64_t m = ballot(!(qc & UC_DEAD) && uplay(qc) == p);
                 while (m) {
@@ -1857,14 +1895,14 @@ struct Game {
         wsync();
     }
     DEV void clearSnap() {
-        for (int o = lane_id(); o < CAP; o += 64) snap[o] = 0;
+        for (int o = lid(); o < CAP; o += 64) snap[o] = 0;
         wsync();
     }
 
     // ------------------------------------------------------------------ cycle
     DEV void kill(int k) {  // GameState.removeUnit (rts/GameState.java:79-82)
         killedLanes |= ballot(readySlot == k);
-        if (lane_id() == 0) {
+        if (lid() == 0) {
             const uint32_t c = uc[k];
             uc[k] = c | UC_DEAD;
             cell[uy(c) * W + ux(c)] = EMPTY;
@@ -1885,12 +1923,12 @@ struct Game {
                 const int nx = x + dxo(prm), ny = y + dyo(prm);
                 if (!dead) {
                     if (uni(cell[ny * W + nx]) != EMPTY) addErr(E_COLLISION);
-                    if (lane_id() == 0) {
+                    if (lid() == 0) {
                         cell[y * W + x] = EMPTY;
                         cell[ny * W + nx] = (uint16_t)s;
                     }
                 }
-                if (lane_id() == 0) uc[s] = (cu & ~0xFFFFu) | (uint32_t)nx | ((uint32_t)ny << 8);
+                if (lid() == 0) uc[s] = (cu & ~0xFFFFu) | (uint32_t)nx | ((uint32_t)ny << 8);
                 wsync();
             } break;
             case T_ATTACK: {
@@ -1903,7 +1941,7 @@ struct Game {
                         rngStore(H_RNG_DAMAGE, rd);
                     }
                     const int nhp = uni(hp[n]) - dmg;
-                    if (lane_id() == 0) hp[n] = (int16_t)nhp;
+                    if (lid() == 0) hp[n] = (int16_t)nhp;
                     wsync();
                     if (nhp <= 0) kill(n);
                 }
@@ -1914,7 +1952,7 @@ struct Game {
                     const int n = uni(cell[ny * W + nx]);
                     if (n < CAP && (U.flags[utyp(uniu(uc[n]))] & F_RESOURCE) && (U.flags[typ] & F_HARVEST) && uni(res[s]) == 0) {
                         const int nr = uni(res[n]) - U.harvestAmt[typ];
-                        if (lane_id() == 0) {
+                        if (lid() == 0) {
                             res[n] = (int16_t)nr;
                             res[s] = (int16_t)U.harvestAmt[typ];
                         }
@@ -1930,7 +1968,7 @@ struct Game {
                     const int carried = uni(res[s]);
                     if (n < CAP && (U.flags[utyp(uniu(uc[n]))] & F_STOCKPILE) && carried > 0) {
                         addPres(pl, carried);
-                        if (lane_id() == 0) res[s] = 0;
+                        if (lid() == 0) res[s] = 0;
                         wsync();
                     }
                 }
@@ -1944,7 +1982,7 @@ struct Game {
                     } else if (nu >= CAP) {
                         addErr(E_CAPACITY);
                     } else {
-                        if (lane_id() == 0) {
+                        if (lid() == 0) {
                             uc[nu] = pack_uc(nx, ny, ut, pl);
                             hp[nu] = (int16_t)U.hp[ut];
                             res[nu] = 0;
@@ -1976,7 +2014,7 @@ struct Game {
         // gather the ready list into LDS (slot order), count R
         int R = 0;
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             bool ready = false;
             if (o < nu) {
                 const uint32_t a = ua[o];
@@ -1995,7 +2033,7 @@ struct Game {
         if (R == 0) return;
         if (R <= 64) {
             // rank by insertion sequence: lane k holds ready item k
-            const int k = lane_id();
+            const int k = lid();
             const int myseq = k < R ? rseq[k] : INF;
             const int myslot = k < R ? rslot[k] : 0;
             int rank = 0;
@@ -2031,15 +2069,15 @@ struct Game {
         } else {  // > 64 ready assignments: repeated minimum search
             while (true) {
                 int best = INF;
-                for (int o = lane_id(); o < nu; o += 64)
+                for (int o = lid(); o < nu; o += 64)
                     if (ua[o] & UA_READY) best = min(best, as[o]);
                 best = wave_min(best);
                 if (best == INF) break;
                 int os = INF;
-                for (int o = lane_id(); o < nu; o += 64)
+                for (int o = lid(); o < nu; o += 64)
                     if ((ua[o] & UA_READY) && as[o] == best) os = o;
                 os = wave_min(os);
-                if (lane_id() == 0) ua[os] &= ~(UA_READY | UA_PRESENT);
+                if (lid() == 0) ua[os] &= ~(UA_READY | UA_PRESENT);
                 wsync();
                 execute(os);
             }
@@ -2049,7 +2087,7 @@ struct Game {
     // (in parallel); NONE executes as a no-op, so only the other ready assignments are ordered — by
     // insertion sequence (unique), ranked in registers — and executed one by one from registers.
     DEV void cycleLanes() {
-        const int l = lane_id();
+        const int l = lid();
         bool ready = false;
         uint32_t a = 0, cu = 0;
         int prm = 0, sq = 0;
@@ -2083,7 +2121,7 @@ struct Game {
     DEV void outcome(bool& gameover, int& winner) {
         int c0 = 0, c1 = 0;
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             const uint32_t c = o < nu ? uc[o] : UC_DEAD;
             const bool live = !(c & UC_DEAD);
             c0 += __popcll(ballot(live && uplay(c) == 0));
@@ -2096,7 +2134,7 @@ struct Game {
     DEV bool complete() const {
         bool idle = false;
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             if (o < nu) {
                 const uint32_t c = uc[o];
                 idle |= !(c & UC_DEAD) && uplay(c) >= 0 && !(ua[o] & UA_PRESENT);
@@ -2108,7 +2146,7 @@ struct Game {
     DEV void compact() {
         int base = 0;
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             const bool alive = o < nu && !(uc[o] & UC_DEAD);
             const uint64_t m = ballot(alive);
             const int idx = base + lanes_below(m);
@@ -2140,7 +2178,7 @@ struct Game {
             base += __popcll(m);
         }
         nu = base;
-        for (int c = lane_id(); c < HW; c += 64)
+        for (int c = lid(); c < HW; c += 64)
             if (cell[c] != WALL) cell[c] = EMPTY;
         wsync();
         placeUnits();
@@ -2155,7 +2193,7 @@ struct Game {
     DEV void closerBefore() {
         int b0 = -1, b1 = -1;
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             const uint32_t c = o < nu ? uc[o] : UC_DEAD;
             const bool base = !(c & UC_DEAD) && (U.flags[utyp(c)] & N_BASE);
             const uint64_t m0 = ballot(base && uplay(c) == 0), m1 = ballot(base && uplay(c) == 1);
@@ -2173,7 +2211,7 @@ struct Game {
     DEV void closerMin(int& sq0, int& sq1) {
         const int basePos0 = hget(HX_BASE), basePos1 = hget(HX_BASE + 1);
         int m0 = INF, m1 = INF;
-        for (int o = lane_id(); o < nu; o += 64) {
+        for (int o = lid(); o < nu; o += 64) {
             const uint32_t c = uc[o];
             if ((c & UC_DEAD) || !mobileType(utyp(c))) continue;
             const int pl = uplay(c);
@@ -2200,12 +2238,12 @@ struct Game {
         bool resLeft = false;
         if (D.reward_need & RN_RESOURCES)
             for (int o0 = 0; o0 < nu; o0 += 64) {
-                const int o = o0 + lane_id();
+                const int o = o0 + lid();
                 resLeft |= ballot(o < nu && !(uc[o] & UC_DEAD) && (U.flags[utyp(uc[o])] & N_RESOURCE) && res[o] > 0) != 0;
             }
         const int k0 = (int)(D.reward_kinds4 & 15u);
         const bool done0 = k0 == RF_WINLOSS ? gameover : (k0 == RF_RESOURCE_GATHER ? !resLeft : false);
-        const int L = lane_id();
+        const int L = lid();
         if (L < nslots * R && (D.reward || D.done)) {
             const int i = L / R, j = L - i * R;
             const int p = i ? pl1 : pl0;
@@ -2258,7 +2296,7 @@ struct Game {
     DEV void writeObsFull(int slot0, int nslots, int player0) {
         int32_t* o0 = D.obs + (size_t)slot0 * D.C * HW;
         if ((HW & 3) == 0) {
-            for (int c4 = 4 * lane_id(); c4 < HW; c4 += 256) {
+            for (int c4 = 4 * lid(); c4 < HW; c4 += 256) {
                 // obsCell for 4 cells without branches: the 4 cell entries, then the occupants' 4
                 // fields each (an empty cell reads slot 0 and is masked), so the lane waits for two
                 // LDS rounds instead of one pair per occupied cell
@@ -2312,7 +2350,7 @@ struct Game {
         } else {
             for (int i = 0; i < nslots; i++) {
                 int32_t* o = o0 + (size_t)i * D.C * HW;
-                for (int c = lane_id(); c < HW; c += 64) {
+                for (int c = lid(); c < HW; c += 64) {
                     int v[6];
                     obsCell(c, player0 + i, v);
 #pragma unroll
@@ -2338,7 +2376,7 @@ struct Game {
     // map), when that unit is in the view, and the view's dead units on it (a register list: few),
     // so no per-cell scratch map is built.  Same output as the general form below.
     DEV void writeObsPOFast(int slot, int p, bool delta) {
-        const int l = lane_id(), NCW = poChunkWords(HW), NC = HW >> 2;
+        const int l = lid(), NCW = poChunkWords(HW), NC = HW >> 2;
         uint32_t* mineRows = vis;
         uint32_t* theirRows = vis + H;
         uint32_t* dirty = poDirty;
@@ -2493,7 +2531,7 @@ struct Game {
     // buffer holds its previous render (writeObsPOFast's delta).  Same output as
     // writeObsPOFast(slot0, 0, delta & 1) followed by writeObsPOFast(slot0 + 1, 1, delta >> 1 & 1).
     DEV void writeObsPOFast2(int slot0, uint32_t delta) {
-        const int l = lane_id(), NCW = poChunkWords(HW), NC = HW >> 2;
+        const int l = lid(), NCW = poChunkWords(HW), NC = HW >> 2;
         uint32_t* const rowsV0 = vis;   // [mine H][theirs H]
         uint32_t* const rowsV1 = vis2;
         int32_t* pr = D.po_prev ? D.po_prev + (size_t)g * D.po_words : nullptr;
@@ -2677,15 +2715,15 @@ struct Game {
 #ifdef MRTS_ABLATE
         if (!ab(AB_PO_NOSCELL))
 #endif
-        for (int c = lane_id(); c < HW; c += 64) scell[c] = 0;
+        for (int c = lid(); c < HW; c += 64) scell[c] = 0;
         const int NW = H * ((W + 31) >> 5);
         uint32_t* mineRows = vis;
         uint32_t* theirRows = vis + NW;
-        for (int i = lane_id(); i < 2 * NW; i += 64) vis[i] = 0;
+        for (int i = lid(); i < 2 * NW; i += 64) vis[i] = 0;
         wsync();
         const bool fastPaint = W <= 32 && U.maxSight <= 15;
         for (int o0 = 0; o0 < nu; o0 += 64) {
-            const int o = o0 + lane_id();
+            const int o = o0 + lid();
             const bool in = o < nu && snap_in(snap[o], p);
             const uint32_t cu = in ? uc[o] : 0u;
             if (in) {
@@ -2712,7 +2750,7 @@ struct Game {
         const int NC = (HW + 3) >> 2, NCW = poChunkWords(HW);
         int n = NC;  // chunks to render: all, or the dirty list (delta maps have HW % 4 == 0)
         if (delta) {
-            const int l = lane_id();
+            const int l = lid();
             if (l < NCW) poDirty[l] = poPend[p * NCW + l];
             wsync();
             const int nu0 = hget(H_NU);  // the header holds the loaded unit count until store()
@@ -2760,7 +2798,7 @@ struct Game {
             wsync();
         }
         int32_t* out = D.obs + (size_t)slot * D.C * HW;
-        for (int it = lane_id(); it < n; it += 64) {
+        for (int it = lid(); it < n; it += 64) {
             const int c4 = delta ? (int)poList[it] : it;  // lane = 4 consecutive cells, dwordx4 per plane
             int sc[4];
 #pragma unroll
@@ -2811,7 +2849,7 @@ struct Game {
     // the PO record of view p for the next write: this render's sight rows and the chunks of its units
     // that died (the compaction removes them before the next render)
     DEV void poRecord(int p) {
-        const int l = lane_id(), NCW = poChunkWords(HW), SW = poSnapWords(CAP);
+        const int l = lid(), NCW = poChunkWords(HW), SW = poSnapWords(CAP);
         int32_t* pr = D.po_prev + (size_t)g * D.po_words;
         for (int i = l; i < 2 * H; i += 64) pr[1 + SW + p * 2 * H + i] = (int32_t)vis[i];
         if (l < NCW) poDirty[l] = 0;
@@ -2831,8 +2869,8 @@ struct Game {
     DEV void poRecordSnaps(uint32_t views) {
         int32_t* pr = D.po_prev + (size_t)g * D.po_words;
         const uint32_t* sw = (const uint32_t*)snap;
-        for (int w = lane_id(); w < (nu + 3) / 4; w += 64) pr[1 + w] = (int32_t)sw[w];
-        if (lane_id() == 0) pr[0] = (int32_t)views;
+        for (int w = lid(); w < (nu + 3) / 4; w += 64) pr[1 + w] = (int32_t)sw[w];
+        if (lid() == 0) pr[0] = (int32_t)views;
     }
 
     // ------------------------------------------------------------------ legal-action masks
@@ -2924,7 +2962,7 @@ struct Game {
     DEV MaskTables maskTables() const {
         // the constant sets come with the unit-type table (host-computed, DevUtt::mt*); only the
         // affordability sets depend on the step (the players' resources now)
-        const int t = lane_id();
+        const int t = lid();
         const bool ok = t < NT;
         const int cost = ok ? U.cost[t] : 0;
         MaskTables T;
@@ -3059,7 +3097,7 @@ struct Game {
     // Park each idle unit's 79-bit mask in its unused assignment words (at/as/ua low bits).
     // pset: bit p = park the masks of player p's idle units (both players in one pass for self-play)
     DEV void stashMasks(int pset) {
-        for (int o = lane_id(); o < nu; o += 64) {
+        for (int o = lid(); o < nu; o += 64) {
             const uint32_t c = uc[o];
             const int op = uplay(c);
             if ((c & UC_DEAD) || op < 0 || !((pset >> op) & 1) || (ua[o] & UA_PRESENT)) continue;
@@ -3123,7 +3161,7 @@ struct Game {
         const int MW = maskWords(HW);
         const bool delta = D.mask_delta && (total & 15) == 0;
         uint32_t* pg = prevG();
-        const int l = lane_id();
+        const int l = lid();
         if (delta && nu <= 64 && nslots * MW <= 64 && writeMasksUnits(slot0, nslots, pl0, pl1)) return;
         int nlist = 0;
         for (int i = 0; i < nslots; i++) {
@@ -3150,6 +3188,7 @@ struct Game {
                         nlist += n;
                     }
                 }
+                if (l < 2 && w + l < MW) mprev[p * MW + w + l] = mine;  // after the read: a multi-step launch's next base
             }
         }
         MPHASE(11);
@@ -3181,7 +3220,7 @@ struct Game {
     // Returns false (nothing written) when the list would exceed 64 cells.
     DEV bool writeMasksUnits(int slot0, int nslots, int pl0, int pl1) {
         const int MW = maskWords(HW), NW = nslots * MW;
-        const int l = lane_id();
+        const int l = lid();
         uint32_t* nb = (uint32_t*)rseq;  // cycle() scratch, free here: [slot i][MW] new bits
         if (l < NW) nb[l] = 0;
         wsync();
@@ -3210,6 +3249,7 @@ struct Game {
         if (l < NW) {
             if (D.source) D.source[(size_t)(slot0 + i) * MW + w] = cur;
             prevG()[(i ? pl1 : pl0) * MW + w] = cur;
+            mprev[(i ? pl1 : pl0) * MW + w] = cur;
         }
         if (total == 0) return true;
         int k = incl - n;
@@ -3288,7 +3328,7 @@ struct Game {
     // now get a zero record (and a zero row).  Same buffer contents as stashMasks + writeMasks.
     DEV void writeMasksLanes(int slot0, int nslots, int pl0, int pl1) {
         const int MW = maskWords(HW), NW = nslots * MW;
-        const int l = lane_id();
+        const int l = lid();
         const int total = HW * K;
         uint32_t* nb = (uint32_t*)rseq;  // cycle() scratch, free here: [slot i][MW] new bits
         if (l < NW) nb[l] = 0;
@@ -3354,6 +3394,7 @@ struct Game {
             old = mprev[(i ? pl1 : pl0) * MW + w];
             if (D.source) D.source[(size_t)(slot0 + i) * MW + w] = cur;
             prevG()[(i ? pl1 : pl0) * MW + w] = cur;
+            mprev[(i ? pl1 : pl0) * MW + w] = cur;  // the next iteration's base (multi-step launch)
         }
         const bool pol = D.pol_actions && D.pol_delta;
         // forward the sampled rows of a self-play game (read by selfPlayFast next launch); K - 23 - NT
@@ -3384,17 +3425,20 @@ struct Game {
 #ifdef MRTS_ABLATE
                 if (ab(AB_POLICY)) {
                     int32_t a2[7];
-                    sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)launder(slot), NT, K,
+                    sampleBitsRaw(D.pol_seed, polStep, D.pol_slot_base + (uint32_t)launder(slot), NT, K,
                                   launder((lo >> 1) | ((uint64_t)w2 << 63)), launder((uint64_t)(w2 >> 1)), launder(c), a2);
                     keepv(a2[0] + a2[1] + a2[2] + a2[3] + a2[4] + a2[5] + a2[6]);
                 }
 #endif
-                sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
+                sampleBitsRaw(D.pol_seed, polStep, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
                               (uint64_t)(w2 >> 1), c, a);
                 int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
                 st4u<WT_MASK>(dst, a[0], a[1], a[2], a[3]);
                 st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
-                if (fwdW) st1<WT_STATE>(st() + stateFwdOff(CAP, HW) + l, (int32_t)packFwd(a));
+                if (fwdW) {
+                    lfwd = packFwd(a);  // the next iteration of a multi-step launch decodes from it
+                    st1<WT_STATE>(st() + stateFwdOff(CAP, HW) + l, (int32_t)lfwd);
+                }
             }
         }
         fwdWritten = fwdW;
@@ -3439,7 +3483,7 @@ struct Game {
         cellMaskBits(c, p, lo, hi);
         int32_t a[7];
         if (lo & 1ull) {
-            sampleBitsRaw(D.pol_seed, D.pol_step, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)hi << 63),
+            sampleBitsRaw(D.pol_seed, polStep, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)hi << 63),
                           (uint64_t)(hi >> 1), c, a);
         } else {
 #pragma unroll
@@ -3451,7 +3495,7 @@ struct Game {
     }
     DEV void writePolicyAll(int slot0, int nslots, int pl0, int pl1) const {
         for (int i = 0; i < nslots; i++)
-            for (int c = lane_id(); c < HW; c += 64) policyRow(slot0 + i, c, i ? pl1 : pl0);
+            for (int c = lid(); c < HW; c += 64) policyRow(slot0 + i, c, i ? pl1 : pl0);
     }
     // rewrite the chunks of the listed dirty cells (rslot[0..n): slot index << 15 | cell)
     DEV void flushDirty(int n, int slot0, int pl0, int pl1) {
@@ -3459,7 +3503,7 @@ struct Game {
         const int total = HW * K;
         const int NCH = (K + 14) / 16 + 1;  // chunks a K-byte record can touch
         for (int base = 0; base < NCH * n; base += 64) {
-            const int item = base + lane_id();
+            const int item = base + lid();
             if (item < NCH * n) {
                 const int k = item / NCH, t = item - k * NCH;
                 const uint32_t e = rslot[k];
@@ -3485,7 +3529,7 @@ DEV void aiGetAction(Game& G, int kind, int p) {
 // observability compile-time constants, so LDS offsets fold into immediates and the bot / Java-row
 // code vanishes — c3 (16x16, 320 slots), c2 (8x8, 128), c5 (32x32 PO, 320 slots = max_units 256).
 // FIX = 0: anything (launchEnv picks).
-template <int MODE, int FIX, int FCAP = 0, bool FPO = false>
+template <int MODE, int FIX, int FCAP = 0, bool FPO = false, bool MULTI = false>
 // stateArg and PS lead the argument list so that kernarg preloading (-amdgpu-kernarg-preload-count,
 // Makefile) hands them over in SGPRs: the first memory round (state block, unit-type table) issues
 // without waiting for a scalar load of the kernel arguments.
@@ -3493,7 +3537,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     extern __shared__ __align__(16) uint8_t smem[];
     const KStatic& P = *PS;
     Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
-           FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius);
+           FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI);
 #ifdef MRTS_ABLATE
     G.G_AB = g_ablate;
 #endif
@@ -3530,20 +3574,35 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
 #ifdef MRTS_ABLATE
         if (G.ab(AB_LOAD)) G.load(D.mask_delta && D.masks);
 #endif
+    }
+    // Multi-step launch (MULTI instances: mrts_rollout_fused_dev on the specialised full-observability
+    // self-play shapes): the game runs D.n_iter consecutive fused steps with its state in LDS — each
+    // iteration is one whole step (decode, issue, cycle, rewards, auto-reset, observation, masks, next
+    // rows, all written to their buffers) — and stores the state once at the end.  A separate
+    // instance: the loop changes register allocation (values live across iterations), and the
+    // single-step kernels must not pay for it.
+    const int kind = FIX ? GT_SELFPLAY : G.hget(H_KIND);
+    const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
+    const bool external = gtype != GT_BOT_VS_BOT;  // bot-only clients return no observation / masks
+    const int niter = MULTI ? D.n_iter : 1;
+    for (int it = 0; it < niter; it++) {
+    if (it > 0) {
+        G.nextStep();
+        freshObs = true;
+    }
+    if (MODE != MODE_RESET) {
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
-        {
-            const int q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
-            if (q == 1) __builtin_amdgcn_s_setprio(1);
-            else if (q == 2) __builtin_amdgcn_s_setprio(2);
-            else if (q == 3) __builtin_amdgcn_s_setprio(3);
-        }
+        const int q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
+        if (q == 0) {
+            if (it > 0) __builtin_amdgcn_s_setprio(0);
+        } else if (q == 1) __builtin_amdgcn_s_setprio(1);
+        else if (q == 2) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(3);
     }
 #ifdef MRTS_PHASE_TIMING
     const int nu0_ = G.nu;
 #endif
-    const int kind = FIX ? GT_SELFPLAY : G.hget(H_KIND);
-    const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
     if (G.po) G.clearSnap();
     PHASE(0);
 
@@ -3671,7 +3730,6 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         PHASE(5);
     }
 
-    const bool external = gtype != GT_BOT_VS_BOT;  // bot-only clients return no observation / masks
     if (MODE != MODE_MASKS && D.obs && external) {
         if (G.po) {
             // persistent buffer: the views the previous write rendered for this game can be updated
@@ -3731,6 +3789,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         }
         PHASE(9);
     }
+    }  // iterations
     if (MODE != MODE_MASKS) {
         wsync();
         if (G.po && D.obs && external && D.po_prev && poDeltaShape(G.H, G.W))
@@ -4153,7 +4212,9 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
     auto is = [&](int w, int cap, bool po) { return fixable && hs.W == w && hs.CAP == cap && (hs.partial_obs != 0) == po; };
     switch (mode) {
         case MODE_STEP:
-            if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
+            if (D.n_iter > 1 && is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false, true>), grid, block, lds, stream, D.state, ds, D);
+            else if (D.n_iter > 1 && is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true>), grid, block, lds, stream, D.state, ds, D);
+            else if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
             else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, D.state, ds, D);
             else if (is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, D.state, ds, D);
             else hipLaunchKernelGGL((k_env<MODE_STEP, 0>), grid, block, lds, stream, D.state, ds, D);
@@ -4163,6 +4224,13 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
         default:hipLaunchKernelGGL((k_env<MODE_MASKS, 0>), grid, block, lds, stream, D.state, ds, D); break;
     }
     return hipGetLastError();
+}
+// launchEnv(MODE_STEP) would run a specialised full-observability self-play kernel, the one whose
+// games can iterate several steps in one launch (KDyn.n_iter)
+bool envIterable(const KStatic& hs) {
+    const bool fixable = hs.n_sp_games == hs.n_games && hs.utt.K == 79 && hs.utt.ntypes == 7 && hs.utt.maxAttackRadius == 7 &&
+                         hs.H == hs.W && !hs.partial_obs;
+    return fixable && ((hs.W == 16 && hs.CAP == 320) || (hs.W == 8 && hs.CAP == 128));
 }
 hipError_t prepareLds(size_t bytes) {
     hipError_t e = hipFuncSetAttribute((const void*)k_env<MODE_STEP, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

@@ -459,9 +459,20 @@ class DeviceVecEnv:
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
+    def set_multi_step(self, on):
+        """rollout_fused may run several steps per launch (default; mrts_set_multi_step)."""
+        _lib.check(self._h.L.mrts_set_multi_step(self._h.h, 1 if on else 0))
+
+    @property
+    def multi_step_capable(self):
+        """rollout_fused runs several steps per launch on this handle (mrts_multi_step_capable)."""
+        return bool(self._h.L.mrts_multi_step_capable(self._h.h))
+
     def rollout_fused(self, seed, first_next_step, n_steps, stream=None):
         """n_steps step_fused calls (next_step = first_next_step, first_next_step + 1, ...) enqueued by
-        native code (mrts_rollout_fused_dev): identical launches, no Python between them."""
+        native code (mrts_rollout_fused_dev): no Python between them; on the specialised
+        full-observability self-play shapes, in the steady fused state, up to MRTS_MAX_ITER steps per
+        launch (each game's state kept in LDS between its steps) — bit-identical results."""
         h = self._h
         assert self.masks is not None, "the fused policy samples from the masks"
         if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:

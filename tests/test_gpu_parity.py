@@ -714,6 +714,56 @@ def test_native_rollout_matches_fused_steps(mp, n_sp):
     del torch
 
 
+@pytest.mark.parametrize("mp,n_sp,max_steps", [("maps/16x16/basesWorkers16x16.xml", 48, 300),
+                                                ("maps/8x8/basesWorkers8x8.xml", 64, 150),
+                                                ("maps/16x16/EightBasesWorkers16x16.xml", 8, 2000)])
+def test_multi_step_rollout_matches_single_launches(mp, n_sp, max_steps):
+    """Multi-step launches (mrts_rollout_fused_dev running up to MRTS_MAX_ITER steps per game in one
+    launch, state kept in LDS between steps) = one launch per step (mrts_set_multi_step(0)), bit for
+    bit: observations, rewards, dones, masks, source bits, next actions, env steps and every game's
+    state — rollouts of 1 .. 250 steps across auto-resets, games above 64 units (EightBasesWorkers:
+    the multi-block decode, mask and non-forwarded row paths inside the loop), then single fused
+    steps, a plain step and a mask write after the multi-step launches (handle bookkeeping)."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mk = lambda: DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=5)  # noqa: E731
+    A, B = mk(), mk()
+    A.set_multi_step(False)
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+    names = ("obs", "reward", "done", "masks", "actions", "source")
+
+    def same(tag):
+        A.synchronize()
+        B.synchronize()
+        for name in names:
+            assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} {tag}"
+        for s in range(0, n_sp, 2):
+            assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} {tag}"
+        assert np.array_equal(A._h.env_steps(), B._h.env_steps()), f"env steps {tag}"
+
+    k = 0
+    for n in (1, 2, 5, 64, 250):
+        A.rollout_fused(SEED, k + 1, n)
+        B.rollout_fused(SEED, k + 1, n)
+        k += n
+        same(f"after rollout to {k}")
+    for e in (A, B):
+        e.step_fused(SEED, k + 1)
+        e.step_fused(SEED, k + 2)
+    same("after single fused steps")
+    for e in (A, B):
+        e.rollout_fused(SEED, k + 3, 30)
+        e.step()
+        e.rollout_fused(SEED, k + 40, 20)  # not in the steady state: first step alone, then a loop
+    same("after a plain step between rollouts")
+    assert not A.error_flags().any() and not B.error_flags().any()
+    A.close()
+    B.close()
+
+
 @pytest.mark.parametrize("mp,n_sp,n_bot,rows,max_units", [
     ("maps/BWDistantResources32x32.xml", 8, 4, False, 256),
     ("maps/16x16/basesWorkers16x16.xml", 16, 4, False, 0),
