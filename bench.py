@@ -294,7 +294,7 @@ def main():
     # multi-step launches: the native fused rollout runs the K steps of every game in one k_env launch
     # (state in LDS between steps; mrts_rollout_fused_dev), so the launch's own duration is the
     # kernel time — fence-free events around it inside the timed window
-    multi = native and fused and env.multi_step_capable
+    multi = native and (fused or (uniform and mode["uni_fused"])) and env.multi_step_capable
     roll_ev = (_FenceFreeEvent(), _FenceFreeEvent()) if multi and event_kind.startswith("hipEvent") else None
     run_steps(a.burnin, a.warmup)  # the W untimed warmup steps, immediately before the window
     if world > 1:
@@ -303,7 +303,11 @@ def main():
     env.synchronize()
     t0 = time.perf_counter()
     if native and uniform:
+        if roll_ev is not None:
+            roll_ev[0].record(stream)
         env.rollout_uniform(SEED, base, a.steps, fused=mode["uni_fused"])
+        if roll_ev is not None:
+            roll_ev[1].record(stream)
     elif native:
         if roll_ev is not None:
             roll_ev[0].record(stream)
@@ -427,7 +431,7 @@ def main():
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": "off" if uniform else a.mask_mode,
-            "launch": ("one mrts_rollout_fused_dev call: ONE k_env launch runs the K steps of every game (multi-step "
+            "launch": (f"one {'mrts_rollout_uniform_dev' if uniform else 'mrts_rollout_fused_dev'} call: ONE k_env launch runs the K steps of every game (multi-step "
                        "launch, each game's state kept in LDS between its steps; every step's observation, masks, "
                        "rewards, dones and next action rows written to HBM)" if multi
                        else "one mrts_rollout_uniform_dev call (K fused policy+step launches from C++)" if native and uni_fused
@@ -495,16 +499,18 @@ def main():
         # the same native rollout with one launch per step (mrts_set_multi_step(0)), next K steps
         base3 = base + 2 * a.steps + 10
         env.set_multi_step(False)
-        env.rollout_fused(SEED, base3 - 4, 5)
+        roll = (lambda f, n: env.rollout_uniform(SEED, f, n)) if uniform else (lambda f, n: env.rollout_fused(SEED, f, n))
+        roll(base3 - 4, 5)
         torch.cuda.synchronize(env.device)
         t1 = time.perf_counter()
-        env.rollout_fused(SEED, base3 + 1, a.steps)
+        roll(base3 + 1, a.steps)
         torch.cuda.synchronize(env.device)
         t2 = time.perf_counter() - t1
         env.set_multi_step(True)
         out["single_step_launches"] = {"value": total_games * a.steps / t2, "ms_per_step": 1e3 * t2 / a.steps,
                                        "step_kernel_ms": single_kern_ms,
-                                       "launch": "one mrts_rollout_fused_dev call issuing K single-step launches"}
+                                       "launch": f"one {'mrts_rollout_uniform_dev' if uniform else 'mrts_rollout_fused_dev'} "
+                                                 "call issuing K single-step launches"}
         assert not env.error_flags().any()
     if world == 1 and native and uniform and gather_buf is None and not a.no_compare:
         # the other uniform form (fused <-> split) over the next K steps, native launches both

@@ -182,7 +182,8 @@ int mrts_step_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_pl
                           void* stream);
 /* n_steps x (mrts_policy_uniform_dev(step = first_step + k) then mrts_step_dev without masks),
  * enqueued from native code: the c2 random-policy rollout.  fused != 0: each step as one
- * mrts_step_uniform_dev launch (same results).  n_steps >= 0. */
+ * mrts_step_uniform_dev launch, or — on the multi-step shapes of mrts_rollout_fused_dev, unless
+ * mrts_set_multi_step(env, 0) — up to MRTS_MAX_ITER steps per launch (same results).  n_steps >= 0. */
 int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                              uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps, int32_t fused,
                              void* stream);

@@ -1028,32 +1028,44 @@ int mrts_policy_uniform_dev(mrts_env* env, uint64_t seed, uint32_t step, int32_t
     }
 }
 
+namespace {
+// n_iter fused uniform steps (step, step + 1, ...) as ONE launch on the multi-step shapes (the rows
+// are drawn in the kernel, so no steady state is needed), else one.  Returns the steps enqueued.
+int stepUniform(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
+                uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t step, int32_t n_iter, void* stream) {
+    if (!env || !d_actions) throw Fail{-EINVAL, "null argument"};
+    if ((uintptr_t)d_actions & 3) throw Fail{-EINVAL, "misaligned buffer"};
+    if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
+    HIPCHK(hipSetDevice(env->device));
+    KDyn D;
+    std::memset(&D, 0, sizeof(D));
+    D.actions = d_actions;
+    D.players = d_players;
+    D.obs = d_obs;
+    D.reward = d_reward;
+    D.done = d_done;
+    D.masks = d_masks;
+    D.mask_player = mask_player;
+    env->prepMasks(D);
+    env->prepObs(D);
+    D.uni_actions = d_actions;
+    D.uni_seed = seed;
+    D.uni_step = step;
+    D.uni_slot_base = (uint32_t)env->slotIdBase;
+    // masks in a loop need the delta row sets of the previous write (kept in LDS between iterations)
+    const bool loopable = envIterable(env->hstatic) && (!d_masks || D.mask_delta);
+    D.n_iter = (loopable && n_iter > 1) ? n_iter : 1;
+    if (d_masks || env->fusedActions == d_actions) env->fusedActions = nullptr;
+    if (env->lastPolicyActions == d_actions) env->polValid = false;
+    HIPCHK(env->launch(0, D, pickStream(env, stream)));
+    return D.n_iter;
+}
+}  // namespace
+
 int mrts_step_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                           uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t step, void* stream) {
     try {
-        if (!env || !d_actions) throw Fail{-EINVAL, "null argument"};
-        if ((uintptr_t)d_actions & 3) throw Fail{-EINVAL, "misaligned buffer"};
-        if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
-        HIPCHK(hipSetDevice(env->device));
-        KDyn D;
-        std::memset(&D, 0, sizeof(D));
-        D.actions = d_actions;
-        D.players = d_players;
-        D.obs = d_obs;
-        D.reward = d_reward;
-        D.done = d_done;
-        D.masks = d_masks;
-        D.mask_player = mask_player;
-        env->prepMasks(D);
-        env->prepObs(D);
-        D.uni_actions = d_actions;
-        D.uni_seed = seed;
-        D.uni_step = step;
-        D.uni_slot_base = (uint32_t)env->slotIdBase;
-        // the tensor no longer holds what a masked policy or a fused step wrote there
-        if (d_masks || env->fusedActions == d_actions) env->fusedActions = nullptr;
-        if (env->lastPolicyActions == d_actions) env->polValid = false;
-        HIPCHK(env->launch(0, D, pickStream(env, stream)));
+        stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed, step, 1, stream);
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1064,15 +1076,21 @@ int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d
                              uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps, int32_t fused,
                              void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
-    for (int32_t k = 0; k < n_steps; k++) {
-        int r;
-        if (fused) {
-            r = mrts_step_uniform_dev(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed,
-                                      first_step + (uint32_t)k, stream);
-        } else {
-            r = mrts_policy_uniform_dev(env, seed, first_step + (uint32_t)k, d_actions, stream);
-            if (!r) r = mrts_step_dev(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, stream);
+    if (fused) {
+        try {
+            for (int32_t k = 0; k < n_steps;) {
+                const int32_t n = std::min<int32_t>(n_steps - k, env->multiStep ? MRTS_MAX_ITER : 1);
+                k += stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, n,
+                                 stream);
+            }
+            return 0;
+        } catch (const Fail& f) {
+            return fail(f);
         }
+    }
+    for (int32_t k = 0; k < n_steps; k++) {
+        int r = mrts_policy_uniform_dev(env, seed, first_step + (uint32_t)k, d_actions, stream);
+        if (!r) r = mrts_step_dev(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, stream);
         if (r) return r;
     }
     return 0;

@@ -437,6 +437,7 @@ struct Game {
     // the smallest squared distance from the OTHER player's mobile units to it, before the step
     int readySlot;         // per lane: the unit slot of ready item lid() (-1 outside cycle)
     uint32_t polStep;      // the fused policy's Philox step (D.pol_step, + 1 per iteration of a multi-step launch)
+    uint32_t uniStep;      // the fused uniform policy's step (D.uni_step, likewise)
     int maxProd0, maxProd1, sumProd0, sumProd1;
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
@@ -473,6 +474,7 @@ struct Game {
         fwdWritten = false;
         lfwd = 0;
         polStep = d.pol_step;
+        uniStep = d.uni_step;
         freshLane();
     }
     // HX_*: snapshot sequence limits (PO), CloserToEnemy* base positions / old minimum distances
@@ -677,11 +679,12 @@ struct Game {
         fwdOn = fwdWritten;
         // without forwarded words the next decode reads the rows the previous iteration's policy
         // stored to the action tensor: make this wave's stores visible to its own loads first
-        if (!fwdWritten) __threadfence();
+        if (!fwdWritten && !D.uni_actions) __threadfence();
         fwdWritten = false;
         ixValid = false;
         deaths = 0;
         polStep++;
+        uniStep++;
         if (l >= H_WORDS && l < 32) hdr[l] = (l >= HX_BASE && l < HX_BASE + 2) ? -1 : (l >= HX_OLDSQ && l < HX_OLDSQ + 2) ? INF : 0;
         wsync();
     }
@@ -829,7 +832,7 @@ struct Game {
     // (writeUniformRows) — drawn again in registers instead of read back.
     DEV void fetchRow(const int32_t* rows, int slot, int c, int32_t a[7]) const {
         if (D.uni_actions) {
-            uniformRow(D.uni_seed, D.uni_step, D.uni_slot_base + (uint32_t)slot, c, NT, K - 23 - NT, a);
+            uniformRow(D.uni_seed, uniStep, D.uni_slot_base + (uint32_t)slot, c, NT, K - 23 - NT, a);
             return;
         }
         const int32_t* r = rows + (size_t)c * 7;
@@ -841,7 +844,7 @@ struct Game {
         for (int i = 0; i < nslots; i++)
             for (int c = lid(); c < HW; c += 64) {
                 int32_t a[7];
-                uniformRow(D.uni_seed, D.uni_step, D.uni_slot_base + (uint32_t)(slot0 + i), c, NT, K - 23 - NT, a);
+                uniformRow(D.uni_seed, uniStep, D.uni_slot_base + (uint32_t)(slot0 + i), c, NT, K - 23 - NT, a);
                 int32_t* dst = D.uni_actions + ((size_t)(slot0 + i) * HW + c) * 7;
                 st4u<false>(dst, a[0], a[1], a[2], a[3]);
                 st3u<false>(dst + 4, a[4], a[5], a[6]);

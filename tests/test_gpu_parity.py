@@ -906,12 +906,18 @@ def test_uniform_fused_matches_split(mp, n_sp, n_bot, po, masks):
             for s in range(a.dims[0]):
                 assert np.array_equal(a.dump_state(s), b.dump_state(s)), f"state of slot {s} differs at step {step}"
     assert not a.error_flags().any() and not b.error_flags().any()
-    # the native rollout's fused and split forms agree too
-    a.rollout_uniform(SEED, 300, 40, fused=False)
-    b.rollout_uniform(SEED, 300, 40, fused=True)
+    # the native rollout's fused and split forms agree too (fused: multi-step launches on the
+    # self-play-only 16x16 / 8x8 handles), across an auto-reset
+    assert b.multi_step_capable == (n_bot == 0)
+    a.rollout_uniform(SEED, 300, 100, fused=False)
+    b.rollout_uniform(SEED, 300, 100, fused=True)
     a.synchronize()
     b.synchronize()
     assert torch.equal(a.obs, b.obs) and torch.equal(a.actions, b.actions)
+    assert torch.equal(a.reward, b.reward) and torch.equal(a.done, b.done)
+    for s in range(a.dims[0]):
+        assert np.array_equal(a.dump_state(s), b.dump_state(s)), f"state of slot {s} differs after the rollout"
+    assert np.array_equal(a._h.env_steps(), b._h.env_steps())
     a.close()
     b.close()
 
