@@ -393,15 +393,20 @@ def main():
         contract += S * HW * 28
     survey = S * (HW * 7 * 4 + C * HW * 4 + (0 if uniform else HW * K) + (16 * mean_units + 2 * HW + 16))
     achieved = contract / (kern_ms * 1e-3) / 1e9
+    # a launch = the K steps of the multi-step launch, else one step
+    steps_per_launch = a.steps if launch_ms is not None else 1
     # roofline.traffic: HBM bytes per k_env launch from the rocprofv3 --pmc passes of this same command
     # (tools/gpu_profile.sh + tools/summarize_profile.py -> profiles/pmc_latest.json), when they exist
-    traffic, traffic_src = a.pmc_traffic, "--pmc-traffic" if a.pmc_traffic is not None else None
+    traffic, traffic_src = a.pmc_traffic, "--pmc-traffic (bytes per launch)" if a.pmc_traffic is not None else None
     pl = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if traffic is None and os.path.exists(pl):
         pj = json.load(open(pl))
-        if pj.get("mask_mode") == a.mask_mode and pj.get("envs_per_gpu") == E and a.map in (pj.get("workload") or ""):
-            traffic = pj["traffic_bytes_per_launch"]
-            traffic_src = f"profiles/pmc_latest.json ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes)"
+        if (pj.get("mask_mode") == a.mask_mode and pj.get("envs_per_gpu") == E and a.map in (pj.get("workload") or "")
+                and ("multi-step" in pj.get("kernel", "")) == (launch_ms is not None)):
+            per_step = pj.get("traffic_bytes_per_step", pj.get("traffic_bytes_per_launch"))
+            traffic = per_step * steps_per_launch
+            traffic_src = (f"profiles/pmc_latest.json ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes; "
+                           f"{per_step / 1e6:.1f} MB per step x {steps_per_launch} steps per launch)")
     total_games = E * world
     value = total_games * a.steps / t
     out = {
@@ -465,7 +470,9 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_src,
             "kernel": "k_env<MODE_STEP>" + (" + fused policy rows" if fused else " + fused uniform rows" if uni_fused else ""),
-            "alg_bytes_per_launch": contract,
+            "alg_bytes_per_launch": contract * steps_per_launch,
+            "alg_bytes_per_step": contract,
+            "launch_duration_ms": kern_ms * steps_per_launch,
             "alg_bytes_note": f"step contract bytes, {'no' if uniform else a.mask_mode} masks: {rows:.2f} idle-unit rows and {dirty:.2f} "
                               f"changed mask rows per slot" + (f", {obs_chunks:.1f} changed (plane, 4-cell chunk) "
                               f"observation pieces per slot (persistent PO views)" if po_delta else "")

@@ -154,8 +154,9 @@ int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_play
 /* n_steps consecutive mrts_step_fused_dev calls (next_step = first_next_step, first_next_step + 1,
  * ...) enqueued from native code, without a host language's per-call overhead between them (a
  * random-policy rollout; the outputs of the last step remain in the buffers).  n_steps >= 0.
- * Multi-step launches (default on, mrts_set_multi_step): on full-observability self-play handles of
- * the specialised shapes (16x16 / 8x8 maps, the built-in unit-type tables), once the handle is in the
+ * Multi-step launches (default on, mrts_set_multi_step): on self-play handles of the specialised
+ * shapes (16x16 / 8x8 full observability, 32x32 partially observable with the default unit capacity
+ * of max_units 256; the built-in unit-type tables), once the handle is in the
  * steady fused state (the previous launch was a fused step on these buffers), one launch runs up to
  * MRTS_MAX_ITER of the steps: each game's wave keeps its state in LDS between steps and performs
  * every step in full (decode, issue, cycle, rewards, auto-reset, observation, masks and the next

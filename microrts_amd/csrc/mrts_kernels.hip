@@ -431,6 +431,7 @@ struct Game {
     bool fwdOn;            // this game's forwarded action words are current (H_FWD == fwd_stamp - 1)
     bool fwdWritten;       // this launch wrote the forwarded action words (store() stamps H_FWD)
     uint32_t lkey, lsnap;  // PO delta: lane l's hp | resources << 16 as loaded, its previous render's snapshot byte
+    bool poLds;            // the last PO render (writeObsPOFast2) left its whole record in LDS as well
     uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
     int curP;              // player whose pa is being issued
     // CloserToEnemyBase/Unit: each player's first Base before the step (x | y << 8, -1 = none) and
@@ -473,6 +474,7 @@ struct Game {
         fwdOn = false;
         fwdWritten = false;
         lfwd = 0;
+        poLds = false;
         polStep = d.pol_step;
         uniStep = d.uni_step;
         freshLane();
@@ -678,9 +680,32 @@ struct Game {
         lua = ua[l];
         fwdOn = fwdWritten;
         // without forwarded words the next decode reads the rows the previous iteration's policy
-        // stored to the action tensor: make this wave's stores visible to its own loads first
-        if (!fwdWritten && !D.uni_actions) __threadfence();
+        // stored to the action tensor (partially observable games always do), and a PO game re-reads
+        // the render record the previous iteration stored: this wave's own plain stores, read back on
+        // the same CU — a workgroup-scope fence (the stores' vmcnt drain; an agent-scope
+        // __threadfence would also write back the XCD's L2 every step: c5 measured 4x slower)
+        const bool poRec = po && D.obs_delta && D.po_prev && poDeltaShape(H, W);
+        const bool poReload = poRec && !poLds;  // a render that kept no LDS copy: re-read the record
+        if (po || (!fwdWritten && !D.uni_actions)) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         fwdWritten = false;
+        poLds = false;
+        hset(H_NU, nu);  // "the loaded unit count" of this iteration (PO delta render)
+        if (poRec && !poReload) {  // the previous render's record from its LDS copies
+            lkey = (uint32_t)(uint16_t)hp[l] | ((uint32_t)(uint16_t)res[l] << 16);
+            lsnap = snap[l];  // after the compaction = the record's snapshot bytes; before clearSnap
+        } else if (poReload) {  // the previous render's record, as load() takes it
+            const int32_t* pr = D.po_prev + (size_t)g * D.po_words;
+            const int NCW = poChunkWords(HW), SW = poSnapWords(CAP);
+            const int32_t prv0 = pr[0], prsb = pr[1 + (l >> 2)];
+            const int32_t prvv = l < 4 * H ? pr[1 + SW + l] : 0, prv2 = l + 64 < 4 * H ? pr[1 + SW + l + 64] : 0;
+            const int32_t prpd = l < 2 * NCW ? pr[1 + SW + 4 * H + l] : 0;
+            lkey = (uint32_t)(uint16_t)hp[l] | ((uint32_t)(uint16_t)res[l] << 16);
+            lsnap = ((uint32_t)prsb >> (8 * (l & 3))) & 0xFFu;
+            if (l < 4 * H) poVis[l] = (uint32_t)prvv;
+            if (l + 64 < 4 * H) poVis[l + 64] = (uint32_t)prv2;
+            if (l < 2 * NCW) poPend[l] = (uint32_t)prpd;
+            if (l == 0) hdr[HX_POVALID] = prv0;
+        }
         ixValid = false;
         deaths = 0;
         polStep++;
@@ -2599,6 +2624,7 @@ struct Game {
                 const uint32_t row = (v ? rowsV1 : rowsV0)[l];
                 if (v ? d1 : d0) {
                     const uint32_t d = row ^ poVis[v * 2 * H + l];
+                    poVis[v * 2 * H + l] = row;  // the record's LDS copy (a multi-step launch's next render)
                     if (d) {
                         uint32_t gbits = 0;  // bit j = column group 4j..4j+3 changed
 #pragma unroll
@@ -2615,6 +2641,7 @@ struct Game {
                     }
                 }
                 if (pr) pr[1 + SW + v * 2 * H + l] = (int32_t)row;
+                if (!(v ? d1 : d0)) poVis[v * 2 * H + l] = row;
             }
         }
         wsync();
@@ -2638,7 +2665,10 @@ struct Game {
         if (pr && l < NCW) {
             pr[1 + SW + 4 * H + l] = (int32_t)poDirty[NCW + l];
             pr[1 + SW + 4 * H + NCW + l] = (int32_t)poDirty[3 * NCW + l];
+            poPend[l] = poDirty[NCW + l];  // LDS copies, as the sight rows above
+            poPend[NCW + l] = poDirty[3 * NCW + l];
         }
+        poLds = pr != nullptr;
         wsync();
         int32_t* out = D.obs + (size_t)slot0 * D.C * HW;
         const __amdgpu_buffer_rsrc_t rs = bufRsrc(out, (uint32_t)(2 * D.C * HW * 4));
@@ -2873,7 +2903,10 @@ struct Game {
         int32_t* pr = D.po_prev + (size_t)g * D.po_words;
         const uint32_t* sw = (const uint32_t*)snap;
         for (int w = lid(); w < (nu + 3) / 4; w += 64) pr[1 + w] = (int32_t)sw[w];
-        if (lid() == 0) pr[0] = (int32_t)views;
+        if (lid() == 0) {
+            pr[0] = (int32_t)views;
+            hdr[HX_POVALID] = (int32_t)views;  // the record's LDS copy (multi-step launch)
+        }
     }
 
     // ------------------------------------------------------------------ legal-action masks
@@ -3792,11 +3825,13 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         }
         PHASE(9);
     }
+    if (MODE != MODE_MASKS && G.po && D.obs && external && D.po_prev && poDeltaShape(G.H, G.W)) {
+        wsync();
+        G.poRecordSnaps(selfplay ? 3u : (1u << side));
+    }
     }  // iterations
     if (MODE != MODE_MASKS) {
         wsync();
-        if (G.po && D.obs && external && D.po_prev && poDeltaShape(G.H, G.W))
-            G.poRecordSnaps(selfplay ? 3u : (1u << side));
         G.store();
 #ifdef MRTS_ABLATE
         if (G.ab(AB_STORE)) G.store();
@@ -4217,6 +4252,7 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
         case MODE_STEP:
             if (D.n_iter > 1 && is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false, true>), grid, block, lds, stream, D.state, ds, D);
             else if (D.n_iter > 1 && is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true>), grid, block, lds, stream, D.state, ds, D);
+            else if (D.n_iter > 1 && is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
             else if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
             else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, D.state, ds, D);
             else if (is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, D.state, ds, D);
@@ -4228,12 +4264,14 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
     }
     return hipGetLastError();
 }
-// launchEnv(MODE_STEP) would run a specialised full-observability self-play kernel, the one whose
-// games can iterate several steps in one launch (KDyn.n_iter)
+// launchEnv(MODE_STEP) would run a specialised self-play kernel (16x16 / 8x8 full observability,
+// 32x32 partially observable), the ones whose games can iterate several steps in one launch
+// (KDyn.n_iter, MULTI instances)
 bool envIterable(const KStatic& hs) {
     const bool fixable = hs.n_sp_games == hs.n_games && hs.utt.K == 79 && hs.utt.ntypes == 7 && hs.utt.maxAttackRadius == 7 &&
-                         hs.H == hs.W && !hs.partial_obs;
-    return fixable && ((hs.W == 16 && hs.CAP == 320) || (hs.W == 8 && hs.CAP == 128));
+                         hs.H == hs.W;
+    return fixable && ((hs.W == 16 && hs.CAP == 320 && !hs.partial_obs) || (hs.W == 8 && hs.CAP == 128 && !hs.partial_obs) ||
+                       (hs.W == 32 && hs.CAP == 320 && hs.partial_obs));
 }
 hipError_t prepareLds(size_t bytes) {
     hipError_t e = hipFuncSetAttribute((const void*)k_env<MODE_STEP, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);

@@ -714,22 +714,26 @@ def test_native_rollout_matches_fused_steps(mp, n_sp):
     del torch
 
 
-@pytest.mark.parametrize("mp,n_sp,max_steps", [("maps/16x16/basesWorkers16x16.xml", 48, 300),
-                                                ("maps/8x8/basesWorkers8x8.xml", 64, 150),
-                                                ("maps/16x16/EightBasesWorkers16x16.xml", 8, 2000)])
-def test_multi_step_rollout_matches_single_launches(mp, n_sp, max_steps):
+@pytest.mark.parametrize("mp,n_sp,max_steps,po", [("maps/16x16/basesWorkers16x16.xml", 48, 300, False),
+                                                   ("maps/8x8/basesWorkers8x8.xml", 64, 150, False),
+                                                   ("maps/16x16/EightBasesWorkers16x16.xml", 8, 2000, False),
+                                                   ("maps/BWDistantResources32x32.xml", 32, 200, True)])
+def test_multi_step_rollout_matches_single_launches(mp, n_sp, max_steps, po):
     """Multi-step launches (mrts_rollout_fused_dev running up to MRTS_MAX_ITER steps per game in one
     launch, state kept in LDS between steps) = one launch per step (mrts_set_multi_step(0)), bit for
     bit: observations, rewards, dones, masks, source bits, next actions, env steps and every game's
     state — rollouts of 1 .. 250 steps across auto-resets, games above 64 units (EightBasesWorkers:
     the multi-block decode, mask and non-forwarded row paths inside the loop), then single fused
-    steps, a plain step and a mask write after the multi-step launches (handle bookkeeping)."""
+    steps, a plain step and a mask write after the multi-step launches (handle bookkeeping); the 32x32
+    partially observable views (persistent-buffer delta renders whose record is re-read per step)."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
 
-    mk = lambda: DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=5)  # noqa: E731
+    mk = lambda: DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=5, partial_obs=po,  # noqa: E731
+                              max_units=256 if po else 0)
     A, B = mk(), mk()
     A.set_multi_step(False)
+    assert B.multi_step_capable
     for e in (A, B):
         e.reset()
         e.random_policy(SEED, 0)
