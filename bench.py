@@ -386,7 +386,14 @@ def main():
     # of the action tensor is written by the step kernel
     uni_fused = uniform and mode["uni_fused"]
     row_in = 4 if fused else 0 if uni_fused else 28
-    contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * (2 * (64 + 28 * mean_units) + HW + 2 * 2 * MWB)
+    # per game: the state (header + unit rows) read and written, the terrain read, both players' row sets
+    # read and written — per step; a multi-step launch keeps state, terrain and row sets in LDS, so it
+    # loads / stores them once per launch (1/K per step) and only writes the row sets each step
+    state_io = 2 * (64 + 28 * mean_units) + HW
+    if launch_ms is not None:
+        contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * ((state_io + 2 * MWB) / a.steps + 2 * MWB)
+    else:
+        contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * (state_io + 2 * 2 * MWB)
     if fused:  # the policy's action rows (and their forwarded words) leave the step kernel too
         contract += S * (dirty if a.mask_mode == "delta" else HW) * 28 + S * rows * 4
     if uni_fused:

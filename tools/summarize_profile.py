@@ -8,8 +8,8 @@ also shown x2 (MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE under-reports wide s
 our reads are narrow, so the true value lies between the two).
 
 Multi-step launches (bench.json `launch_ms` set): the timed window is ONE k_env launch running all
-`--window` steps; it is the longest k_env launch among the last window + 10 (the eager per-step
-kernel-timing pass and the probe steps follow it).  Its duration and counters are divided by the
+`--window` steps; it is the last k_env launch longer than ten single-step launches (the eager
+per-step kernel-timing pass and the probe steps follow it).  Its duration and counters are divided by the
 window's step count (per-step figures); the eager pass gives the single-step launch average.
 """
 import argparse
@@ -30,10 +30,12 @@ def dur(r):
 
 
 def multi_launch(rows, n):
-    """(index in start order, row) of the timed multi-step k_env launch: the longest of the last n + 10."""
+    """(index in start order, row) of the timed multi-step k_env launch: the last launch longer than ten
+    single-step launches (the median of the last n: the eager kernel-timing pass and the probe steps
+    follow the timed launch; the burn-in and warmup launches precede it)."""
     rs = sorted((r for r in rows if r["Kernel_Name"].startswith("k_env")), key=lambda r: int(r["Start_Timestamp"]))
-    tail = list(enumerate(rs))[-(n + 10):]
-    return max(tail, key=lambda t: dur(t[1]))
+    single = statistics.median(dur(r) for r in rs[-n:])
+    return [(i, r) for i, r in enumerate(rs) if dur(r) > 10 * single][-1]
 
 
 def main():
