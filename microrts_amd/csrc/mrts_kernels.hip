@@ -911,33 +911,25 @@ struct Game {
     }
     // UnitAction.fromVectorAction (rts/UnitAction.java:675-709) of row components a[0..6] for a unit
     // with core word cu
+    // Branch-free (selects only): the lanes of one wave hold rows of every type, and a divergent switch
+    // runs each present case's instructions for the whole wave.
     DEV bool decodeFields(uint32_t cu, const int32_t a[7], int& t, int& pr, int& ut, int& tx, int& ty) const {
         const int ctr = R / 2;
         const int x = ux(cu), y = uy(cu);
         t = (a[0] >= 0 && a[0] <= 5) ? a[0] : ACT_INVALID;
-        pr = -1;
-        ut = tx = ty = 0;
-        bool bad = false;
-        switch (t) {
-            case T_MOVE: pr = clampdir(a[1]); break;
-            case T_HARVEST: pr = clampdir(a[2]); break;
-            case T_RETURN: pr = clampdir(a[3]); break;
-            case T_PRODUCE:
-                pr = clampdir(a[4]);
-                if (a[5] < 0 || a[5] >= NT) bad = true;  // utt.getUnitType(int) throws (:697)
-                else ut = a[5];
-                break;
-            case T_ATTACK: {
-                const int ax = x + (a[6] % R - ctr), ay = y + (a[6] / R - ctr);
-                if (inb(ax, ay)) {
-                    tx = ax;
-                    ty = ay;
-                } else {
-                    tx = ty = 255;  // off-map target: never legal
-                }
-            } break;
-        }
-        return bad;
+        // MOVE / HARVEST / RETURN / PRODUCE: the direction of that type's component
+        const int d = t == T_MOVE ? a[1] : t == T_HARVEST ? a[2] : t == T_RETURN ? a[3] : a[4];
+        pr = (t >= T_MOVE && t <= T_PRODUCE) ? clampdir(d) : -1;
+        // PRODUCE: utt.getUnitType(int) throws for a type outside the table (:697)
+        const bool prod = t == T_PRODUCE;
+        const bool badType = a[5] < 0 || a[5] >= NT;
+        ut = (prod && !badType) ? a[5] : 0;
+        // ATTACK: the target cell of the window index, off-map -> never legal
+        const int ax = x + (a[6] % R - ctr), ay = y + (a[6] / R - ctr);
+        const bool att = t == T_ATTACK, on = inb(ax, ay);
+        tx = att ? (on ? ax : 255) : 0;
+        ty = att ? (on ? ay : 255) : 0;
+        return prod && badType;
     }
 
     // ------------------------------------------------------------------ Java row layout
@@ -2272,6 +2264,14 @@ struct Game {
         const int k0 = (int)(D.reward_kinds4 & 15u);
         const bool done0 = k0 == RF_WINLOSS ? gameover : (k0 == RF_RESOURCE_GATHER ? !resLeft : false);
         const int L = lid();
+        if (R == 1 && k0 == RF_WINLOSS) {  // WinLoss alone (the common case): a wave-uniform branch, no switch
+            if (L < nslots) {
+                const int p = L ? pl1 : pl0;
+                if (D.reward) D.reward[slot0 + L] = gameover ? (winner == p ? 1.0 : -1.0) : 0.0;
+                if (D.done) D.done[slot0 + L] = gameover ? 1 : 0;
+            }
+            return done0;
+        }
         if (L < nslots * R && (D.reward || D.done)) {
             const int i = L / R, j = L - i * R;
             const int p = i ? pl1 : pl0;

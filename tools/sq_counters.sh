@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-BARGS="--steps 100 --warmup 10 --burnin 1000 --no-cpu-baseline --no-graph"
+BARGS=${SQ_BARGS:-"--steps 100 --warmup 10 --burnin 1000 --no-cpu-baseline --no-graph"}
 i=0
 for grp in "SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
            "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" \
