@@ -3621,6 +3621,9 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     const int gtype = kind & 15, ai1 = (kind >> 4) & 15, ai2 = (kind >> 8) & 15;
     const bool external = gtype != GT_BOT_VS_BOT;  // bot-only clients return no observation / masks
     const int niter = MULTI ? D.n_iter : 1;
+#ifdef MRTS_PHASE_TIMING
+    int nu0_ = 0;
+#endif
     for (int it = 0; it < niter; it++) {
     if (it > 0) {
         G.nextStep();
@@ -3637,7 +3640,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         else __builtin_amdgcn_s_setprio(3);
     }
 #ifdef MRTS_PHASE_TIMING
-    const int nu0_ = G.nu;
+    if (it == 0) nu0_ = G.nu;
 #endif
     if (G.po) G.clearSnap();
     PHASE(0);
