@@ -832,7 +832,14 @@ struct Game {
                         keepv(a1 + a2 + a3 + a4 + a5);
                     }
 #endif
-                    legality(l, cu, tt, prm, ttx, tty, tut);
+                    // A forwarded row was sampled by the fused policy from this unit's mask record, which
+                    // the previous step wrote from this same state (no cycle in between): its type bit
+                    // and parameter bits are members of getUnitActions' list (a PRODUCE's free
+                    // directions x affordable types is a full product), and issuing the other player's
+                    // pairs changes nothing the test reads (positions, hp, resources move only in
+                    // cycle) — so issueSafe's legality test returns the row unchanged and is skipped.
+                    // Any other row (the caller's tensor, the uniform policy) is tested.
+                    if (!fwdOn) legality(l, cu, tt, prm, ttx, tty, tut);
                 }
                 wsync();
                 MPHASE(24);
