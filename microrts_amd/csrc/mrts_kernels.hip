@@ -679,14 +679,15 @@ struct Game {
         lcu = uc[l];  // l < 64 <= CAP; selfPlayFast ignores lanes >= nu
         lua = ua[l];
         fwdOn = fwdWritten;
-        // without forwarded words the next decode reads the rows the previous iteration's policy
-        // stored to the action tensor (partially observable games always do), and a PO game re-reads
-        // the render record the previous iteration stored: this wave's own plain stores, read back on
-        // the same CU — a workgroup-scope fence (the stores' vmcnt drain; an agent-scope
-        // __threadfence would also write back the XCD's L2 every step: c5 measured 4x slower)
+        // without forwarded words (more than 64 units) the next decode reads the rows the previous
+        // iteration's policy stored to the action tensor, and a PO render that kept no LDS copy of
+        // its record makes the next one re-read it: this wave's own plain stores, read back on the
+        // same CU — a workgroup-scope fence (the stores' vmcnt drain, which also waits for the
+        // iteration's observation stores: only when needed — c5 paid ~6 us per step draining them
+        // every step; an agent-scope __threadfence would also write back the XCD's L2: 4x slower)
         const bool poRec = po && D.obs_delta && D.po_prev && poDeltaShape(H, W);
         const bool poReload = poRec && !poLds;  // a render that kept no LDS copy: re-read the record
-        if (po || (!fwdWritten && !D.uni_actions)) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        if (poReload || (!fwdWritten && !D.uni_actions)) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
         fwdWritten = false;
         poLds = false;
         hset(H_NU, nu);  // "the loaded unit count" of this iteration (PO delta render)
@@ -893,7 +894,12 @@ struct Game {
             const uint32_t cu = uc[l];
             const int pl = uplay(cu);
             act = !(pl < 0 || (ua[l] & UA_PRESENT) || (only >= 0 && pl != only));
-            if (act) fetchRow(pl == 0 ? rows0 : rows1, pl == 0 ? s0 : s1, uy(cu) * W + ux(cu), a);
+            if (act) {
+                // units 0..63 of a self-play game: the fused policy's forwarded word when current
+                // (as selfPlayFast), else the action tensor
+                if (fwdOn) unpackFwd(lfwd, a);
+                else fetchRow(pl == 0 ? rows0 : rows1, pl == 0 ? s0 : s1, uy(cu) * W + ux(cu), a);
+            }
         }
         if (!po && (HW + 2 * W + 31) / 32 <= 64) buildIndex();
         if (act) bad_any |= decodeRow(l, a);
@@ -1125,7 +1131,10 @@ struct Game {
             tx = ua_tx(a);
             ty = ua_ty(a);
             ut = ua_ut(a);
-            legality(o, t, prm, tx, ty, ut);
+            // forwarded fused-policy rows (every decoded row here when fwdOn: all units in one wave)
+            // are members of getUnitActions' list — see selfPlayFast; the masks, and so the rows,
+            // come from the full state in partially observable games too (JNIGridnetClient.java:210-223)
+            if (!fwdOn) legality(o, t, prm, tx, ty, ut);
         }
         wsync();
         if (acc) issueBatch(isPA, irank, __popcll(acc), o, t, prm, tx, ty, ut);
@@ -1885,6 +1894,9 @@ struct Game {
     // units inside the sight of player p's (live) units, with the assignments they hold now.  Lane =
     // unit, a uniform loop over the observers (few; painting disks costs more here).
     DEV void snapshot(int p) {
+#ifdef MRTS_ABLATE
+        if (ab(AB_PO_NOSNAPSHOT)) return;
+#endif
         for (int o0 = 0; o0 < nu; o0 += 64) {
             const int o = o0 + lid();
             uint32_t cu = 0;
@@ -2600,6 +2612,9 @@ struct Game {
         wsync();
         {
             const bool pt0 = in0 && own >= 0, pt1 = in1 && own >= 0;
+#ifdef MRTS_ABLATE
+            if (!ab(AB_PO_NOPAINT))
+#endif
             if (ballot(pt0 || pt1))
                 paintDisks2(pt0, own == 0 ? rowsV0 : rowsV0 + H, pt1, own == 1 ? rowsV1 : rowsV1 + H, cu);
         }
@@ -2677,6 +2692,9 @@ struct Game {
         }
         poLds = pr != nullptr;
         wsync();
+#ifdef MRTS_ABLATE
+        if (ab(AB_PO_NOSTORE)) n = 0;  // no render pass (gather + stores)
+#endif
         int32_t* out = D.obs + (size_t)slot0 * D.C * HW;
         const __amdgpu_buffer_rsrc_t rs = bufRsrc(out, (uint32_t)(2 * D.C * HW * 4));
         const uint64_t deadAny = deadM0 | deadM1;
