@@ -1910,14 +1910,18 @@ struct Game {
             for (int q0 = 0; q0 < nu; q0 += 64) {
                 const int q = q0 + lid();
                 uint32_t qc = q < nu ? uc[q] : UC_DEAD;
-                uint64_t m = ballot(!(qc & UC_DEAD) && uplay(qc) == p);
+                const bool obs = !(qc & UC_DEAD) && uplay(qc) == p;
+                // each observer's x | y << 8 | sight^2 << 16, looked up once per lane, so the serial
+                // loop below is one readlane per observer (no dependent LDS read of the sight table)
+                const int sr = obs ? U.sight[utyp(qc)] : 0;
+                const uint32_t ow = (uint32_t)ux(qc) | ((uint32_t)uy(qc) << 8) | ((uint32_t)(sr * sr) << 16);
+                uint64_t m = ballot(obs);
                 while (m) {
                     const int k = __builtin_ctzll(m);
                     m &= m - 1;
-                    const uint32_t oc = (uint32_t)rl((int)qc, k);
-                    const int sr = U.sight[utyp(oc)];
-                    const int dx = ux(oc) - x, dy = uy(oc) - y;
-                    vis |= dx * dx + dy * dy <= sr * sr;
+                    const uint32_t w = (uint32_t)rl((int)ow, k);
+                    const int dx = (int)(w & 0xFFu) - x, dy = (int)((w >> 8) & 0xFFu) - y;
+                    vis |= dx * dx + dy * dy <= (int)(w >> 16);
                 }
             }
             if (o < nu) {
