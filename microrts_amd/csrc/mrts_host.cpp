@@ -27,6 +27,7 @@ hipError_t launchPolicyUniform(int32_t* actions, int n_slots, int HW, int ntypes
                                uint32_t slot_base, hipStream_t stream);
 #ifdef MRTS_ABLATE
 hipError_t setAblate(uint32_t v);
+hipError_t getDbg(unsigned long long* out, int reset);
 #endif
 #ifdef MRTS_PHASE_TIMING
 hipError_t phaseTimes(unsigned long long* out, int reset);
@@ -1790,6 +1791,7 @@ int mrts_evaluate(mrts_env* env, int32_t maxplayer, float* out) {
 #ifdef MRTS_ABLATE
 // diagnostic build only: g_ablate (tools/ablate_price.py)
 int mrts_set_ablate(unsigned v) { return mrts::setAblate(v) == hipSuccess ? 0 : -EIO; }
+int mrts_get_dbg(unsigned long long* out, int reset) { return mrts::getDbg(out, reset) == hipSuccess ? 0 : -EIO; }
 #endif
 #ifdef MRTS_PHASE_TIMING
 // diagnostic build only: per-phase cycle sums of k_env (tools/phase_timing.py)

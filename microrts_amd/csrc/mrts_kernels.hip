@@ -78,6 +78,7 @@ constexpr int mileOf(int ph) {
 // the real, contended kernel.  Never loaded by the package.
 #ifdef MRTS_ABLATE
 __device__ uint32_t g_ablate;
+__device__ unsigned long long g_dbg[4];  // diagnostics: [0] PO render items, [1] PO renders, [2] delta renders
 template <class T>
 DEV T launder(T v) {
     asm volatile("" : "+v"(v));
@@ -711,7 +712,9 @@ struct Game {
         deaths = 0;
         polStep++;
         uniStep++;
-        if (l >= H_WORDS && l < 32) hdr[l] = (l >= HX_BASE && l < HX_BASE + 2) ? -1 : (l >= HX_OLDSQ && l < HX_OLDSQ + 2) ? INF : 0;
+        // (HX_POVALID stays: it is the PO render record's "views rendered", set by poRecordSnaps)
+        if (l >= H_WORDS && l < 32 && l != HX_POVALID)
+            hdr[l] = (l >= HX_BASE && l < HX_BASE + 2) ? -1 : (l >= HX_OLDSQ && l < HX_OLDSQ + 2) ? INF : 0;
         wsync();
     }
     // new GameState(PhysicalGameState.load(map)) — JNIGridnetClient.reset (tests/JNIGridnetClient.java:239-241).
@@ -2697,6 +2700,11 @@ struct Game {
         poLds = pr != nullptr;
         wsync();
 #ifdef MRTS_ABLATE
+        if (l == 0) {
+            atomicAdd(&g_dbg[0], (unsigned long long)n);
+            atomicAdd(&g_dbg[1], 1ull);
+            if (delta) atomicAdd(&g_dbg[2], 1ull);
+        }
         if (ab(AB_PO_NOSTORE)) n = 0;  // no render pass (gather + stores)
 #endif
         int32_t* out = D.obs + (size_t)slot0 * D.C * HW;
@@ -2757,6 +2765,15 @@ struct Game {
                 vv[j][7] = (int)((tr >> (x0 + j)) & 1u);
             }
             const uint32_t base = (uint32_t)(v * D.C * HW + 4 * c4) * 4u;
+#ifdef MRTS_ABLATE
+            if (ab(AB_PO_ZEROSTORE)) {  // pricing: the render's values computed, not stored
+                int acc = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++) acc += vv[0][k] ^ vv[1][k] ^ vv[2][k] ^ vv[3][k];
+                keepv(acc);
+                continue;
+            }
+#endif
             if (SC1_POOBS) {
 #pragma unroll
                 for (int k = 0; k < 8; k++) st4sc1(rs, base + (uint32_t)(k * HW) * 4u, vv[0][k], vv[1][k], vv[2][k], vv[3][k]);
@@ -4081,6 +4098,14 @@ __global__ __launch_bounds__(64) void k_policy(PolicyParams Q) {
 namespace mrts {
 #ifdef MRTS_ABLATE
 hipError_t setAblate(uint32_t v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_ablate), &v, sizeof(v)); }
+hipError_t getDbg(unsigned long long* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dbg), sizeof(unsigned long long) * 4);
+    if (e == hipSuccess && reset) {
+        unsigned long long z[4] = {0, 0, 0, 0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof(z));
+    }
+    return e;
+}
 #endif
 #ifdef MRTS_PHASE_TIMING
 // out[16]: per-phase sums over games (and the max over games in out[16..31] when given 32 slots)

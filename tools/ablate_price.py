@@ -22,7 +22,7 @@ from microrts_amd import DeviceVecEnv  # noqa: E402
 
 NAMES = ["load", "obs", "store", "maskbits", "record", "policy", "accept", "legality", "outcome+rewards", "index",
          "gone", "tables", "rank", "decode", "(issue)", "(cyclerank)", "SKIP obs", "SKIP records",
-         "PO obs without stores", "PO obs stores of zeros only", "SKIP PO disk painting", "SKIP PO cell map",
+         "SKIP PO render pass", "PO render without its stores", "SKIP PO disk painting", "SKIP PO cell map",
          "SKIP PO render record", "(snapshot)"]
 SEED = 0x5EEDC0DE
 
