@@ -1919,12 +1919,16 @@ struct Game {
                 const int sr = obs ? U.sight[utyp(qc)] : 0;
                 const uint32_t ow = (uint32_t)ux(qc) | ((uint32_t)uy(qc) << 8) | ((uint32_t)(sr * sr) << 16);
                 uint64_t m = ballot(obs);
+                // two observers per round: independent readlane -> test chains (the loop is latency-bound)
                 while (m) {
-                    const int k = __builtin_ctzll(m);
+                    const int k1 = __builtin_ctzll(m);
                     m &= m - 1;
-                    const uint32_t w = (uint32_t)rl((int)ow, k);
-                    const int dx = (int)(w & 0xFFu) - x, dy = (int)((w >> 8) & 0xFFu) - y;
-                    vis |= dx * dx + dy * dy <= (int)(w >> 16);
+                    const int k2 = m ? __builtin_ctzll(m) : k1;
+                    m &= m ? m - 1 : 0ull;
+                    const uint32_t w1 = (uint32_t)rl((int)ow, k1), w2 = (uint32_t)rl((int)ow, k2);
+                    const int dx1 = (int)(w1 & 0xFFu) - x, dy1 = (int)((w1 >> 8) & 0xFFu) - y;
+                    const int dx2 = (int)(w2 & 0xFFu) - x, dy2 = (int)((w2 >> 8) & 0xFFu) - y;
+                    vis |= (dx1 * dx1 + dy1 * dy1 <= (int)(w1 >> 16)) | (dx2 * dx2 + dy2 * dy2 <= (int)(w2 >> 16));
                 }
             }
             if (o < nu) {
