@@ -97,7 +97,7 @@ enum { AB_LOAD = 0, AB_OBS = 1, AB_STORE = 2, AB_MASKBITS = 3, AB_RECORD = 4, AB
        // PO observation split: everything but the stores (values kept alive) / only the stores (zeros)
        AB_PO_NOSTORE = 18, AB_PO_ZEROSTORE = 19,
        // PO observation pieces skipped: sight-disk painting, the last-writer cell map, the render record
-       AB_PO_NOPAINT = 20, AB_PO_NOSCELL = 21, AB_PO_NORECORD = 22, AB_PO_NOSNAPSHOT = 23 };
+       AB_PO_NOPAINT = 20, AB_PO_NOSCELL = 21, AB_PO_NORECORD = 22, AB_PO_NOSNAPSHOT = 23, AB_COUNT = 24 };
 #endif
 enum { GT_SELFPLAY = 0, GT_AGENT_VS_BOT = 1, GT_BOT_VS_BOT = 2, GT_PLAYOUT = 3 };  // game_kind & 15
 // per-player counters of this step's issued pairs, as the TraceEntry holds them (after issueSafe's
@@ -1944,6 +1944,54 @@ struct Game {
         hset(HX_SNAP + p, seq);
         wsync();
     }
+    // Both views' membership at once (self-play, poFast2 shapes): lane = unit paints its sight disk
+    // into its own player's row bitmap (the host table's half-widths: the cells dx^2 + dy^2 <= sight^2,
+    // exactly snapshot()'s test), then a unit is in view p iff it is live and its cell's bit is set
+    // in p's rows (own units cover their own cell).  View 0's assignment bits are taken now; view 1's
+    // by snapshotActions(1) after player 0's pairs are issued (the views' unitActions copies are taken
+    // at different times; positions and liveness do not change in between).  `vis` is scratch here
+    // (the render clears it).
+    DEV bool snapBothOk() const { return W <= 32 && H <= 32 && nu <= 64 && U.maxSight <= 15; }
+    DEV void snapshotBoth() {
+#ifdef MRTS_ABLATE
+        if (ab(AB_PO_NOSNAPSHOT)) return;
+#endif
+        const int l = lid();
+        uint32_t* const r0 = vis;
+        uint32_t* const r1 = vis + H;
+        if (l < 2 * H) vis[l] = 0;
+        const bool inList = l < nu;
+        const uint32_t cu = inList ? uc[l] : UC_DEAD;
+        const bool live = !(cu & UC_DEAD);
+        const int own = uplay(cu);
+        wsync();
+        paintDisks2(live && own == 0, r0, live && own == 1, r1, cu);
+        wsync();
+        if (inList) {
+            const int x = ux(cu), y = uy(cu);
+            const bool in0 = live && ((r0[y] >> x) & 1u), in1 = live && ((r1[y] >> x) & 1u);
+            uint32_t b = (in0 ? 1u : 0u) | (in1 ? 2u : 0u);
+            const uint32_t a = ua[l];
+            if (in0 && (a & UA_PRESENT)) b |= (uint32_t)(ua_type(a) + 1) << 2;
+            snap[l] = (uint8_t)b;
+        }
+        hset(HX_SNAP + 0, seq);
+        wsync();
+    }
+    DEV void snapshotActions(int p) {  // view p's assignment bits now (membership from snapshotBoth)
+#ifdef MRTS_ABLATE
+        if (ab(AB_PO_NOSNAPSHOT)) return;
+#endif
+        const int l = lid();
+        if (l < nu) {
+            uint32_t b = snap[l] & ~(7u << (2 + 3 * p));
+            const uint32_t a = ua[l];
+            if (((b >> p) & 1u) && (a & UA_PRESENT)) b |= (uint32_t)(ua_type(a) + 1) << (2 + 3 * p);
+            snap[l] = (uint8_t)b;
+        }
+        hset(HX_SNAP + p, seq);
+        wsync();
+    }
     DEV void clearSnap() {
         for (int o = lid(); o < CAP; o += 64) snap[o] = 0;
         wsync();
@@ -2704,7 +2752,7 @@ struct Game {
         poLds = pr != nullptr;
         wsync();
 #ifdef MRTS_ABLATE
-        if (l == 0) {
+        if (ab(AB_COUNT) && l == 0) {  // contended global atomics: only when counting
             atomicAdd(&g_dbg[0], (unsigned long long)n);
             atomicAdd(&g_dbg[1], 1ull);
             if (delta) atomicAdd(&g_dbg[2], 1ull);
@@ -3759,8 +3807,14 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
             } else {
             G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1, slot0, slot0 + 1);
             PHASE(1);
+            const bool snapBoth = G.po && G.snapBothOk();
             for (int p = 0; p < 2; p++) {
-                if (G.po) G.snapshot(p);
+                if (snapBoth) {
+                    if (p == 0) G.snapshotBoth();
+                    else G.snapshotActions(1);
+                } else if (G.po) {
+                    G.snapshot(p);
+                }
                 if (G.nu <= 64) {
                     G.decode(p, true);
                 } else {
@@ -3828,8 +3882,13 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
             const uint32_t valid = canDelta ? (uint32_t)G.hget(Game::HX_POVALID) : 0u;
             if (selfplay && G.poFast2()) {
                 if (freshObs) {  // PO views of the reset state (snapshot(p) touches only view p's bits)
-                    G.snapshot(0);
-                    G.snapshot(1);
+                    if (G.snapBothOk()) {
+                        G.snapshotBoth();
+                        G.snapshotActions(1);
+                    } else {
+                        G.snapshot(0);
+                        G.snapshot(1);
+                    }
                 }
 #ifdef MRTS_ABLATE
                 if (!G.ab(AB_SKIP_OBS))

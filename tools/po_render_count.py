@@ -14,6 +14,8 @@ from microrts_amd import _lib  # noqa: E402
 
 L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_ablate.so"))
 L.mrts_get_dbg.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.mrts_set_ablate.argtypes = [ctypes.c_uint]
+L.mrts_set_ablate(1 << 24)  # AB_COUNT: the render-item counters (contended atomics: diagnostics only)
 from microrts_amd import DeviceVecEnv  # noqa: E402
 
 SEED = 0x5EEDC0DE
