@@ -272,14 +272,21 @@ def main():
     base = a.burnin + a.warmup
     graph = None
     native = native_path
-    if a.launch == "graph" and gather_buf is None:
+    if a.launch == "graph":
         try:
+            if gather_buf is not None:  # the capture starts with no collective in flight
+                gather_buf.wait()
+                torch.cuda.synchronize(env.device)
+                gather_buf.fired = [False, False]
             graph = torch.cuda.CUDAGraph()
             cap = torch.cuda.Stream(env.device)
             cap.wait_stream(torch.cuda.current_stream(env.device))
-            with torch.cuda.graph(graph, stream=cap):
+            # thread_local: the process group's watchdog thread may query events during the capture
+            with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
                 for k in range(a.steps):
                     one_step(base + k)
+                if gather_buf is not None:
+                    gather_buf.wait()  # the comm stream joins the capture: the last exchange is in the graph
             torch.cuda.synchronize(env.device)
         except Exception as ex:  # capture unsupported here: time eagerly instead
             print(f"bench: hipGraph capture failed ({ex!r}); eager launches", file=sys.stderr)
@@ -443,7 +450,8 @@ def main():
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": "off" if uniform else a.mask_mode,
-            "launch": (f"one {'mrts_rollout_uniform_dev' if uniform else 'mrts_rollout_fused_dev'} call: ONE k_env launch runs the K steps of every game (multi-step "
+            "launch": ("hipGraph replay of the K timed steps and their RCCL exchanges" if graph is not None and gather_buf is not None
+                       else f"one {'mrts_rollout_uniform_dev' if uniform else 'mrts_rollout_fused_dev'} call: ONE k_env launch runs the K steps of every game (multi-step "
                        "launch, each game's state kept in LDS between its steps; every step's observation, masks, "
                        "rewards, dones and next action rows written to HBM)" if multi
                        else "one mrts_rollout_uniform_dev call (K fused policy+step launches from C++)" if native and uni_fused
