@@ -35,11 +35,15 @@ def main():
     burn = int(os.environ.get("BURNIN", 1000))
     K = 100
     PO = os.environ.get("PO", "0") == "1"
+    UNI = os.environ.get("UNIFORM", "0") == "1"  # c2: fused unmasked uniform rows, no masks
     env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=SEED, partial_obs=PO,
-                       max_units=int(os.environ.get("MAXU", 0)))
+                       max_units=int(os.environ.get("MAXU", 0)), with_masks=not UNI)
+    roll = ((lambda first, n: env.rollout_uniform(SEED, first, n)) if UNI
+            else (lambda first, n: env.rollout_fused(SEED, first, n)))
     env.reset()
-    env.random_policy(SEED, 0)
-    env.rollout_fused(SEED, 1, burn)
+    if not UNI:
+        env.random_policy(SEED, 0)
+    roll(1, burn)
     torch.cuda.synchronize()
     ck = env.checkpoint()
     acts = env.actions.clone()
@@ -49,9 +53,9 @@ def main():
         assert L.mrts_set_ablate(bits) == 0
         env.restore(ck)
         env.actions.copy_(acts)
-        env.rollout_fused(SEED, burn + 1, 5)
+        roll(burn + 1, 5)
         s.record()
-        env.rollout_fused(SEED, burn + 6, K)
+        roll(burn + 6, K)
         e.record()
         e.synchronize()
         return 1e3 * s.elapsed_time(e) / K  # us per step
@@ -76,13 +80,13 @@ def main():
     L.mrts_set_ablate(0)
     env.restore(ck)
     env.actions.copy_(acts)
-    env.rollout_fused(SEED, burn + 1, 30)
+    roll(burn + 1, 30)
     torch.cuda.synchronize()
     d0 = [env.dump_state(x) for x in range(0, 64, 2)]
     L.mrts_set_ablate((1 << 14) - 1)  # every doubling (no skips)
     env.restore(ck)
     env.actions.copy_(acts)
-    env.rollout_fused(SEED, burn + 1, 30)
+    roll(burn + 1, 30)
     torch.cuda.synchronize()
     d1 = [env.dump_state(x) for x in range(0, 64, 2)]
     print(json.dumps({"dynamics_unchanged": all(np.array_equal(a, b) for a, b in zip(d0, d1)), "summary": out}), flush=True)
