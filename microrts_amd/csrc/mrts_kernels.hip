@@ -130,6 +130,19 @@ DEV int lane_id() { return (int)threadIdx.x; }
 // reads (the same game runs on the same XCD every launch: tools/xcd_placement.py) keep theirs:
 // 32 full-observability planes (c3 +3.2 %), 128 partially observable planes (c5 +3.4 %), 64 delta
 // mask records (byte-granular partial lines: c3 -5 %, off).  profiles/round2_store_policy.md.
+#ifndef MRTS_MULTI_NOPRIO
+#define MRTS_MULTI_NOPRIO 0
+#endif
+// issue-priority thresholds on a game's unit count (k_env): 1 / 2 / 3 from T1 / T2 / T3 units
+#ifndef MRTS_PRIO_T1
+#define MRTS_PRIO_T1 24
+#endif
+#ifndef MRTS_PRIO_T2
+#define MRTS_PRIO_T2 30
+#endif
+#ifndef MRTS_PRIO_T3
+#define MRTS_PRIO_T3 36
+#endif
 #ifndef MRTS_WT
 #define MRTS_WT 161
 #endif
@@ -3727,10 +3740,10 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         G.nextStep();
         freshObs = true;
     }
-    if (MODE != MODE_RESET) {
+    if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
-        const int q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
+        const int q = G.nu >= MRTS_PRIO_T3 ? 3 : G.nu >= MRTS_PRIO_T2 ? 2 : G.nu >= MRTS_PRIO_T1 ? 1 : 0;
         if (q == 0) {
             if (it > 0) __builtin_amdgcn_s_setprio(0);
         } else if (q == 1) __builtin_amdgcn_s_setprio(1);
