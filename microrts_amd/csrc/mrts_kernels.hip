@@ -134,14 +134,19 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #define MRTS_MULTI_NOPRIO 0
 #endif
 // issue-priority thresholds on a game's unit count (k_env): 1 / 2 / 3 from T1 / T2 / T3 units
+// (units + own idle units; measured against units alone at 24 / 30 / 36: c3 +1.8 % at K = 200,
+// +0.8 % at K = 20)
+#ifndef MRTS_PRIO_IDLE
+#define MRTS_PRIO_IDLE 1
+#endif
 #ifndef MRTS_PRIO_T1
-#define MRTS_PRIO_T1 24
+#define MRTS_PRIO_T1 29
 #endif
 #ifndef MRTS_PRIO_T2
-#define MRTS_PRIO_T2 30
+#define MRTS_PRIO_T2 35
 #endif
 #ifndef MRTS_PRIO_T3
-#define MRTS_PRIO_T3 36
+#define MRTS_PRIO_T3 41
 #endif
 #ifndef MRTS_WT
 #define MRTS_WT 161
@@ -3743,7 +3748,13 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
-        const int q = G.nu >= MRTS_PRIO_T3 ? 3 : G.nu >= MRTS_PRIO_T2 ? 2 : G.nu >= MRTS_PRIO_T1 ? 1 : 0;
+#if MRTS_PRIO_IDLE
+        // units + idle units (the step's decode / issue / mask / policy work grows with the idle ones)
+        const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
+#else
+        const int wq = G.nu;
+#endif
+        const int q = wq >= MRTS_PRIO_T3 ? 3 : wq >= MRTS_PRIO_T2 ? 2 : wq >= MRTS_PRIO_T1 ? 1 : 0;
         if (q == 0) {
             if (it > 0) __builtin_amdgcn_s_setprio(0);
         } else if (q == 1) __builtin_amdgcn_s_setprio(1);
