@@ -3748,13 +3748,15 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
     if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
-#if MRTS_PRIO_IDLE
-        // units + idle units (the step's decode / issue / mask / policy work grows with the idle ones)
-        const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
-#else
-        const int wq = G.nu;
-#endif
-        const int q = wq >= MRTS_PRIO_T3 ? 3 : wq >= MRTS_PRIO_T2 ? 2 : wq >= MRTS_PRIO_T1 ? 1 : 0;
+        int q;
+        if (MRTS_PRIO_IDLE && FIX == 16) {
+            // the c3 shape (four games per SIMD): units + own idle units (the step's decode / issue /
+            // mask / policy work grows with the idle ones)
+            const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
+            q = wq >= MRTS_PRIO_T3 ? 3 : wq >= MRTS_PRIO_T2 ? 2 : wq >= MRTS_PRIO_T1 ? 1 : 0;
+        } else {  // units (the idle count's ballot costs the latency-bound one-game-per-SIMD c2 4.5 %)
+            q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
+        }
         if (q == 0) {
             if (it > 0) __builtin_amdgcn_s_setprio(0);
         } else if (q == 1) __builtin_amdgcn_s_setprio(1);
