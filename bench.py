@@ -204,7 +204,13 @@ def main():
     uniform = a.policy in ("uniform", "uniform-split")
     mode = {"fused": fused, "uni_fused": a.policy == "uniform"}
 
+    # the exchange's int16 transport written by the step kernel itself (full observability: no
+    # narrowing pass); partially observable views keep the narrowing copy in push()
+    kernel16 = gather_buf is not None and not gather_buf.gloo and not a.po
+
     def one_step(k, ev=None):
+        if kernel16:
+            env.set_obs16(gather_buf.begin())
         fused = mode["fused"]
         if uniform and mode["uni_fused"]:  # one launch: rows drawn and written by the step kernel
             if ev is not None:
@@ -213,7 +219,7 @@ def main():
             if ev is not None:
                 ev[1].record(torch.cuda.current_stream(env.device))
             if gather_buf is not None:
-                gather_buf.push(env.obs)
+                gather_buf.finish() if kernel16 else gather_buf.push(env.obs)
             return
         if uniform:
             env.uniform_policy(SEED, k)
@@ -230,7 +236,7 @@ def main():
         if ev is not None:
             ev[1].record(torch.cuda.current_stream(env.device))
         if gather_buf is not None:
-            gather_buf.push(env.obs)
+            gather_buf.finish() if kernel16 else gather_buf.push(env.obs)
 
     env.reset()
     if fused:
@@ -468,7 +474,8 @@ def main():
                               else f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
                               if (native or graph is not None) else f"{event_kind} around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (
-                f", per-step RCCL int16 observation {a.gather_obs} overlapped on a comm stream" if gather_buf is not None
+                f", per-step RCCL int16 observation {a.gather_obs} overlapped on a comm stream"
+                + (" (int16 transport written by the step kernel)" if kernel16 else "") if gather_buf is not None
                 else ", no collective in the step"),
         },
         "step_kernel_ms": kern_ms,

@@ -165,6 +165,12 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
                            uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
                            int32_t n_steps, void* stream);
 #define MRTS_MAX_ITER 1024
+/* Every later observation write of this handle (any step / reset call with an observation buffer)
+ * also writes the planes as int16 into d_obs16 [n_slots][C][H][W] (every value fits: hp, unit
+ * types, action types, 0..2 owner, terrain, resources <= 32767 by map validation) — the compact
+ * transport of the observation exchange, written by the step kernel instead of a
+ * separate narrowing pass.  NULL turns it off.  Full observability only; 8-byte aligned. */
+int mrts_set_obs16(mrts_env* env, int16_t* d_obs16);
 /* on = 0: mrts_rollout_fused_dev issues one launch per step (for comparison / debugging). */
 int mrts_set_multi_step(mrts_env* env, int32_t on);
 /* 1 when mrts_rollout_fused_dev on this handle runs several steps per launch (shape + switch), else 0. */

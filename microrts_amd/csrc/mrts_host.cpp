@@ -474,6 +474,7 @@ struct mrts_env {
     // last launch wrote observations to (null after a launch that changed the state without one, or
     // after an invalidation) and the per-game render records (PO handles on delta-capable maps)
     int obsDelta = 0;
+    int16_t* obs16 = nullptr;  // mrts_set_obs16: int16 copy of each observation write (full observability)
     int multiStep = 1;  // mrts_rollout_fused_dev may run several steps per launch (mrts_set_multi_step)
     const int32_t* lastObsPtr = nullptr;
     int32_t* d_poPrev = nullptr;
@@ -509,6 +510,7 @@ struct mrts_env {
     // every launch that changes the state or writes observations; the library-owned buffer of the
     // host-pointer API is always persistent
     void prepObs(KDyn& D) {
+        D.obs16 = D.obs ? obs16 : nullptr;
         D.obs_delta = (D.obs && D.obs == lastObsPtr && (obsDelta || D.obs == d_obs)) ? 1 : 0;
         D.po_prev = D.obs ? d_poPrev : nullptr;
         D.po_words = poWords;
@@ -1108,6 +1110,14 @@ int mrts_set_obs_delta(mrts_env* env, int32_t on) {
     if (!env) return fail(Fail{-EINVAL, "null handle"});
     env->obsDelta = on ? 1 : 0;
     env->lastObsPtr = nullptr;
+    return 0;
+}
+
+int mrts_set_obs16(mrts_env* env, int16_t* d_obs16) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    if (d_obs16 && env->partialObs) return fail(Fail{-EINVAL, "the int16 observation copy is for full observability"});
+    if ((uintptr_t)d_obs16 & 7) return fail(Fail{-EINVAL, "misaligned buffer (8 bytes)"});
+    env->obs16 = d_obs16;
     return 0;
 }
 

@@ -153,6 +153,9 @@ struct KDyn {
     int32_t* uni_actions;
     uint64_t uni_seed;
     uint32_t uni_step, uni_slot_base;
+    // full observability: the observation planes also as int16 [n_slots][C][HW] (the compact transport
+    // of the observation exchange, mrts_set_obs16); null = off
+    int16_t* obs16;
     // multi-step launch (mrts_rollout_fused_dev): > 1 = this launch runs n_iter consecutive fused steps
     // per game (pol_step, pol_step + 1, ...), the state kept in LDS in between (specialised
     // full-observability self-play kernels; the host issues it only in the steady fused state:

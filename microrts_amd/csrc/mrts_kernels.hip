@@ -212,6 +212,10 @@ DEV int dyo(int d) { return d == 0 ? -1 : (d == 2 ? 1 : 0); }
 DEV int clampdir(int d) { return (d >= 0 && d <= 3) ? d : ACT_INVALID; }
 
 DEV int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+// four int32 values (each within int16) as four packed int16
+DEV uint2 pk16(int4 w) {
+    return make_uint2(((uint32_t)w.x & 0xFFFFu) | ((uint32_t)w.y << 16), ((uint32_t)w.z & 0xFFFFu) | ((uint32_t)w.w << 16));
+}
 DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 DEV uint32_t uniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 DEV uint64_t ballot(bool p) { return __ballot(p); }
@@ -2455,6 +2459,23 @@ struct Game {
                     if (SC1_OBS) st4sc1(rs, (uint32_t)(pl * HW + c4) * 4u, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
                     else st4<WT_OBS>(o0 + (size_t)pl * HW + c4, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
                 }
+                if (MRTS_UNLIKELY(D.obs16 != nullptr)) {  // the int16 transport copy (mrts_set_obs16)
+                    int16_t* h0 = D.obs16 + (size_t)slot0 * D.C * HW;
+#pragma unroll
+                    for (int pl = 0; pl < 6; pl++) {
+                        int4 w = make_int4(v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
+                        *(uint2*)(h0 + (size_t)pl * HW + c4) = pk16(w);
+                        if (nslots == 2) {
+                            if (pl == 2) {
+                                w.x = w.x ? 3 - w.x : 0;
+                                w.y = w.y ? 3 - w.y : 0;
+                                w.z = w.z ? 3 - w.z : 0;
+                                w.w = w.w ? 3 - w.w : 0;
+                            }
+                            *(uint2*)(h0 + (size_t)(D.C + pl) * HW + c4) = pk16(w);
+                        }
+                    }
+                }
                 if (nslots == 2) {  // the other player's view differs only in the owner plane
                     int32_t* o1 = o0 + (size_t)D.C * HW;
 #pragma unroll
@@ -2479,6 +2500,11 @@ struct Game {
                     obsCell(c, player0 + i, v);
 #pragma unroll
                     for (int pl = 0; pl < 6; pl++) o[(size_t)pl * HW + c] = v[pl];
+                    if (D.obs16) {
+                        int16_t* h = D.obs16 + (size_t)(slot0 + i) * D.C * HW;
+#pragma unroll
+                        for (int pl = 0; pl < 6; pl++) h[(size_t)pl * HW + c] = (int16_t)v[pl];
+                    }
                 }
             }
         }

@@ -104,6 +104,33 @@ class ObservationGather:
         self.fired[b] = True
         return self.recv[b]
 
+    def begin(self):
+        """Kernel-written transport (DeviceVecEnv.set_obs16): the int16 send buffer the NEXT step
+        must write, after making the current stream wait until the collective that last read it
+        (two steps ago) finished.  Pass it to env.set_obs16, run the step, then call finish()."""
+        b = self.i & 1
+        if self.comm is not None and self.fired[b]:
+            torch.cuda.current_stream(self.send[b].device).wait_event(self.done[b])
+        return self.send[b]
+
+    def finish(self):
+        """The step that wrote begin()'s buffer is enqueued: start its collective (as push(), without
+        the narrowing copy).  Returns this step's receive buffer (None on non-learner ranks)."""
+        b = self.i & 1
+        self.i += 1
+        if self.comm is None:
+            self._collective(b)
+            return self.recv[b]
+        cur = torch.cuda.current_stream(self.send[b].device)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ready)
+            self._collective(b)
+            self.done[b].record(self.comm)
+        self.fired[b] = True
+        return self.recv[b]
+
     def wait(self):
         """Make the current stream wait for every collective issued so far."""
         if self.comm is not None:

@@ -459,6 +459,16 @@ class DeviceVecEnv:
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
+    def set_obs16(self, out):
+        """Every later observation write also fills `out` (int16 [n_slots][C][H][W], or None = off) —
+        the observation exchange's compact transport, written by the step kernel
+        (mrts_set_obs16; full observability)."""
+        import torch
+        if out is not None:
+            assert out.dtype == torch.int16 and tuple(out.shape) == tuple(self.obs.shape) and out.is_contiguous()
+        _lib.check(self._h.L.mrts_set_obs16(self._h.h, self._p(out) if out is not None else None))
+        self._obs16 = out  # keep it alive while the handle writes into it
+
     def set_multi_step(self, on):
         """rollout_fused may run several steps per launch (default; mrts_set_multi_step)."""
         _lib.check(self._h.L.mrts_set_multi_step(self._h.h, 1 if on else 0))

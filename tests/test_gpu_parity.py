@@ -926,6 +926,47 @@ def test_uniform_fused_matches_split(mp, n_sp, n_bot, po, masks):
     b.close()
 
 
+@pytest.mark.parametrize("mp,n_sp,n_bot", [("maps/16x16/basesWorkers16x16.xml", 24, 0),
+                                          ("maps/8x8/basesWorkers8x8.xml", 16, 6),
+                                          ("maps/NoWhereToRun9x8.xml", 8, 2)])
+def test_obs16_copy_matches_obs(mp, n_sp, n_bot):
+    """mrts_set_obs16: every observation write also leaves the planes as int16 in the given buffer —
+    after reset, plain steps, fused steps and multi-step rollouts (auto-resets included), on the
+    specialised and generic kernels; switching the buffer and turning it off work too."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    bots = ["RandomBiasedAI"] * n_bot if n_bot else None
+    env = DeviceVecEnv(n_sp, n_bot, 120, [mp] * (n_sp + n_bot), seed=12, ai2s=bots)
+    bufs = [torch.full(tuple(env.obs.shape), -7, dtype=torch.int16, device=env.device) for _ in range(2)]
+    env.set_obs16(bufs[0])
+    env.reset()
+    env.synchronize()
+    assert torch.equal(bufs[0], env.obs.to(torch.int16)), "after reset"
+    env.random_policy(SEED, 0)
+    for k in range(200):
+        b = bufs[k & 1]
+        env.set_obs16(b)
+        if k % 3 == 0:
+            env.step()
+            env.random_policy(SEED, k + 1)
+        else:
+            env.step_fused(SEED, k + 1)
+        env.synchronize()
+        assert torch.equal(b, env.obs.to(torch.int16)), f"step {k}"
+    env.set_obs16(bufs[0])
+    env.rollout_fused(SEED, 300, 50)  # multi-step launches on the self-play-only 16x16 handle
+    env.synchronize()
+    assert torch.equal(bufs[0], env.obs.to(torch.int16)), "after a rollout"
+    env.set_obs16(None)
+    before = bufs[0].clone()
+    env.step_fused(SEED, 400)
+    env.synchronize()
+    assert torch.equal(bufs[0], before), "written after set_obs16(None)"
+    assert not env.error_flags().any()
+    env.close()
+
+
 def test_host_mask_views_match_copies():
     """getMasks(copy=False): views of the library-owned pinned arrays (mrts_get_masks_host /
     mrts_get_masks_i32_host) hold the same masks as the copying form, and the next call refills them."""
