@@ -455,6 +455,10 @@ struct Game {
     bool fwdWritten;       // this launch wrote the forwarded action words (store() stamps H_FWD)
     uint32_t lkey, lsnap;  // PO delta: lane l's hp | resources << 16 as loaded, its previous render's snapshot byte
     bool poLds;            // the last PO render (writeObsPOFast2) left its whole record in LDS as well
+    // multi-step launch: this is the launch's last iteration (the state block's internal copies — the
+    // mask row sets, the forwarded words — are stored then only); the first (the terrain plane,
+    // static, is written by the first observation write of the launch only).  One step: both.
+    bool lastIt, firstIt;
     uint64_t killedLanes;  // cycle(): ready-list lanes whose unit was killed earlier in the cycle
     int curP;              // player whose pa is being issued
     // CloserToEnemyBase/Unit: each player's first Base before the step (x | y << 8, -1 = none) and
@@ -498,6 +502,8 @@ struct Game {
         fwdWritten = false;
         lfwd = 0;
         poLds = false;
+        lastIt = true;
+        firstIt = true;
         polStep = d.pol_step;
         uniStep = d.uni_step;
         freshLane();
@@ -2454,8 +2460,11 @@ struct Game {
                     v[j][5] = sc[j] == WALL ? 1 : 0;
                 }
                 const __amdgpu_buffer_rsrc_t rs = bufRsrc(o0, (uint32_t)(nslots * D.C * HW * 4));
+                // the terrain plane (5) is static: within a multi-step launch only its first write stores it
+                const int npl = firstIt ? 6 : 5;
 #pragma unroll
                 for (int pl = 0; pl < 6; pl++) {
+                    if (pl >= npl) break;
                     if (SC1_OBS) st4sc1(rs, (uint32_t)(pl * HW + c4) * 4u, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
                     else st4<WT_OBS>(o0 + (size_t)pl * HW + c4, v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
                 }
@@ -2480,6 +2489,7 @@ struct Game {
                     int32_t* o1 = o0 + (size_t)D.C * HW;
 #pragma unroll
                     for (int pl = 0; pl < 6; pl++) {
+                        if (pl >= npl) break;
                         int4 w = make_int4(v[0][pl], v[1][pl], v[2][pl], v[3][pl]);
                         if (pl == 2) {
                             w.x = w.x ? 3 - w.x : 0;
@@ -3351,7 +3361,7 @@ struct Game {
                 const uint32_t mine = l == 0 ? (uint32_t)m : (uint32_t)(m >> 32);
                 if (l < 2 && w + l < MW) {
                     if (D.source) D.source[(size_t)slot * MW + w + l] = mine;
-                    pg[p * MW + w + l] = mine;
+                    if (lastIt) pg[p * MW + w + l] = mine;
                 }
                 if (delta) {
                     const uint64_t old = (uint64_t)mprev[p * MW + w] | (w + 1 < MW ? (uint64_t)mprev[p * MW + w + 1] << 32 : 0ull);
@@ -3426,7 +3436,7 @@ struct Game {
         if (total > 64) return false;
         if (l < NW) {
             if (D.source) D.source[(size_t)(slot0 + i) * MW + w] = cur;
-            prevG()[(i ? pl1 : pl0) * MW + w] = cur;
+            if (lastIt) prevG()[(i ? pl1 : pl0) * MW + w] = cur;  // the next launch's copy
             mprev[(i ? pl1 : pl0) * MW + w] = cur;
         }
         if (total == 0) return true;
@@ -3571,7 +3581,7 @@ struct Game {
             cur = nb[l];
             old = mprev[(i ? pl1 : pl0) * MW + w];
             if (D.source) D.source[(size_t)(slot0 + i) * MW + w] = cur;
-            prevG()[(i ? pl1 : pl0) * MW + w] = cur;
+            if (lastIt) prevG()[(i ? pl1 : pl0) * MW + w] = cur;  // the next launch's copy
             mprev[(i ? pl1 : pl0) * MW + w] = cur;  // the next iteration's base (multi-step launch)
         }
         const bool pol = D.pol_actions && D.pol_delta;
@@ -3615,7 +3625,7 @@ struct Game {
                 st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
                 if (fwdW) {
                     lfwd = packFwd(a);  // the next iteration of a multi-step launch decodes from it
-                    st1<WT_STATE>(st() + stateFwdOff(CAP, HW) + l, (int32_t)lfwd);
+                    if (lastIt) st1<WT_STATE>(st() + stateFwdOff(CAP, HW) + l, (int32_t)lfwd);  // the next launch's
                 }
             }
         }
@@ -3771,6 +3781,8 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         G.nextStep();
         freshObs = true;
     }
+    G.lastIt = it == niter - 1;
+    G.firstIt = it == 0;
     if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
