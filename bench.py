@@ -393,6 +393,8 @@ def main():
     n_games = S // 2
     m_bytes = 0 if uniform else (dirty * K if a.mask_mode == "delta" else HW * K)
     o_bytes = obs_chunks * 16  # C * HW * 4 for a full write
+    if launch_ms is not None and not a.po:  # a multi-step launch stores the static terrain plane once
+        o_bytes = (C - 1) * HW * 4 + HW * 4 / a.steps
     # fused policy: the idle units' rows arrive as one forwarded 4-B word each (KDyn.fwd_read), and the
     # step writes that word next to the 28-B row it leaves in the action tensor
     # fused uniform policy: no row is read (the idle units' rows are drawn in registers), and every row
@@ -400,15 +402,18 @@ def main():
     uni_fused = uniform and mode["uni_fused"]
     row_in = 4 if fused else 0 if uni_fused else 28
     # per game: the state (header + unit rows) read and written, the terrain read, both players' row sets
-    # read and written — per step; a multi-step launch keeps state, terrain and row sets in LDS, so it
-    # loads / stores them once per launch (1/K per step) and only writes the row sets each step
+    # read and written — per step; a multi-step launch keeps state, terrain, row sets and forwarded
+    # words in LDS / registers, so it loads them at its first step and stores them after its last
+    # (1/K per step)
     state_io = 2 * (64 + 28 * mean_units) + HW
-    if launch_ms is not None:
-        contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * ((state_io + 2 * MWB) / a.steps + 2 * MWB)
+    multi_l = launch_ms is not None
+    if multi_l:
+        row_in = row_in / a.steps if fused else row_in
+        contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * (state_io + 2 * 2 * MWB) / a.steps
     else:
         contract = S * (rows * row_in + o_bytes + m_bytes + MWB) + n_games * (state_io + 2 * 2 * MWB)
     if fused:  # the policy's action rows (and their forwarded words) leave the step kernel too
-        contract += S * (dirty if a.mask_mode == "delta" else HW) * 28 + S * rows * 4
+        contract += S * (dirty if a.mask_mode == "delta" else HW) * 28 + S * rows * 4 / (a.steps if multi_l else 1)
     if uni_fused:
         contract += S * HW * 28
     survey = S * (HW * 7 * 4 + C * HW * 4 + (0 if uniform else HW * K) + (16 * mean_units + 2 * HW + 16))
