@@ -307,7 +307,7 @@ def main():
     # multi-step launches: the native fused rollout runs the K steps of every game in one k_env launch
     # (state in LDS between steps; mrts_rollout_fused_dev), so the launch's own duration is the
     # kernel time — fence-free events around it inside the timed window
-    multi = native and (fused or (uniform and mode["uni_fused"])) and env.multi_step_capable
+    multi = native and ((fused and env.fused_multi_step) or (uniform and mode["uni_fused"] and env.multi_step_capable))
     roll_ev = (_FenceFreeEvent(), _FenceFreeEvent()) if multi and event_kind.startswith("hipEvent") else None
     run_steps(a.burnin, a.warmup)  # the W untimed warmup steps, immediately before the window
     if world > 1:

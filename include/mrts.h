@@ -103,7 +103,14 @@ int mrts_dims(const mrts_env* env, int32_t* n_slots, int32_t* H, int32_t* W, int
 
 /* Host-pointer API (mirrors the Java reuse semantics: returned arrays are library-owned and valid
  * until the next call on the handle, GameState.java:923-925 / JNIGridnetClient.java:211-215). */
-int mrts_reset(mrts_env* env, const int32_t* players, mrts_responses* out);                       /* reset(int[]) :179-211 */
+/* reset(int[]) :179-211.  Reward / done after a reset follow the Java clients: an agent-vs-bot or
+ * bot-only env zeroes every slot (JNIGridnetClient.java:248-251, JNIBotClient.java:159-162); a
+ * self-play game zeroes only reward functions 0 and 1 — its loop runs to rewards.length == 2 players,
+ * not to rfs.length (JNIGridnetClientSelfPlay.java:103-104,235-238) — so functions >= 2 keep the
+ * values the buffer held (the previous step's; zeros before any step).  With ONE reward function
+ * Java's self-play reset throws ArrayIndexOutOfBounds (rewards[i][1]); here the one slot is zeroed
+ * (DESIGN.md §8).  The auto-reset inside a step returns the terminal values of every slot (:248-263). */
+int mrts_reset(mrts_env* env, const int32_t* players, mrts_responses* out);
 int mrts_step(mrts_env* env, const int32_t* actions, const int32_t* players, mrts_responses* out); /* gameStep :213-297 */
 int mrts_get_masks(mrts_env* env, int32_t player, uint8_t* out /* [n_slots][H][W][K] */);          /* getMasks :307-316 */
 /* gameStep with the Java layout, int[][][] action (:213), as flat int32 [n_slots][n_rows][8]: row =
@@ -147,7 +154,11 @@ int mrts_policy_dev(mrts_env* env, const uint8_t* d_masks, const uint32_t* d_sou
  * (d_masks required), then overwrites d_actions with the policy's actions for step `next_step`
  * sampled from the masks just written — identical to mrts_policy_dev(env, d_masks, ..., seed,
  * next_step, d_actions) afterwards, without the second launch and its full pass.  Consecutive fused
- * calls on the same buffers rewrite only changed rows (mask_delta). */
+ * calls on the same buffers rewrite only changed rows (mask_delta).
+ * IMPORTANT: the rows a fused call samples are also kept in the handle's state and the next fused
+ * call on the same d_actions decodes from that copy, not from d_actions.  Any write to d_actions
+ * between fused calls (e.g. overriding some units' rows) MUST be followed by mrts_policy_invalidate(),
+ * otherwise the written rows are ignored.  The same holds for mrts_rollout_fused_dev. */
 int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                         uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step,
                         void* stream);
@@ -173,7 +184,9 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
 int mrts_set_obs16(mrts_env* env, int16_t* d_obs16);
 /* on = 0: mrts_rollout_fused_dev issues one launch per step (for comparison / debugging). */
 int mrts_set_multi_step(mrts_env* env, int32_t on);
-/* 1 when mrts_rollout_fused_dev on this handle runs several steps per launch (shape + switch), else 0. */
+/* 1 when this handle's kernel shape and the switch allow multi-step launches, else 0.  Then
+ * mrts_rollout_uniform_dev uses them; mrts_rollout_fused_dev uses them only on a handle created with
+ * mask_delta = 1 (its steady fused state needs delta masks) — otherwise one launch per step. */
 int mrts_multi_step_capable(const mrts_env* env);
 /* Unmasked uniform random policy (BASELINE config c2): every row of d_actions
  * [n_slots][H*W][7] gets type in [0,6), the four directions in [0,4), produce type in [0,ntypes)
@@ -204,7 +217,8 @@ int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d
  * makes the next write a full one. */
 int mrts_set_obs_delta(mrts_env* env, int32_t on);
 int mrts_obs_invalidate(mrts_env* env);
-/* the next mrts_policy_dev call writes every row */
+/* the next mrts_policy_dev call writes every row, and the next fused step decodes the rows of
+ * d_actions (not the copy the previous fused call kept): call it after writing d_actions yourself */
 int mrts_policy_invalidate(mrts_env* env);
 /* Optional compact output of every mask write: mask slot 0 ("own unit without an action here") as
  * bits, uint32 [n_slots][ceil(H*W/32)] (sticky; NULL disables).  mrts_policy_dev uses it, when
@@ -258,7 +272,7 @@ int mrts_env_steps(mrts_env* env, int32_t* out);
  * `slot`; unit IDs are list positions (Java's come from a JVM-global counter).  NUL-terminated;
  * returns the length, or -(length + 1) when cap is too small.  Synchronous. */
 int mrts_get_state_json(mrts_env* env, int32_t slot, char* buf, int32_t cap);
-/* GameState.fromJSON (rts/GameState.java:889-915) into the game behind `slot` (both slots of a
+/* GameState.fromJSON (rts/GameState.java:897-915) into the game behind `slot` (both slots of a
  * self-play game): time, players, units, terrain and assignments from the JSON; envSteps and the
  * cancel counter restart at 0; the game's random streams are kept.  The next mask / policy write of
  * the handle is a full one.  Synchronous. */

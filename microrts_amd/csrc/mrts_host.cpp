@@ -191,9 +191,9 @@ UttInfo makeUtt(int version, int crs) {
     return I;
 }
 
-// UnitTypeTable.fromJSON (:414-433) + UnitType.createStub / updateFromJSON (UnitType.java:156-161,
-// 217-248), including its quirks: harvestTime is read from "produceTime", returnTime is not read,
-// and absent members take updateFromJSON's defaults (harvestAmount and sightRadius default to 10,
+// UnitTypeTable.fromJSON (:414-433) + UnitType.createStub / updateFromJSON
+// (UnitType.java:156-161, 217-248), including its quirks: harvestTime is read from "produceTime",
+// returnTime is not read, and absent members take updateFromJSON's defaults (harvestAmount and sightRadius default to 10,
 // canMove / canAttack to false).  Limits of this build: <= 8 types, type IDs equal to their list
 // positions, <= 4 produced types, attack range <= 3 (K <= 80 mask slots: an idle unit's mask is
 // parked as 80 bits in its free assignment words), hp in int16, positive durations; every produced /
@@ -414,7 +414,7 @@ MapDef parseMap(const std::string& path, const UttInfo& utt) {
         const std::string ut = x.substr(a, b - a);
         MapDef::U u;
         const std::string tn = attrOf(ut, "type");
-        u.type = utt.typeOf(tn);  // utt.getUnitType(name) (Unit.java:608)
+        u.type = utt.typeOf(tn);  // utt.getUnitType(name) (Unit.java:610)
         if (u.type < 0) throw Fail{-EINVAL, "map: unknown unit type " + tn};
         u.id = std::stoll(attrOf(ut, "ID"));
         u.player = toInt(attrOf(ut, "player"));
@@ -782,6 +782,10 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         HIPCHK(hipHostMalloc(&env->h_reward, S * R * 8, hipHostMallocDefault));
         HIPCHK(hipHostMalloc(&env->h_done, S * R, hipHostMallocDefault));
         HIPCHK(hipMemset(env->d_players, 0, S * 4));
+        // the Java clients' arrays start as zeros (new double[rfs.length], JNIGridnetClientSelfPlay.java:
+        // 134-135); a self-play reset leaves slots >= 2 alone, so they must not start as garbage
+        HIPCHK(hipMemset(env->d_reward, 0, S * R * 8));
+        HIPCHK(hipMemset(env->d_done, 0, S * R));
         // static kernel parameters → device buffer
         env->buildStatic();
         HIPCHK(hipMalloc(&env->d_static, sizeof(KStatic)));
@@ -1477,7 +1481,7 @@ static std::string gameToJson(const mrts_env* env, const std::vector<int32_t>& s
     return w.str();
 }
 
-// GameState.fromJSON (rts/GameState.java:889-915): PhysicalGameState.fromJSON (:735-756, terrain raw
+// GameState.fromJSON (rts/GameState.java:897-915): PhysicalGameState.fromJSON (:735-756, terrain raw
 // or A/B), Player.fromJSON, Unit.fromJSON (Unit.java:629-642: hitpoints default 1), the actions by
 // unit ID in array order (UnitAction.fromJSON, UnitAction.java:647-658).  A new GameState: time from
 // the JSON, unitCancelationCounter 0.  Writes the words of block `s` it describes; everything else

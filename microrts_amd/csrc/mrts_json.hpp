@@ -1,6 +1,6 @@
 // mrts_json.hpp — a small JSON reader (RFC 8259 values; numbers kept as double + int64) for the
 // reference's JSON inputs: unit-type tables (UnitTypeTable.fromJSON, rts/units/UnitTypeTable.java:
-// 414-433) and game states (GameState.fromJSON, rts/GameState.java:889-915).  Header-only.
+// 414-433) and game states (GameState.fromJSON, rts/GameState.java:897-915).  Header-only.
 #pragma once
 #include <cstdint>
 #include <cstdlib>

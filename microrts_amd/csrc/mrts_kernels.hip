@@ -278,7 +278,7 @@ struct JRand {
 };
 DEV uint64_t rng_of(int lo, int hi) { return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32); }
 
-// Snapshot byte per unit for PartiallyObservableGameState views (rts/PartiallyObservableGameState.java:90-109):
+// Snapshot byte per unit for PartiallyObservableGameState views (rts/PartiallyObservableGameState.java:35-54):
 // bit p = unit is in player p's snapshot list; bits 2-4 / 5-7 = (snapshot UAA action type + 1), 0 = none.
 DEV int snap_in(uint32_t b, int p) { return (b >> p) & 1; }
 DEV int snap_act(uint32_t b, int p) { return (int)((b >> (2 + 3 * p)) & 7); }
@@ -1050,7 +1050,7 @@ struct Game {
         issueFills(p, fillDur);
     }
 
-    // Base reservations of every current assignment the deciding view holds (PlayerAction.java:497-505,
+    // Base reservations of every current assignment the deciding view holds (PlayerAction.java:387-394,
     // merged as ResourceUsage.java:92-97); in a PO view only snapshot units' assignments count.
     DEV void baseReservations(int p, int& r0, int& r1) {
         const int NB = (HW + 2 * W + 31) / 32;
@@ -1079,7 +1079,7 @@ struct Game {
         wsync();
     }
 
-    // PlayerAction.fromVectorAction (rts/PlayerAction.java:495-528): decoded rows in ascending cell
+    // PlayerAction.fromVectorAction (rts/PlayerAction.java:384-417): decoded rows in ascending cell
     // order; accepted iff ua.ru.consistentWith(running ru) (rts/ResourceUsage.java:31-50).  Only the
     // acceptance chain is serial; accepted units get UA_PA.
     // issueNow (self-play, all units in one wave): the accepted rows are issued straight from the
@@ -1243,7 +1243,7 @@ struct Game {
         if (isAcc) irank = __popcll(accR & ((1ull << rank) - 1ull));
         return ballot(isAcc);
     }
-    // ua.ru.consistentWith(running ru) for the n candidates in rank order (PlayerAction.java:503-520);
+    // ua.ru.consistentWith(running ru) for the n candidates in rank order (PlayerAction.java:400-415);
     // returns the accepted lanes
     // keepBits: `bits` is left as it was (the chain's additions stay in registers)
     // irank: each accepted lane's rank among the accepted (the pa's issue order)
@@ -1466,7 +1466,7 @@ struct Game {
     }
 
     // Issue index over ALL units (GameState.issue checks every present assignment, :255-262); under
-    // full observability it is also every view's base ResourceUsage (PlayerAction.java:497-505).
+    // full observability it is also every view's base ResourceUsage (PlayerAction.java:387-394).
     DEV void buildIndex() {
 #ifdef MRTS_PHASE_TIMING
 #ifndef MRTS_SPAN_ONLY
@@ -1618,7 +1618,7 @@ struct Game {
         issueBatch(isPA, rank, n, s, t, prm, tx, ty, ut);
     }
     // Agent pa = [accepted rows in cell order] + PlayerAction.fillWithNones(gs, p, fillDur)
-    // (rts/PlayerAction.java:328-346) in list order; AI pa (RandomBiasedAI / PassiveAI) = its units
+    // (rts/PlayerAction.java:217-235) in list order; AI pa (RandomBiasedAI / PassiveAI) = its units
     // in list order (listOrder).
     DEV void issuePlayer(int p, int fillDur, bool listOrder) {
         curP = p;
@@ -1856,7 +1856,7 @@ struct Game {
     }
 
     // ------------------------------------------------------------------ PO snapshot
-    // new PartiallyObservableGameState(gs, p) (rts/PartiallyObservableGameState.java:90-109):
+    // new PartiallyObservableGameState(gs, p) (rts/PartiallyObservableGameState.java:35-54):
     // the list keeps p's units and every other unit whose cell p observes (:116-126); the
     // assignment map is the live one at this moment (UAA objects shared).
     // Sight disks (dx^2 + dy^2 <= sightRadius^2 of the seeing unit's type) painted into per-row bitmaps:
@@ -2311,7 +2311,7 @@ struct Game {
     }
 
     // ------------------------------------------------------------------ reward functions
-    // CloserToEnemyBaseRewardFunction.java:22-66 (and the identical CloserToEnemyUnit text): the enemy
+    // CloserToEnemyBaseRewardFunction.java:16-60 (and the identical CloserToEnemyUnit text): the enemy
     // Base is the first unit of minplayer named "Base" in the pre-cycle list; distances are from
     // maxplayer's Light/Heavy/Ranged/Worker units.  Squared distances are exact integers and sqrt is
     // monotone, so min(sqrt) = sqrt(min).
@@ -2354,9 +2354,10 @@ struct Game {
     // computeReward of every a_rfs entry for the game's external slots (slot0 + i is player pl(i)),
     // written to reward / done [slot][R]; returns done of a_rfs[0] (drives the auto-reset,
     // JNIGridnetVecClient.java:247,272).  WinLoss: WinLossRewardFunction.java:16-24; ResourceGather:
-    // ResourceGatherRewardFunction.java:22-44; ProduceWorker / ProduceBuilding / ProduceCombatUnit:
-    // Produce*RewardFunction.java:22-33; Attack: AttackRewardFunction.java:22-38 (a legal attack always
-    // targets a minplayer unit of the pre-cycle pgs).  Constants are float 1.
+    // ResourceGatherRewardFunction.java:22-42; ProduceWorker / ProduceBuilding / ProduceCombatUnit:
+    // ProduceWorkerRewardFunction.java:20-30 (the other two: the same lines of their files); Attack:
+    // AttackRewardFunction.java:20-36 (a legal attack always targets a minplayer unit of the pre-cycle
+    // pgs).  Constants are float 1.
     DEV bool writeRewards(int slot0, int nslots, int pl0, int pl1, bool gameover, int winner) {
         const int R = D.n_rewards;
         int newSq0 = INF, newSq1 = INF;
@@ -2519,7 +2520,7 @@ struct Game {
             }
         }
     }
-    // PartiallyObservableGameState.getVectorObservation (rts/PartiallyObservableGameState.java:137-209):
+    // PartiallyObservableGameState.getVectorObservation (rts/PartiallyObservableGameState.java:82-154):
     // the snapshot's units (live fields, possibly dead) in list order, last writer per cell; the
     // snapshot's assignments; walls; own / enemy sight disks of the snapshot units (:211-234).
     // delta: the buffer holds this game's view-p render of the previous observation write and the PO
@@ -3753,7 +3754,12 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         G.storeTerrain();
         G.resetFromTemplate();
         if (D.mask_delta && D.masks) G.loadPrev();
+        // JNIGridnetClientSelfPlay.reset zeroes reward/done slots j < rewards.length == 2 only
+        // (tests/JNIGridnetClientSelfPlay.java:103-104,235-238): slots >= 2 keep the caller buffer's
+        // previous values; JNIGridnetClient / JNIBotClient.reset zero every slot
+        // (JNIGridnetClient.java:248-251, JNIBotClient.java:159-162)
         for (int k = lane_id(); k < nslots * D.n_rewards; k += 64) {
+            if (selfplay && k % D.n_rewards >= 2) continue;
             if (D.reward) D.reward[(size_t)slot0 * D.n_rewards + k] = 0.0;
             if (D.done) D.done[(size_t)slot0 * D.n_rewards + k] = 0;
         }

@@ -128,11 +128,20 @@ def _kinds(ais, n):
     return (ctypes.c_int32 * max(1, n))(*(kinds or [0]))
 
 
+def _last_map_index(n_selfplay, n_bot):
+    """The largest a_mapPaths index Java reads: mapPaths[i*2] per self-play client
+    (JNIGridnetVecClient.java:119), mapPaths[a_num_selfplayenvs + i] per bot env (:123), and
+    mapPaths[0] for the storage sizing (:127)."""
+    return max([0] + ([2 * (n_selfplay // 2 - 1)] if n_selfplay >= 2 else []) +
+               ([n_selfplay + n_bot - 1] if n_bot > 0 else []))
+
+
 class _Handle:
     def __init__(self, n_selfplay, n_bot, max_steps, map_paths, ai2s, utt, partial_obs, device, seed, slot_id_base,
                  ai1s=None, mask_delta=False, rewards=None, forward_model=False, max_units=0):
-        if len(map_paths) < n_selfplay + n_bot:  # mapPaths[i] per env (JNIGridnetVecClient.java:119,122)
-            raise ValueError(f"{len(map_paths)} map paths for {n_selfplay + n_bot} environments")
+        need = _last_map_index(n_selfplay, n_bot)
+        if len(map_paths) <= need:
+            raise ValueError(f"{len(map_paths)} map paths; Java reads mapPaths[{need}]")
         L = _lib.load()
         self.L = L
         self._paths = (ctypes.c_char_p * len(map_paths))(*[p.encode() for p in map_paths])
@@ -363,6 +372,7 @@ class DeviceVecEnv:
                           slot_id_base, ai1s=ai1s, mask_delta=mask_delta and with_masks, rewards=_check_rfs(rfs),
                           max_units=max_units)
         h = self._h
+        self.mask_delta = bool(mask_delta and with_masks)
         dev = torch.device("cuda", device)
         self.device = dev
         S, H, W, C, K = h.S, h.H, h.W, h.C, h.K
@@ -475,8 +485,15 @@ class DeviceVecEnv:
 
     @property
     def multi_step_capable(self):
-        """rollout_fused runs several steps per launch on this handle (mrts_multi_step_capable)."""
+        """The handle's shape and switch allow multi-step launches (mrts_multi_step_capable):
+        rollout_uniform uses them; rollout_fused only with mask_delta (see fused_multi_step)."""
         return bool(self._h.L.mrts_multi_step_capable(self._h.h))
+
+    @property
+    def fused_multi_step(self):
+        """rollout_fused runs several steps per launch on this handle: the shape allows it and the
+        handle keeps delta masks (the steady fused state needs them)."""
+        return self.multi_step_capable and bool(self.mask_delta)
 
     def rollout_fused(self, seed, first_next_step, n_steps, stream=None):
         """n_steps step_fused calls (next_step = first_next_step, first_next_step + 1, ...) enqueued by

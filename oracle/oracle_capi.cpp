@@ -62,7 +62,7 @@ static void computeReward(int kind, int maxplayer, int minplayer, const TraceEnt
                 reward = after.winner() == maxplayer ? 1.0 : -1.0;
             }
             break;
-        case RF_RESOURCE_GATHER: {  // ResourceGatherRewardFunction.java:22-44 (float constants 1)
+        case RF_RESOURCE_GATHER: {  // ResourceGatherRewardFunction.java:22-42 (float constants 1)
             for (auto& p : te.actions) {
                 if (p->m_a->player == maxplayer && p->m_b->type == UnitAction::TYPE_HARVEST) reward += 1.0f;
                 else if (p->m_a->player == maxplayer && p->m_b->type == UnitAction::TYPE_RETURN) reward += 1.0f;
@@ -74,9 +74,9 @@ static void computeReward(int kind, int maxplayer, int minplayer, const TraceEnt
                     break;
                 }
         } break;
-        case RF_PRODUCE_WORKER:       // ProduceWorkerRewardFunction.java:22-33
-        case RF_PRODUCE_BUILDING:     // ProduceBuildingRewardFunction.java:22-33
-        case RF_PRODUCE_COMBAT_UNIT:  // ProduceCombatUnitRewardFunction.java:22-33
+        case RF_PRODUCE_WORKER:       // ProduceWorkerRewardFunction.java:20-30
+        case RF_PRODUCE_BUILDING:     // ProduceBuildingRewardFunction.java:20-30
+        case RF_PRODUCE_COMBAT_UNIT:  // ProduceCombatUnitRewardFunction.java:20-30
             for (auto& p : te.actions) {
                 if (p->m_a->player != maxplayer || p->m_b->type != UnitAction::TYPE_PRODUCE || !p->m_b->unitType) continue;
                 const std::string& n = p->m_b->unitType->name;
@@ -86,7 +86,7 @@ static void computeReward(int kind, int maxplayer, int minplayer, const TraceEnt
                 if (hit) reward += 1.0f;
             }
             break;
-        case RF_ATTACK:  // AttackRewardFunction.java:22-38
+        case RF_ATTACK:  // AttackRewardFunction.java:20-36
             for (auto& p : te.actions) {
                 if (p->m_a->player == maxplayer && p->m_b->type == UnitAction::TYPE_ATTACK_LOCATION) {
                     const Unit* other = te.pgs->getUnitAt(p->m_b->x, p->m_b->y);
@@ -97,8 +97,8 @@ static void computeReward(int kind, int maxplayer, int minplayer, const TraceEnt
                 }
             }
             break;
-        case RF_CLOSER_TO_ENEMY_BASE:    // CloserToEnemyBaseRewardFunction.java:22-66
-        case RF_CLOSER_TO_ENEMY_UNIT: {  // CloserToEnemyUnitRewardFunction.java:22-66 (same text: enemy *Base*)
+        case RF_CLOSER_TO_ENEMY_BASE:    // CloserToEnemyBaseRewardFunction.java:16-60
+        case RF_CLOSER_TO_ENEMY_UNIT: {  // CloserToEnemyUnitRewardFunction.java:16-60 (same text: enemy *Base*)
             int baseX = 0, baseY = 0;
             bool baseExists = false;
             for (auto& t : te.pgs->units)
@@ -177,9 +177,15 @@ struct Env {
     void rewards(Resp& r, int maxplayer, const TraceEntry& te) {
         for (size_t j = 0; j < w->rfs.size(); j++) computeReward(w->rfs[j], maxplayer, 1 - maxplayer, te, *gs, r.reward[j], r.done[j]);
     }
+    // JNIGridnetClient.reset zeroes every slot (tests/JNIGridnetClient.java:248-251); the self-play
+    // client's loop is bounded by rewards.length == numPlayers == 2, not by rfs.length
+    // (tests/JNIGridnetClientSelfPlay.java:103-104,235-238): slots >= 2 keep the previous step's
+    // values.  (With one reward function Java throws there; here the single slot is zeroed —
+    // DESIGN.md §8.)
     void clearRewards(Resp& r) {
-        std::fill(r.reward.begin(), r.reward.end(), 0.0);
-        std::fill(r.done.begin(), r.done.end(), 0);
+        const size_t n = selfplay ? std::min<size_t>(2, r.reward.size()) : r.reward.size();
+        std::fill(r.reward.begin(), r.reward.begin() + n, 0.0);
+        std::fill(r.done.begin(), r.done.begin() + n, 0);
     }
     GSP makeView(int player) {
         if (w->partialObs) return std::make_shared<PartiallyObservableGameState>(*gs, player);
@@ -215,7 +221,7 @@ struct Env {
         }
         return rows;
     }
-    // JNIAI.getAction (ai/jni/JNIAI.java:316-320)
+    // JNIAI.getAction (ai/jni/JNIAI.java:51-55)
     PlayerAction jniGetAction(int player, const GameState& g, const std::vector<int>& rows) const {
         int n = (int)(rows.size() / 8);
         PlayerAction pa = PlayerAction::fromVectorAction(rows, n, g, w->utt, player, w->maxAttackRadius);

@@ -566,7 +566,7 @@ void getValidActionArray(const Unit& u, const GameState& gs, const UnitTypeTable
 }
 
 // ---------------------------------------------------------------- PlayerAction
-void PlayerAction::fillWithNones(const GameState& s, int pID, int duration) {  // PlayerAction.java:328-346
+void PlayerAction::fillWithNones(const GameState& s, int pID, int duration) {  // PlayerAction.java:217-235
     for (auto& u : s.pgs->units) {
         if (u->player == pID) {
             if (s.unitActions.get(u.get()) == nullptr) {
@@ -590,7 +590,7 @@ bool PlayerAction::integrityCheck() const {  // :355-370
     return true;
 }
 
-// PlayerAction.java:495-528 ; rows = nrows × 8 ints (Java layout [pos, a_t, ...])
+// PlayerAction.java:384-417 ; rows = nrows × 8 ints (Java layout [pos, a_t, ...])
 PlayerAction PlayerAction::fromVectorAction(const std::vector<int>& rows, int nrows, const GameState& gs,
                                             const UnitTypeTable& utt, int currentPlayer, int maxAttackRadius) {
     PlayerAction pa;
@@ -773,7 +773,7 @@ void GameState::getVectorObservation(int player, int32_t* out) const {  // :922-
 }
 
 // ---------------------------------------------------------------- PartiallyObservableGameState
-PartiallyObservableGameState::PartiallyObservableGameState(const GameState& gs, int a_player)  // :90-109
+PartiallyObservableGameState::PartiallyObservableGameState(const GameState& gs, int a_player)  // :35-54
     : GameState(gs.pgs->cloneKeepingUnits(), gs.utt), observer(a_player) {
     unitCancelationCounter = gs.unitCancelationCounter;
     time = gs.time;
@@ -806,7 +806,7 @@ static void calculateVisibility(const std::vector<std::array<int, 3>>& us, int W
             }
     }
 }
-void PartiallyObservableGameState::getVectorObservation(int player, int32_t* out) const {  // :137-209
+void PartiallyObservableGameState::getVectorObservation(int player, int32_t* out) const {  // :82-154
     const int H = pgs->height, W = pgs->width, HW = H * W;
     std::memset(out, 0, sizeof(int32_t) * 8 * (size_t)HW);
     std::vector<std::array<int, 3>> friendly, enemy;

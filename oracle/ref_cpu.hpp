@@ -159,7 +159,7 @@ struct UAMap {
     }
 };
 
-// rts/PhysicalGameState.java:34-787
+// rts/PhysicalGameState.java:31-787
 struct PhysicalGameState {
     int width = 8, height = 8;
     std::shared_ptr<std::vector<int>> terrain;
@@ -185,13 +185,13 @@ struct Pair {  // util/Pair — mutable fields, identity semantics
 };
 using PairP = std::shared_ptr<Pair>;
 
-// rts/PlayerAction.java:134-530
+// rts/PlayerAction.java:23-419
 struct PlayerAction {
     std::vector<PairP> actions;
     ResourceUsage r;
     void addUnitAction(const UnitP& u, const UnitActionP& a) { actions.push_back(std::make_shared<Pair>(Pair{u, a})); }
     bool isEmpty() const { return actions.empty(); }
-    void fillWithNones(const GameState& s, int pID, int duration);  // :217-235 (file :328-346)
+    void fillWithNones(const GameState& s, int pID, int duration);  // :217-235
     bool integrityCheck() const;                                    // :355-370
     static PlayerAction fromVectorAction(const std::vector<int>& rows, int nrows, const GameState& gs,
                                          const UnitTypeTable& utt, int currentPlayer, int maxAttackRadius);
@@ -232,12 +232,12 @@ struct GameState {
 };
 using GSP = std::shared_ptr<GameState>;
 
-// rts/PartiallyObservableGameState.java:70-235
+// rts/PartiallyObservableGameState.java:15-180
 struct PartiallyObservableGameState : GameState {
     int observer;
-    PartiallyObservableGameState(const GameState& gs, int a_player);  // :90-109
+    PartiallyObservableGameState(const GameState& gs, int a_player);  // :35-54
     bool observable(int x, int y) const override;                      // :116-126
-    void getVectorObservation(int player, int32_t* out) const override;  // :137-209
+    void getVectorObservation(int player, int32_t* out) const override;  // :82-154
     int numObservationPlanes() const override { return 8; }
 };
 

@@ -105,7 +105,22 @@ def test_vecclient_mirror_rejects_missing_bots():
     with pytest.raises(ValueError, match="a_ai1s"):
         JNIGridnetVecClient.bots(100, None, "", [m] * 2, ["PassiveAI"], ["PassiveAI"] * 2)
     with pytest.raises(ValueError, match="map paths"):
-        JNIGridnetVecClient(4, 0, 100, None, "", [m] * 3)
+        JNIGridnetVecClient(4, 0, 100, None, "", [m] * 2)  # Java reads mapPaths[2]
+    with pytest.raises(ValueError, match="map paths"):
+        JNIGridnetVecClient(2, 2, 100, None, "", [m] * 3, ["PassiveAI"] * 2)  # mapPaths[3]
+
+
+def test_vecclient_mirror_map_index_is_javas():
+    """the mirror requires exactly the mapPaths indices Java reads — [i*2] per self-play
+    client (JNIGridnetVecClient.java:119), [a_num_selfplayenvs + i] per bot env (:123), [0] for the
+    storage sizing (:127) — so a self-play-only client with n-1 paths is accepted like Java's."""
+    from microrts_amd.vec_client import _last_map_index
+
+    assert _last_map_index(4, 0) == 2  # 3 paths suffice for 4 self-play slots
+    assert _last_map_index(2, 0) == 0
+    assert _last_map_index(0, 3) == 2
+    assert _last_map_index(2, 2) == 3
+    assert _last_map_index(0, 0) == 0
 
 
 def _utt_with(sight_of_worker):

@@ -1,0 +1,236 @@
+"""The shipped benchmark forms against the CPU oracle, at the BASELINE configs' full sizes.
+
+bench.py times each config as ONE native rollout call that runs K steps per `k_env` launch
+(multi-step launches).  Here the same calls run at the bench's sizes (c3: 4096
+self-play games on 16x16; c2: 1024 games on 8x8; c5: 2048 partially observable games on 32x32 with
+max_units 256) after a 1000-step burn-in, followed by K = 20 and K = 200 step launches.  Picked
+games are replayed by the oracle with its OWN policy stream: the oracle computes its masks
+(JNIGridnetVecClient.getMasks, :307-316) and samples the same Philox masked-uniform (or unmasked
+uniform) rows from them, so no GPU-produced action ever enters the oracle.  UTT v1 + CANCEL_BOTH
+draws no Java random numbers, so such an oracle game is an exact replica of the picked GPU game.  At
+each launch end: observations, rewards, dones, masks, the next action rows and the canonical state
+dumps (units in list order, assignments in LinkedHashMap order) must be bit-identical.
+
+Also here: TestLoadingMaps (test/microrts/TestLoadingMaps.java:24-51) on the product path — all 140
+maps through the host parser + on-device reset, against the oracle's parser — and the C-ABI
+contract that a write to d_actions between fused calls needs mrts_policy_invalidate().
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from tests import oracle_py
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EEDC0DE
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BURNIN = 1000
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _picks(n_games, mid):
+    """Slots of the first, a middle and the last game (both players of each)."""
+    g = [0, mid, n_games - 1]
+    return [s for k in g for s in (2 * k, 2 * k + 1)]
+
+
+class _MaskedReplica:
+    """Oracle self-play games replaying picked GPU slots under the masked-uniform policy: the
+    actions of step t are oracle_py.policy(the oracle's own masks, SEED, global slot id, t)."""
+
+    def __init__(self, mp, picks, seed, partial_obs=False):
+        self.picks = picks
+        self.ref = oracle_py.OracleVecClient(len(picks), 0, 2000, [mp] * len(picks), seed=seed, partial_obs=partial_obs)
+        self.ref.reset()
+        self.t = 0
+
+    def actions(self, step):
+        m = self.ref.get_masks(0)
+        return m, np.stack([oracle_py.policy(m[i], SEED, s, step, 0) for i, s in enumerate(self.picks)])
+
+    def run(self, n):
+        for _ in range(n):
+            _, a = self.actions(self.t)
+            self.ref.step(a)
+            self.t += 1
+
+
+def _compare_launch_end(env, rep, tag):
+    env.synchronize()
+    ref, picks = rep.ref, rep.picks
+    assert np.array_equal(env.obs.cpu().numpy()[picks], ref.obs), f"{tag}: observations"
+    assert np.array_equal(env.reward.cpu().numpy()[picks], ref.reward), f"{tag}: rewards"
+    assert np.array_equal(env.done.cpu().numpy()[picks], ref.done), f"{tag}: dones"
+    m, nxt = rep.actions(rep.t)  # the rows the launch sampled for the next step
+    assert np.array_equal(env.masks.cpu().numpy()[picks], m), f"{tag}: masks"
+    assert np.array_equal(env.actions.cpu().numpy()[picks], nxt), f"{tag}: next action rows"
+    for i, s in enumerate(picks):
+        assert np.array_equal(env.dump_state(s), ref.dump(i)), f"{tag}: state of slot {s}"
+
+
+def _masked_multi_step(mp, n_games, mid, seed, partial_obs=False, max_units=0):
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    S = 2 * n_games
+    env = DeviceVecEnv(S, 0, 2000, [mp] * S, seed=seed, partial_obs=partial_obs, max_units=max_units)
+    assert env.fused_multi_step, "the bench's shape must run multi-step launches"
+    rep = _MaskedReplica(mp, _picks(n_games, mid), seed, partial_obs)
+    env.reset()
+    env.random_policy(SEED, 0)
+    env.rollout_fused(SEED, 1, BURNIN)  # the first launch is a single step, then multi-step launches
+    rep.run(BURNIN)
+    _compare_launch_end(env, rep, f"after the {BURNIN}-step burn-in")
+    k = BURNIN
+    for K in (20, 200):  # the driver's K and the bench default
+        env.rollout_fused(SEED, k + 1, K)
+        rep.run(K)
+        k += K
+        _compare_launch_end(env, rep, f"after a {K}-step launch (step {k})")
+    assert not env.error_flags().any()
+    env.close()
+    rep.ref.close()
+
+
+def test_full_size_c3_multi_step():
+    """BASELINE configs[2] (c3) as bench.py times it: 4096 self-play games on basesWorkers16x16, the
+    fused masked policy, delta masks, K steps per k_env launch."""
+    _masked_multi_step("maps/16x16/basesWorkers16x16.xml", 4096, 1234, seed=5)
+
+
+def test_full_size_c5_multi_step():
+    """BASELINE configs[4] (c5) per GPU: 2048 partially observable self-play games on
+    BWDistantResources32x32, max_units 256, multi-step launches with incremental PO views."""
+    _masked_multi_step("maps/BWDistantResources32x32.xml", 2048, 777, seed=7, partial_obs=True, max_units=256)
+
+
+def test_full_size_c2_multi_step():
+    """BASELINE configs[1] (c2) as bench.py times it: 1024 games on basesWorkers8x8, unmasked uniform
+    rows drawn by the step kernel, K steps per launch.  The oracle draws the same rows itself
+    (oracle_py.policy_uniform = mrts_policy_uniform_dev's Philox stream)."""
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    E = 1024
+    mp = "maps/8x8/basesWorkers8x8.xml"
+    env = DeviceVecEnv(2 * E, 0, 2000, [mp] * (2 * E), seed=8)
+    assert env.multi_step_capable
+    S, H, W, C, K = env.dims
+    picks = _picks(E, 500)
+    ref = oracle_py.OracleVecClient(len(picks), 0, 2000, [mp] * len(picks), seed=8)
+    env.reset()
+    ref.reset()
+    t = 0
+
+    def ref_run(n):
+        nonlocal t
+        for _ in range(n):
+            ref.step(np.stack([oracle_py.policy_uniform(H, W, K, SEED, s, t) for s in picks]))
+            t += 1
+
+    for n in (BURNIN, 20, 200):
+        env.rollout_uniform(SEED, t, n, fused=True)
+        ref_run(n)
+        env.synchronize()
+        tag = f"c2 after a {n}-step rollout (step {t})"
+        assert np.array_equal(env.obs.cpu().numpy()[picks], ref.obs), f"{tag}: observations"
+        assert np.array_equal(env.reward.cpu().numpy()[picks], ref.reward), f"{tag}: rewards"
+        assert np.array_equal(env.done.cpu().numpy()[picks], ref.done), f"{tag}: dones"
+        last = np.stack([oracle_py.policy_uniform(H, W, K, SEED, s, t - 1) for s in picks])
+        assert np.array_equal(env.actions.cpu().numpy()[picks], last), f"{tag}: the last step's rows"
+        for i, s in enumerate(picks):
+            assert np.array_equal(env.dump_state(s), ref.dump(i)), f"{tag}: state of slot {s}"
+    assert not env.error_flags().any()
+    env.close()
+    ref.close()
+
+
+MAPS = sorted(glob.glob(os.path.join(ROOT, "maps", "**", "*.xml"), recursive=True))
+
+
+def test_all_maps_load_product_path():
+    """TestLoadingMaps (test/microrts/TestLoadingMaps.java:24-51) on the product path: every one of
+    the 140 maps goes through libmrts's host XML parser (terrain RLE, PhysicalGameState.java:577-607,
+    765-777; units in file order, Unit.java:597-620) into a device template and an on-device reset.
+    The reset observation and the canonical state dump equal the oracle's parse.  Maps above 64x64
+    cells run with max_units 1024 (their full unit capacity does not fit one CU's LDS; the largest
+    map holds 64 units)."""
+    _torch()
+    from microrts_amd import DeviceVecEnv
+
+    assert len(MAPS) == 140
+    for m in MAPS:
+        rel = os.path.relpath(m, ROOT)
+        ref = oracle_py.OracleVecClient(2, 0, 100, [rel, rel])
+        obs, _, _ = ref.reset()
+        mu = 1024 if ref.H * ref.W > 64 * 64 else 0
+        env = DeviceVecEnv(2, 0, 100, [rel, rel], max_units=mu)
+        env.reset()
+        env.synchronize()
+        assert env.dims[1:3] == (ref.H, ref.W), rel
+        assert np.array_equal(env.obs.cpu().numpy(), obs), f"{rel}: reset observation"
+        assert np.array_equal(env.masks.cpu().numpy(), ref.get_masks(0)), f"{rel}: reset masks"
+        for s in (0, 1):
+            assert np.array_equal(env.dump_state(s), ref.dump(s)), f"{rel}: state"
+        env.close()
+        ref.close()
+
+
+def test_c_abi_fused_write_needs_invalidate():
+    """include/mrts.h: a fused call keeps the rows it sampled and the next fused call on
+    the same d_actions decodes from that copy.  Through the raw C entry points (no Python version
+    counter involved): rows written into d_actions between fused calls are used iff
+    mrts_policy_invalidate() is called — then the step equals a plain mrts_step_dev of those rows on
+    a twin handle; without it they are ignored (the documented contract, shown here to hold)."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n = 16
+    mp = "maps/16x16/basesWorkers16x16.xml"
+    A, B, C = (DeviceVecEnv(n, 0, 300, [mp] * n, seed=5) for _ in range(3))
+    L = B._h.L
+    p = DeviceVecEnv._p
+
+    def raw_fused(e, k):
+        s = ctypes.c_void_p(torch.cuda.current_stream(e.device).cuda_stream)
+        r = L.mrts_step_fused_dev(e._h.h, p(e.actions), p(e.players), p(e.obs), p(e.reward), p(e.done), p(e.masks), 0,
+                                  SEED, k, s)
+        assert r == 0
+
+    for e in (A, B, C):
+        e.reset()
+        e.random_policy(SEED, 0)
+    for k in range(12):
+        A.step()
+        A.random_policy(SEED, k + 1)
+        raw_fused(B, k + 1)
+        raw_fused(C, k + 1)
+    torch.cuda.synchronize()
+    for name in ("obs", "masks", "actions"):
+        assert torch.equal(getattr(A, name), getattr(B, name)) and torch.equal(getattr(A, name), getattr(C, name))
+    g = torch.Generator(device="cpu").manual_seed(3)
+    hi = torch.tensor([6, 4, 4, 4, 4, 7, 49], dtype=torch.int32)
+    alt = (torch.rand(tuple(A.actions.shape), generator=g) * hi).to(torch.int32).to(A.device)
+    for e in (A, B, C):
+        e.actions.copy_(alt)
+    assert L.mrts_policy_invalidate(B._h.h) == 0
+    A.step()  # the plain step decodes every row of d_actions
+    raw_fused(B, 100)
+    raw_fused(C, 100)  # no invalidate: decodes the kept copy of the previous sample
+    torch.cuda.synchronize()
+    for s in range(0, n, 2):
+        assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"invalidated fused step, slot {s}"
+    assert any(not np.array_equal(A.dump_state(s), C.dump_state(s)) for s in range(0, n, 2)), \
+        "without invalidate the written rows should have been ignored"
+    for e in (A, B, C):
+        e.close()

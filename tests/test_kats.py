@@ -344,27 +344,42 @@ class VecRunner:
     """Two self-play slots + one agent-vs-PassiveAI env through the JNIGridnetVecClient mirror (GPU:
     mrts_reset / mrts_step) or the oracle VecClient; all-zero grid actions (NONE rows)."""
 
-    def __init__(self, backend, map_path, max_steps):
+    def __init__(self, backend, map_path, max_steps, rfs=("WinLossRewardFunction",)):
         self.backend = backend
         if backend == "oracle":
-            self.e = oracle_py.OracleVecClient(2, 1, max_steps, [map_path] * 3, bot_kinds=[oracle_py.BOT_PASSIVE])
+            self.e = oracle_py.OracleVecClient(2, 1, max_steps, [map_path] * 3, bot_kinds=[oracle_py.BOT_PASSIVE],
+                                               rewards=[oracle_py.REWARD_IDS[r] for r in rfs])
         else:
             from microrts_amd import JNIGridnetVecClient
 
-            self.e = JNIGridnetVecClient(2, 1, max_steps, ["WinLossRewardFunction"], "", [map_path] * 3,
-                                         a_ai2s=["PassiveAI"])
+            self.e = JNIGridnetVecClient(2, 1, max_steps, list(rfs), "", [map_path] * 3, a_ai2s=["PassiveAI"])
         self.S = 3
+        self.R = len(rfs)
 
     def reset(self):
-        self.e.reset([0] * self.S)
+        """-> (reward [S][R], done [S][R]) of the reset Responses."""
+        if self.backend == "oracle":
+            _, rew, done = self.e.reset([0] * self.S)
+        else:
+            r = self.e.reset([0] * self.S)
+            rew, done = r.reward, r.done
+        return (np.asarray(rew, np.float64).reshape(self.S, self.R).copy(),
+                np.asarray(done).astype(bool).reshape(self.S, self.R).copy())
+
+    def step_full(self, actions=None):
+        """-> (reward [S][R], done [S][R])."""
+        a = np.zeros((self.S, 25, 7), np.int32) if actions is None else np.asarray(actions, np.int32)
+        if self.backend == "oracle":
+            _, rew, done = self.e.step(a, [0] * self.S)
+        else:
+            r = self.e.gameStep(a, [0] * self.S)
+            rew, done = r.reward, r.done
+        return (np.asarray(rew, np.float64).reshape(self.S, self.R).copy(),
+                np.asarray(done).astype(bool).reshape(self.S, self.R).copy())
 
     def step(self):
         """-> done[0] per slot (bool[S])."""
-        if self.backend == "oracle":
-            _, _, d = self.e.step(np.zeros((self.S, 25, 7), np.int32), [0] * self.S)
-            return d.astype(bool)
-        r = self.e.gameStep(np.zeros((self.S, 25, 7), np.int32), [0] * self.S)
-        return r.done[:, 0].copy()
+        return self.step_full()[1][:, 0]
 
     def env_steps(self):
         if self.backend == "oracle":
@@ -401,10 +416,40 @@ def kat_env_steps_survive_reset(tmp, backend):
     r.close()
 
 
+def kat_selfplay_reset_keeps_slots_from_two(tmp, backend):
+    """A.10 / SURVEY a1 — an explicit reset() of a self-play game zeroes reward/done only for
+    j < rewards.length, and rewards = new double[2][] (numPlayers, JNIGridnetClientSelfPlay.java:103-104,
+    135-136) so the bound is 2, not rfs.length (:235-238): reward/done slots >= 2 keep the previous
+    step's values.  JNIGridnetClient.reset (the agent-vs-bot env) zeroes every slot (:248-251).
+    rfs = [WinLoss, Attack, ProduceWorker, ResourceGather] on a map with no Resource units: on step 1
+    player 0's Base produces a Worker (PRODUCE right, Worker), so ProduceWorker (slot 2) = 1.0 for
+    player 0 (ProduceWorkerRewardFunction.java:20-30: every pair of the TraceEntry), 0.0 for player 1;
+    ResourceGather (slot 3) is done = true every step (no Resource left, ResourceGatherRewardFunction.java:
+    31-40).  After reset(): self-play slots keep [2] = 1.0 / 0.0 and done[3] = true, slots 0 and 1
+    zero; the bot env (slot 2) is all zero."""
+    m = write_map(tmp / "k13.xml", 5, 5, [(BASE, 0, 0, 0), (BASE, 1, 4, 4)])
+    r = VecRunner(backend, m, 100, rfs=("WinLossRewardFunction", "AttackRewardFunction", "ProduceWorkerRewardFunction",
+                                        "ResourceGatherRewardFunction"))
+    rew, done = r.reset()
+    assert not rew.any() and not done.any()  # new double[rfs.length]: zeros before any step
+    a = np.zeros((3, 25, 7), np.int32)
+    a[0, 0] = a[2, 0] = [PRODUCE, 0, 0, 0, RIGHT, WORKER, 0]  # player 0's Base at cell 0 (slot 0 and the bot env)
+    rew, done = r.step_full(a)
+    assert rew.tolist() == [[0, 0, 1, 0], [0, 0, 0, 0], [0, 0, 1, 0]]
+    assert done.tolist() == [[False, False, False, True]] * 3
+    rew, done = r.reset()
+    assert rew.tolist() == [[0, 0, 1, 0], [0, 0, 0, 0], [0, 0, 0, 0]]
+    assert done.tolist() == [[False, False, False, True], [False, False, False, True], [False] * 4]
+    rew, done = r.step_full()  # every slot recomputed by the step
+    assert rew.tolist() == [[0, 0, 0, 0]] * 3
+    assert done.tolist() == [[False, False, False, True]] * 3
+    r.close()
+
+
 KATS = [kat_illegal_becomes_none_eta, kat_resource_quirk_row_order, kat_rows_that_do_not_count,
         kat_player1_sees_player0_reservations, kat_dead_unit_still_executes, kat_simultaneous_kill_is_a_draw,
         kat_harvest_deplete_return, kat_duplicate_row_keeps_map_position, kat_po_killed_unit_in_view, kat_mask_record,
-        kat_reward_functions, kat_env_steps_survive_reset]
+        kat_reward_functions, kat_env_steps_survive_reset, kat_selfplay_reset_keeps_slots_from_two]
 
 
 @pytest.mark.parametrize("kat", KATS, ids=[k.__name__ for k in KATS])

@@ -1,5 +1,5 @@
 """Game-state serialisation (SURVEY.md §4 checkpoint/resume, §8f-4 serialisers): GameState.toJSON /
-fromJSON (rts/GameState.java:819-837, 889-915) and whole-handle checkpoints.
+fromJSON (rts/GameState.java:819-837, 897-915) and whole-handle checkpoints.
 
 CPU: the oracle's writer against the Java text format on a known state (a hand-derived KAT), its
 reader round trip.  GPU: the HIP handle's JSON equals the oracle's (unit IDs normalised: the build
