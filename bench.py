@@ -56,8 +56,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--burnin", type=int, default=1000,
                     help="untimed steps from reset before warmup: the timed window sees mid-episode unit counts")
-    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
-                    help="BASELINE.json workload preset (c3 = the headline; c2 / c5 = the other single-GPU configs)")
+    ap.add_argument("--config", choices=sorted(CONFIGS) + ["c1"], default="c3",
+                    help="BASELINE.json workload preset (c3 = the headline; c2 / c5 = the other single-GPU configs; "
+                         "c1 = one bot-vs-bot env, RandomBiasedAI x 2, with the CPU oracle beside it)")
     ap.add_argument("--envs", type=int, default=None, help="self-play games per GPU (default: the preset's)")
     ap.add_argument("--map", default=None)
     ap.add_argument("--mask-mode", choices=["delta", "full"], default="delta",
@@ -79,11 +80,16 @@ def parse():
                          "(the default for --policy kernel), eager = one Python call per step")
     ap.add_argument("--no-graph", action="store_true", help="alias of --launch eager")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-gather-window", action="store_true",
+                    help="skip the second timed window with the per-step RCCL observation all-gather (with_gather)")
     ap.add_argument("--no-compare", action="store_true", help="skip the other policy form's comparison window")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per step-kernel launch from a rocprofv3 --pmc pass (profiles/), for roofline.traffic")
     a = ap.parse_args()
+    if a.config == "c1":
+        a.map = a.map or "maps/4x4/base4x4.xml"
+        return a
     m, e, po, mu = CONFIGS[a.config]
     a.map = a.map or m
     a.envs = a.envs or e
@@ -148,43 +154,198 @@ class _FenceFreeEvent:
         return ms.value
 
 
-def cpu_baseline(map_path, threads, burnin, uniform=False):
+def host_info():
+    """The host the CPU baseline ran on: logical CPUs (nproc), the CPUs this process may use, the model."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": model}
+
+
+def cpu_baseline(map_path, threads, burnin, uniform=False, po=False, runs=5):
     """The CPU oracle (C++ restatement of the Java engine; the JVM is not available) running the
-    same workload: VecClient self-play + getMasks + the same Philox policy, std::thread shards."""
+    same workload: VecClient self-play + getMasks + the same Philox policy (or c2's uniform rows),
+    partially observable views for c5, std::thread shards over games.  Median of `runs` runs
+    (SURVEY.md §8(d)); a bounded sample (a few seconds of CPU time per run)."""
+    import statistics
+
     from tests import oracle_py
 
     L = oracle_py.load()
-    games_per_thread, steps = 48, 300
+    games_per_thread, steps = (8 if po else 48), 300
     games = games_per_thread * threads
-    secs = L.oref_bench2(map_path.encode(), games, steps, threads, SEED, burnin, int(uniform))
-    one = L.oref_bench2(map_path.encode(), games_per_thread, steps, 1, SEED, burnin, int(uniform))
+    flags = (1 if uniform else 0) | (2 if po else 0)
+    rates = [games * steps / L.oref_bench3(map_path.encode(), games, steps, threads, SEED, burnin, flags) for _ in range(runs)]
+    ones = [games_per_thread * steps / L.oref_bench3(map_path.encode(), games_per_thread, steps, 1, SEED, burnin, flags)
+            for _ in range(3)]
+    what = "uniform rows, no masks" if uniform else "masks + masked policy" + (", partially observable views" if po else "")
     return {
-        "value": games * steps / secs,
+        "value": statistics.median(rates),
         "unit": "env-steps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{games} self-play games x {steps} timed steps after {burnin} untimed, {threads} threads (same map/policy/masks{'' if not uniform else ' (uniform rows, no masks)'}; "
-                  f"1 thread: {games_per_thread * steps / one:.0f} env-steps/s)",
+        "sample": f"{games} self-play games x {steps} timed steps after {burnin} untimed, {threads} threads (same map, "
+                  f"{what}); median of {runs} runs {[round(r) for r in rates]}; 1 thread: "
+                  f"{statistics.median(ones):.0f} env-steps/s (median of 3)",
+        "runs": rates,
+        "one_thread": statistics.median(ones),
+        "host": host_info(),
     }
+
+
+def cpu_baseline_c1(map_path, runs=5, steps=200_000, burnin=1000):
+    """BASELINE config c1: one JNIBotClient env, RandomBiasedAI vs RandomBiasedAI (seeded
+    java.util.Random 42), bot-only VecClient auto-reset; env-steps/s, 1 thread, median of `runs`."""
+    import statistics
+
+    from tests import oracle_py
+
+    L = oracle_py.load()
+    rates = [steps / L.oref_bench_bots(map_path.encode(), steps, 42, burnin) for _ in range(runs)]
+    return {"value": statistics.median(rates), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"1 env x {steps} timed gameSteps after {burnin} untimed (JNIBotClient semantics, RandomBiasedAI x 2, "
+                      f"java.util.Random seed 42); median of {runs} runs {[round(r) for r in rates]}",
+            "runs": rates, "host": host_info()}
+
+
+def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, dist):
+    """K steps with the observation all-gather after every step (xg["buf"] makes one_step run it),
+    one step launch per step, the K steps and their collectives captured in one hipGraph; the
+    barrier + synchronize bracket and max over ranks of the headline window.  -> the JSON block."""
+    gb = mdist.ObservationGather(env.obs.shape, env.device, mode="allgather")
+    xg["buf"] = gb
+    try:
+        for k in range(3):  # untimed: the first collectives set up the communicator's channels
+            one_step(base + k)
+        gb.wait()
+        torch.cuda.synchronize(env.device)
+        gb.fired = [False, False]
+        graph = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(env.device)
+        cap.wait_stream(torch.cuda.current_stream(env.device))
+        with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
+            for k in range(a.steps):
+                one_step(base + 3 + k)
+            gb.wait()  # the comm stream joins the capture: the last exchange is in the graph
+        torch.cuda.synchronize(env.device)
+        graph.replay()  # warm replay (first replays carry one-off costs)
+        torch.cuda.synchronize(env.device)
+        dist.barrier()
+        torch.cuda.synchronize(env.device)
+        t0 = time.perf_counter()
+        graph.replay()
+        torch.cuda.synchronize(env.device)
+        dist.barrier()
+        t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
+    finally:
+        xg["buf"] = None
+        env.set_obs16(None)
+    return {
+        "value": total_games * a.steps / t,
+        "ms_per_step": 1e3 * t / a.steps,
+        "collective": "all-gather of the int16 observation tensor every step (RCCL, ring over xGMI), comm stream "
+                      "overlapping the next step; " + ("int16 written by the step kernel" if not a.po else
+                                                       "narrowing copy (partially observable planes)"),
+        "payload_bytes_per_rank": env.obs.numel() * 2,  # int16 observation of one rank's slots, per step
+        "launch": "one step launch per step (a per-step consumer cannot use multi-step launches), the K steps and "
+                  "their collectives in one hipGraph",
+    }
+
+
+def main_c1(a, json_fd):
+    """BASELINE config c1: one JNIBotClient env (bot-only JNIGridnetVecClient, :157-177 / JNIBotClient
+    :108-135), RandomBiasedAI vs RandomBiasedAI — plumbing; the CPU oracle's rate is the reference
+    figure.  GPU: the same env as a bot-only DeviceVecEnv, K steps captured in one hipGraph."""
+    import torch
+
+    from microrts_amd import DeviceVecEnv
+
+    assert a.gpus == 1, "c1 is a one-env configuration"
+    torch.cuda.set_device(0)
+    env = DeviceVecEnv(0, 1, 2000, [os.path.join(ROOT, a.map)], ai1s=["RandomBiasedAI"], ai2s=["RandomBiasedAI"],
+                       seed=42, with_masks=False)
+    env.reset()
+    for _ in range(a.burnin):
+        env.step()
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(env.device)
+    cap.wait_stream(torch.cuda.current_stream(env.device))
+    with torch.cuda.graph(graph, stream=cap):
+        for _ in range(a.steps):
+            env.step()
+    torch.cuda.synchronize()
+    graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    graph.replay()
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    assert not env.error_flags().any()
+    out = {
+        "metric": METRIC, "value": a.steps / t, "unit": "env-steps/s", "n_gpus": 1, "rccl_world_size": 1,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": 1e3 * t / a.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (RandomBiasedAI x 2, per-game java.util.Random seeded from 42)",
+        "config": {"workload": f"c1: {a.map}, 1 env, RandomBiasedAI vs RandomBiasedAI (bot-only client, reward/done "
+                               "only) — one wave on the GPU: launch latency, not throughput",
+                   "burnin_steps": a.burnin, "launch": "hipGraph replay of the K timed steps",
+                   "parallelism": "single env"},
+    }
+    if not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_c1(os.path.join(ROOT, a.map))
+    sys.stdout.flush()
+    os.write(json_fd, (json.dumps(out) + "\n").encode())
+    env.close()
 
 
 def main():
     a = parse()
+    # --gpus N without a launcher: spawn the N ranks here, before anything touches a GPU (the parent
+    # only waits; each child is one rank with RANK / LOCAL_RANK / WORLD_SIZE set, as
+    # torch.distributed.run would); under a launcher WORLD_SIZE must equal --gpus
+    from microrts_amd.launch import check_world, free_port, spawn_ranks
+
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    world = check_world(a.gpus)
     # stdout carries exactly one JSON line (rank 0): everything else that writes to fd 1 — RCCL's
     # version banner, library prints — goes to stderr
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    if a.config == "c1":
+        return main_c1(a, json_fd)
     import numpy as np
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_pg = world > 1 or (a.gather_obs is not None and "RANK" in os.environ)  # 1-rank RCCL run: exercise the exchange
-    if use_pg:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    # a process group always: RCCL over xGMI between the ranks, and at N = 1 a one-rank group for the
+    # with-exchange window (SURVEY.md §8e's second curve)
+    pg_error = None
+    if world == 1 and "MASTER_PORT" not in os.environ:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
+    try:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+    except Exception as ex:  # only tolerated at N = 1 (then no exchange window)
+        if world > 1:
+            raise
+        pg_error = repr(ex)
+        print(f"bench: no process group at N=1 ({pg_error}); the exchange window is skipped", file=sys.stderr)
+    use_pg = dist.is_initialized()
+    rccl_world = dist.get_world_size() if use_pg else 1
+    assert rccl_world == world, f"process group has {rccl_world} ranks, --gpus {a.gpus}"
     from microrts_amd import DeviceVecEnv
     from microrts_amd import dist as mdist
 
@@ -199,6 +360,7 @@ def main():
     gather_buf = None
     if a.gather_obs and use_pg:
         gather_buf = mdist.ObservationGather(env.obs.shape, env.device, mode=a.gather_obs)
+    xg = {"buf": gather_buf}  # the exchange one_step performs (None: no collective in the step)
 
     fused = a.policy == "fused"
     uniform = a.policy in ("uniform", "uniform-split")
@@ -209,6 +371,8 @@ def main():
     kernel16 = gather_buf is not None and not gather_buf.gloo and not a.po
 
     def one_step(k, ev=None):
+        gather_buf = xg["buf"]
+        kernel16 = gather_buf is not None and not gather_buf.gloo and not a.po
         if kernel16:
             env.set_obs16(gather_buf.begin())
         fused = mode["fused"]
@@ -439,6 +603,7 @@ def main():
         "value": value,
         "unit": "env-steps/s",
         "n_gpus": world,
+        "rccl_world_size": rccl_world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": 1e3 * t / a.steps,
@@ -558,8 +723,24 @@ def main():
         out["other_policy_form"] = {"policy": "uniform-split" if mode["uni_fused"] else "uniform",
                                     "value": total_games * a.steps / t2, "ms_per_step": 1e3 * t2 / a.steps}
         assert not env.error_flags().any()
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and not a.po:
-        out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin, uniform)
+    if gather_buf is None and not a.no_gather_window:
+        # SURVEY.md §8e's second curve: the same step with the north-star observation exchange every
+        # step (RCCL all-gather of the int16 observation tensor over xGMI, written by the step kernel
+        # under full observability, on a comm stream overlapping the next step).  A per-step consumer
+        # cannot use multi-step launches, so this window runs one step launch per step, captured with
+        # its collectives in one hipGraph.
+        if not use_pg:
+            out["with_gather"] = {"error": f"no process group: {pg_error}"}
+        else:
+            try:
+                out["with_gather"] = gather_window(env, a, xg, one_step, base + 3 * a.steps + 20, E * world, world,
+                                                   mdist, torch, dist)
+            except Exception as ex:  # the headline line must survive a failed exchange window
+                print(f"bench: exchange window failed: {ex!r}", file=sys.stderr)
+                out["with_gather"] = {"error": repr(ex)}
+            assert not env.error_flags().any()
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin, uniform, po=a.po)
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

@@ -892,8 +892,14 @@ double oref_bench2(const char* map_path, int n_games, int steps, int threads, ui
 double oref_bench(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin) {
     return oref_bench2(map_path, n_games, steps, threads, seed, burnin, 0);
 }
+double oref_bench3(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin, int flags);
 // uniform = 1: the c2 workload (unmasked uniform rows, no masks) instead of masks + masked policy
 double oref_bench2(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin, int uniform) {
+    return oref_bench3(map_path, n_games, steps, threads, seed, burnin, uniform ? 1 : 0);
+}
+// flags bit 0: uniform rows (c2); bit 1: partially observable views (c5, PartiallyObservableGameState)
+double oref_bench3(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin, int flags) {
+    const int uniform = flags & 1, po = (flags >> 1) & 1;
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
@@ -903,7 +909,7 @@ double oref_bench2(const char* map_path, int n_games, int steps, int threads, ui
     for (int t = 0; t < threads; t++) {
         per[(size_t)t] = n_games / threads + (t < n_games % threads ? 1 : 0);
         std::vector<const char*> paths((size_t)per[(size_t)t] * 2, map_path);
-        hs[(size_t)t] = oref_create(per[(size_t)t] * 2, 0, nullptr, 2000, 0, 1, 1, paths.data(), seed + (uint64_t)t * 1000003ULL, nullptr);
+        hs[(size_t)t] = oref_create(per[(size_t)t] * 2, 0, nullptr, 2000, po, 1, 1, paths.data(), seed + (uint64_t)t * 1000003ULL, nullptr);
         oref_reset(hs[(size_t)t], nullptr, nullptr, nullptr, nullptr);
     }
     auto worker = [&](int t) {
@@ -943,6 +949,22 @@ double oref_bench2(const char* map_path, int n_games, int steps, int threads, ui
     for (auto& x : th) x.join();
     auto t1 = std::chrono::steady_clock::now();
     for (auto h : hs) oref_destroy(h);
+    return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// BASELINE config c1: JNIBotClient (tests/JNIBotClient.java:108-135) with two RandomBiasedAI sharing
+// one seeded java.util.Random (Sampler.generator is a JVM static, util/Sampler.java:17), one env,
+// bot-only VecClient auto-reset; `steps` timed gameSteps after `burnin` untimed ones.  Seconds.
+double oref_bench_bots(const char* map_path, int steps, int64_t seed, int burnin) {
+    void* h = oref_botclient_create(map_path, BOT_RANDOM_BIASED, BOT_RANDOM_BIASED, 2000, 1, 1, seed, nullptr);
+    if (!h) return -1.0;
+    double rew[RF_COUNT];
+    uint8_t done[RF_COUNT];
+    for (int k = 0; k < burnin; k++) oref_botclient_step(h, 0, rew, done);
+    auto t0 = std::chrono::steady_clock::now();
+    for (int k = 0; k < steps; k++) oref_botclient_step(h, 0, rew, done);
+    auto t1 = std::chrono::steady_clock::now();
+    oref_botclient_destroy(h);
     return std::chrono::duration<double>(t1 - t0).count();
 }
 

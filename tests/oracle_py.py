@@ -67,6 +67,10 @@ def load():
         L.oref_bench.argtypes = [ctypes.c_char_p, I, I, I, U64, I]
         L.oref_bench2.restype = ctypes.c_double
         L.oref_bench2.argtypes = [ctypes.c_char_p, I, I, I, U64, I, I]
+        L.oref_bench3.restype = ctypes.c_double
+        L.oref_bench3.argtypes = [ctypes.c_char_p, I, I, I, U64, I, I]
+        L.oref_bench_bots.restype = ctypes.c_double
+        L.oref_bench_bots.argtypes = [ctypes.c_char_p, I, ctypes.c_int64, I]
         L.oref_policy_uniform.argtypes = [I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, P]
         _lib = L
     return _lib

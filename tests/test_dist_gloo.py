@@ -108,3 +108,38 @@ def test_observation_gather_pipeline(mode):
                 continue
             assert np.array_equal(got.reshape(o.shape).astype(np.int32), o), f"rank {rank} step {step}"
     whole.close()
+
+
+def test_launcher_gpus_2_equals_one_run(tmp_path):
+    """`--gpus N` without torch.distributed.run spawns N ranks (microrts_amd.launch,
+    the launcher bench.py uses), each with RANK / LOCAL_RANK / WORLD_SIZE set; the world the ranks see
+    is 2, and their shards all-gathered equal one process running all 2G games."""
+    import json
+    import subprocess
+    import sys
+
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_launch_worker.py")
+    out = str(tmp_path / "res")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, worker, "--gpus", "2", "--out", out], env=env, timeout=300)
+    assert r.returncode == 0
+    info = json.load(open(out + ".json"))
+    assert info["n_gpus"] == 2 and info["world_size"] == 2 and info["max_time"] == 2.0
+    from tests.dist_launch_worker import G as WG, rollout
+
+    gathered = np.load(out + ".npy")
+    whole = rollout(2 * WG, 0)
+    assert np.array_equal(gathered.reshape(whole.shape).astype(np.int32), whole)
+
+
+def test_launcher_rejects_world_mismatch(tmp_path):
+    """Under a launcher, --gpus must equal WORLD_SIZE (bench.py hard-fails instead of silently
+    running a different world)."""
+    import subprocess
+    import sys
+
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_launch_worker.py")
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, worker, "--gpus", "2", "--out", str(tmp_path / "x")], env=env, timeout=120,
+                       capture_output=True, text=True)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
