@@ -587,15 +587,45 @@ def main():
     # roofline.traffic: HBM bytes per k_env launch from the rocprofv3 --pmc passes of this same command
     # (tools/gpu_profile.sh + tools/summarize_profile.py -> profiles/pmc_latest.json), when they exist
     traffic, traffic_src = a.pmc_traffic, "--pmc-traffic (bytes per launch)" if a.pmc_traffic is not None else None
-    pl = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if traffic is None and os.path.exists(pl):
+    # per-config counters of the same command (tools/profile_config.sh + tools/profile_summary.py)
+    pj = None
+    pl = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
+    if os.path.exists(pl):
         pj = json.load(open(pl))
-        if (pj.get("mask_mode") == a.mask_mode and pj.get("envs_per_gpu") == E and a.map in (pj.get("workload") or "")
-                and ("multi-step" in pj.get("kernel", "")) == (launch_ms is not None)):
-            per_step = pj.get("traffic_bytes_per_step", pj.get("traffic_bytes_per_launch"))
-            traffic = per_step * steps_per_launch
-            traffic_src = (f"profiles/pmc_latest.json ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes; "
-                           f"{per_step / 1e6:.1f} MB per step x {steps_per_launch} steps per launch)")
+        if not (pj.get("envs_per_gpu") == E and a.map in (pj.get("workload") or "")
+                and pj.get("mask_mode") == ("off" if uniform else a.mask_mode) and launch_ms is not None):
+            pj = None  # another workload or launch form: its counters do not describe this line
+    if traffic is None and pj is not None and pj.get("traffic_bytes_per_step"):
+        per_step = pj["traffic_bytes_per_step"]
+        traffic = per_step * steps_per_launch
+        traffic_src = (f"profiles/pmc_{a.config}.json ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes; "
+                       f"{per_step / 1e6:.1f} MB per step x {steps_per_launch} steps per launch)")
+    issue = None
+    if pj is not None and pj.get("issue"):
+        # the issue roofline: VALU instructions per game-step x game-steps/s against the chip's VALU issue
+        # ceiling — 1024 SIMDs x one wave64 VALU instruction per quad-cycle each (SQ_ACTIVE_INST_VALU
+        # measured ~1 quad-cycle per instruction) at the clock GRBM_GUI_ACTIVE gives for the launch
+        iq = pj["issue"]
+        per = iq["per_game_step"]
+        clk = iq.get("clock_ghz_grbm") or 2.4
+        rate = E / (kern_ms * 1e-3)  # game-steps per second of kernel time
+        valu = per["SQ_INSTS_VALU"] * rate
+        ceiling = 1024 * clk * 1e9 / 4
+        issue = {
+            "bound": "valu_issue",
+            "valu_insts_per_game_step": per["SQ_INSTS_VALU"],
+            "salu_insts_per_game_step": per.get("SQ_INSTS_SALU"),
+            "lds_insts_per_game_step": per.get("SQ_INSTS_LDS"),
+            "achieved": valu / 1e9,
+            "peak": ceiling / 1e9,
+            "unit": "G wave-VALU-instructions/s",
+            "frac": valu / ceiling,
+            "valu_busy_frac": iq.get("valu_busy_frac"),
+            "valu_lane_utilization": iq.get("valu_lane_utilization"),
+            "dual_issue_quad_cycles_per_game_step": per.get("SQ_ACTIVE_INST_VALU2"),
+            "clock_ghz": clk,
+            "source": f"profiles/pmc_{a.config}.json ({pj['tag']}: SQ PMC pass of the same command)",
+        }
     total_games = E * world
     value = total_games * a.steps / t
     out = {
@@ -654,7 +684,11 @@ def main():
         "mean_units": mean_units,
         "decoded_rows_per_slot": rows,
         "roofline": {
-            "bound": "hbm",
+            "bound": "valu_issue" if issue is not None and issue["frac"] > achieved / HBM_PEAK_GBS else "hbm",
+            "bound_note": "the HBM figures below are the step contract's bytes; the counters show the kernel limited by "
+                          "VALU issue (roofline.issue)" if issue is not None and issue["frac"] > achieved / HBM_PEAK_GBS
+                          else "HBM step-contract bytes",
+            "issue": issue,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
