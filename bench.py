@@ -653,6 +653,8 @@ def main():
                         + (f", max_units {a.max_units} (capacity errors checked)" if a.max_units else ""),
             "envs_per_gpu": E,
             "utt": "VERSION_ORIGINAL, CANCEL_BOTH",
+            "reward_functions": "[WinLossRewardFunction] (with one reward function Java's self-play reset throws, "
+                                "JNIGridnetClientSelfPlay.java:235-238; here the one slot is zeroed — DESIGN.md §8)",
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": "off" if uniform else a.mask_mode,

@@ -19,9 +19,13 @@ def main():
         if r["Kernel_Name"].startswith("k_env"):
             vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
     ds = sorted(vals)
-    med = sorted(vals[d]["SQ_INSTS_VALU"] for d in ds)[len(ds) // 2]
-    multi = [d for d in ds if vals[d]["SQ_INSTS_VALU"] > 5 * med]
-    multi = multi[-len(meta["order"]):]
+    # every variant enqueues the same dispatch pattern (fused: a single-step launch, then the multi-step
+    # one; uniform: the multi-step one): the tail of the dispatch list is len(order) groups of p; the
+    # burn-in (reset, its launches) precedes them.  In each group the launch with most VALU instructions.
+    n = len(meta["order"])
+    p = next(q for q in (1, 2, 3) if 1 <= len(ds) - n * q <= 5)
+    tail = ds[len(ds) - n * p:]
+    multi = [max(tail[i * p:(i + 1) * p], key=lambda d: vals[d]["SQ_INSTS_VALU"]) for i in range(n)]
     gs = meta["games"] * meta["steps_per_multi_launch"]
     base = [vals[d] for d, n in zip(multi, meta["order"]) if n == "baseline"]
     b = {c: sum(x[c] for x in base) / len(base) for c in base[0]}
