@@ -626,6 +626,19 @@ def main():
             "clock_ghz": clk,
             "source": f"profiles/pmc_{a.config}.json ({pj['tag']}: SQ PMC pass of the same command)",
         }
+    # what the counters show bounds the kernel: VALU issue when the SIMDs' vector issue is saturated
+    # over the waves' lifetimes (c3: four games per SIMD), else the per-game dependent chain (c2 / c5:
+    # one / two games per SIMD leave the issue half idle); HBM only without counters
+    if issue is not None and (issue.get("valu_busy_frac") or 0) >= 0.9:
+        bound, bound_note = "valu_issue", ("SIMD vector issue busy {:.0%} of the waves' lifetimes (roofline.issue); the "
+                                           "HBM figures are the step contract's bytes".format(issue["valu_busy_frac"]))
+    elif issue is not None:
+        bound, bound_note = "latency", ("per-game dependent chain: SIMD vector issue busy only {:.0%} of the waves' "
+                                        "lifetimes with {:.0f} game(s) per SIMD (roofline.issue); the HBM figures are the "
+                                        "step contract's bytes".format(issue.get("valu_busy_frac") or 0,
+                                                                       (pj or {}).get("issue", {}).get("games_per_simd", 0)))
+    else:
+        bound, bound_note = "hbm", "HBM step-contract bytes (no counter file for this workload)"
     total_games = E * world
     value = total_games * a.steps / t
     out = {
@@ -686,10 +699,8 @@ def main():
         "mean_units": mean_units,
         "decoded_rows_per_slot": rows,
         "roofline": {
-            "bound": "valu_issue" if issue is not None and issue["frac"] > achieved / HBM_PEAK_GBS else "hbm",
-            "bound_note": "the HBM figures below are the step contract's bytes; the counters show the kernel limited by "
-                          "VALU issue (roofline.issue)" if issue is not None and issue["frac"] > achieved / HBM_PEAK_GBS
-                          else "HBM step-contract bytes",
+            "bound": bound,
+            "bound_note": bound_note,
             "issue": issue,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
