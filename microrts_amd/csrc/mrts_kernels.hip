@@ -2430,7 +2430,50 @@ struct Game {
     }
     DEV void writeObsFull(int slot0, int nslots, int player0) {
         int32_t* o0 = D.obs + (size_t)slot0 * D.C * HW;
-        if ((HW & 3) == 0) {
+        if (HW <= 64) {
+            // small maps (8x8: c2): lane = cell, one LDS round for the cell entry and one for its
+            // occupant's fields, one dword store per plane (64 lanes = 256 contiguous bytes) — the
+            // 4-cells-per-lane form below would leave 48 of the 64 lanes idle and quadruple each
+            // active lane's dependent work
+            const int c = lid();
+            if (c < HW) {
+                const int sc = cell[c];
+                const int s = sc < CAP ? sc : 0;
+                const uint32_t cu = uc[s], ca = ua[s];
+                const int ch = hp[s], cr = res[s];
+                const bool occ = sc < CAP;
+                const int pl = uplay(cu);
+                int v[6];
+                v[0] = occ ? ch : 0;
+                v[1] = occ ? cr : 0;
+                v[2] = (occ && pl >= 0) ? ((pl + player0) % 2) + 1 : 0;
+                v[3] = occ ? utyp(cu) + 1 : 0;
+                v[4] = (occ && (ca & UA_PRESENT)) ? ua_type(ca) : 0;
+                v[5] = sc == WALL ? 1 : 0;
+                const __amdgpu_buffer_rsrc_t rs = bufRsrc(o0, (uint32_t)(nslots * D.C * HW * 4));
+                const int npl = firstIt ? 6 : 5;  // the static terrain plane: first write of a launch only
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    if (i >= nslots) break;
+#pragma unroll
+                    for (int q = 0; q < 6; q++) {
+                        if (q >= npl) break;
+                        // the other player's view differs only in the owner plane
+                        const int x = (i && q == 2 && v[2]) ? 3 - v[2] : v[q];
+                        const uint32_t off = (uint32_t)((i * D.C + q) * HW + c);
+                        if (SC1_OBS) __builtin_amdgcn_raw_buffer_store_b32(x, rs, (int)(off * 4u), 0, 16);
+                        else st1<WT_OBS>(o0 + off, x);
+                    }
+                }
+                if (MRTS_UNLIKELY(D.obs16 != nullptr)) {  // the int16 transport copy (mrts_set_obs16)
+                    int16_t* h0 = D.obs16 + (size_t)slot0 * D.C * HW;
+                    for (int i = 0; i < nslots; i++)
+#pragma unroll
+                        for (int q = 0; q < 6; q++)
+                            h0[(size_t)(i * D.C + q) * HW + c] = (int16_t)((i && q == 2 && v[2]) ? 3 - v[2] : v[q]);
+                }
+            }
+        } else if ((HW & 3) == 0) {
             for (int c4 = 4 * lid(); c4 < HW; c4 += 256) {
                 // obsCell for 4 cells without branches: the 4 cell entries, then the occupants' 4
                 // fields each (an empty cell reads slot 0 and is masked), so the lane waits for two
@@ -2696,6 +2739,10 @@ struct Game {
         uint32_t* const rowsV0 = vis;   // [mine H][theirs H]
         uint32_t* const rowsV1 = vis2;
         int32_t* pr = D.po_prev ? D.po_prev + (size_t)g * D.po_words : nullptr;
+        // the record's global copy is for the next launch: inside a multi-step launch this render keeps
+        // the record in LDS (poLds) and the next iteration reads it there, so only the last iteration
+        // stores it (the sight rows and pending chunks here, the snapshot bytes in poRecordSnaps)
+        int32_t* const prG = (!iter || lastIt) ? pr : nullptr;
         const int SW = poSnapWords(CAP);
         const bool d0 = delta & 1u, d1 = (delta >> 1) & 1u;
         const int nu0 = delta ? hget(H_NU) : 0;  // the header holds the loaded unit count until store()
@@ -2776,7 +2823,7 @@ struct Game {
                         }
                     }
                 }
-                if (pr) pr[1 + SW + v * 2 * H + l] = (int32_t)row;
+                if (prG) prG[1 + SW + v * 2 * H + l] = (int32_t)row;
                 if (!(v ? d1 : d0)) poVis[v * 2 * H + l] = row;
             }
         }
@@ -2799,8 +2846,10 @@ struct Game {
             }
         }
         if (pr && l < NCW) {
-            pr[1 + SW + 4 * H + l] = (int32_t)poDirty[NCW + l];
-            pr[1 + SW + 4 * H + NCW + l] = (int32_t)poDirty[3 * NCW + l];
+            if (prG) {
+                prG[1 + SW + 4 * H + l] = (int32_t)poDirty[NCW + l];
+                prG[1 + SW + 4 * H + NCW + l] = (int32_t)poDirty[3 * NCW + l];
+            }
             poPend[l] = poDirty[NCW + l];  // LDS copies, as the sight rows above
             poPend[NCW + l] = poDirty[3 * NCW + l];
         }
@@ -3054,10 +3103,14 @@ struct Game {
     // after the compaction: the snapshot bytes of the final slots and the views this launch rendered
     DEV void poRecordSnaps(uint32_t views) {
         int32_t* pr = D.po_prev + (size_t)g * D.po_words;
+        // a render that kept its record in LDS (poLds) is followed, inside a multi-step launch, by an
+        // iteration that reads the LDS copies: the global record is then stored at the last iteration only
+        const bool glob = !iter || lastIt || !poLds;
         const uint32_t* sw = (const uint32_t*)snap;
-        for (int w = lid(); w < (nu + 3) / 4; w += 64) pr[1 + w] = (int32_t)sw[w];
+        if (glob)
+            for (int w = lid(); w < (nu + 3) / 4; w += 64) pr[1 + w] = (int32_t)sw[w];
         if (lid() == 0) {
-            pr[0] = (int32_t)views;
+            if (glob) pr[0] = (int32_t)views;
             hdr[HX_POVALID] = (int32_t)views;  // the record's LDS copy (multi-step launch)
         }
     }
