@@ -161,6 +161,9 @@ struct KDyn {
     // full-observability self-play kernels; the host issues it only in the steady fused state:
     // pol_delta = fwd_read = mask_delta = 1)
     int32_t n_iter;
+    // helper-wave multi-step launches (8x8 fused uniform rollouts, BASELINE c2): byte offset of the
+    // LDS handoff area (rows of the next step, packed observation cells) after the game's own LDS
+    int32_t help_off;
 };
 // PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);
 // snapshot bytes of the unit slots (after the end-of-step compaction); per view p the sight rows

@@ -466,6 +466,9 @@ struct Game {
     int readySlot;         // per lane: the unit slot of ready item lid() (-1 outside cycle)
     uint32_t polStep;      // the fused policy's Philox step (D.pol_step, + 1 per iteration of a multi-step launch)
     uint32_t uniStep;      // the fused uniform policy's step (D.uni_step, likewise)
+    // helper-wave launch (k_env HELP): this iteration's uniform rows, drawn by the helper wave,
+    // packed (packFwd) per [player slot][cell]; null = draw them here (fetchRow)
+    const uint32_t* helpRows = nullptr;
     int maxProd0, maxProd1, sumProd0, sumProd1;
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
@@ -895,6 +898,10 @@ struct Game {
     // uniform-policy step (KDyn.uni_actions), the Philox row the launch also writes there
     // (writeUniformRows) — drawn again in registers instead of read back.
     DEV void fetchRow(const int32_t* rows, int slot, int c, int32_t a[7]) const {
+        if (helpRows) {  // the helper wave drew this step's rows (self-play: slot & 1 = player)
+            unpackFwd(helpRows[(slot & 1) * HW + c], a);
+            return;
+        }
         if (D.uni_actions) {
             uniformRow(D.uni_seed, uniStep, D.uni_slot_base + (uint32_t)slot, c, NT, K - 23 - NT, a);
             return;
@@ -2563,6 +2570,23 @@ struct Game {
             }
         }
     }
+    // helper-wave launch: the observation's cells for the helper wave to render (lane = cell, HW <= 64),
+    // player 0's view: word 0 = hp | resources << 16, word 1 = owner | type << 4 | action << 8 | wall << 12
+    DEV void packObs(uint32_t* buf) const {
+        const int c = lid();
+        if (c < HW) {
+            const int sc = cell[c];
+            const int s = sc < CAP ? sc : 0;
+            const uint32_t cu = uc[s], ca = ua[s];
+            const bool occ = sc < CAP;
+            const int pl = uplay(cu);
+            const uint32_t v0 = occ ? (uint32_t)(uint16_t)hp[s] : 0u, v1 = occ ? (uint32_t)(uint16_t)res[s] : 0u;
+            const uint32_t v2 = (occ && pl >= 0) ? (uint32_t)(pl + 1) : 0u, v3 = occ ? (uint32_t)utyp(cu) + 1 : 0u;
+            const uint32_t v4 = (occ && (ca & UA_PRESENT)) ? (uint32_t)ua_type(ca) : 0u, v5 = sc == WALL ? 1u : 0u;
+            buf[2 * c] = v0 | (v1 << 16);
+            buf[2 * c + 1] = v2 | (v3 << 4) | (v4 << 8) | (v5 << 12);
+        }
+    }
     // PartiallyObservableGameState.getVectorObservation (rts/PartiallyObservableGameState.java:82-154):
     // the snapshot's units (live fields, possibly dead) in list order, last writer per cell; the
     // snapshot's assignments; walls; own / enemy sight disks of the snapshot units (:211-234).
@@ -3771,12 +3795,79 @@ DEV void aiGetAction(Game& G, int kind, int p) {
 // observability compile-time constants, so LDS offsets fold into immediates and the bot / Java-row
 // code vanishes — c3 (16x16, 320 slots), c2 (8x8, 128), c5 (32x32 PO, 320 slots = max_units 256).
 // FIX = 0: anything (launchEnv picks).
-template <int MODE, int FIX, int FCAP = 0, bool FPO = false, bool MULTI = false>
+// The helper wave of a HELP launch (8x8 fused uniform multi-step rollouts, BASELINE c2: one game per
+// SIMD, so the SIMD idles while the game's wave runs its dependent chain).  Work with no input from the
+// game's state moves to a second wave of the workgroup: the unmasked uniform rows (a pure function of
+// slot, step and cell) of the NEXT step — to the action tensor, and packed into LDS for the game wave's
+// decode — and the observation planes of the PREVIOUS step from the cells the game wave packed.  One
+// workgroup barrier per step (A_k: rows(k) ready, obs cells of step k - 1 packed); each LDS buffer is
+// double-buffered by step parity, so a buffer is rewritten only after the other wave passed the
+// barrier that ends its use.  Output: every buffer ends exactly as after the same steps in one wave.
+DEV void helperLoop(const KDyn& D, uint8_t* smem, int g, int niter) {
+    constexpr int HW = 64, NT = 7, K = 79;
+    const int l = (int)threadIdx.x - 64;
+    uint32_t* rowbuf = (uint32_t*)(smem + D.help_off);  // [parity][player slot][cell]
+    uint32_t* obsbuf = rowbuf + 2 * 2 * HW;             // [parity][cell][2]
+    const int slot0 = 2 * g;
+    auto rowsOf = [&](int k) {
+        for (int i = 0; i < 2; i++) {
+            int32_t a[7];
+            uniformRow(D.uni_seed, D.uni_step + (uint32_t)k, D.uni_slot_base + (uint32_t)(slot0 + i), l, NT, K - 23 - NT, a);
+            int32_t* dst = D.uni_actions + ((size_t)(slot0 + i) * HW + l) * 7;
+            st4u<false>(dst, a[0], a[1], a[2], a[3]);
+            st3u<false>(dst + 4, a[4], a[5], a[6]);
+            rowbuf[(k & 1) * 2 * HW + i * HW + l] = packFwd(a);
+        }
+    };
+    auto render = [&](int k) {
+        if (!D.obs) return;
+        const uint32_t w0 = obsbuf[(k & 1) * 2 * HW + 2 * l], w1 = obsbuf[(k & 1) * 2 * HW + 2 * l + 1];
+        int v[6];
+        v[0] = (int)(int16_t)(w0 & 0xFFFFu);
+        v[1] = (int)(w0 >> 16);
+        v[3] = (int)((w1 >> 4) & 15u);
+        v[4] = (int)((w1 >> 8) & 15u);
+        v[5] = (int)((w1 >> 12) & 1u);
+        const int own = (int)(w1 & 15u);  // player + 1, 0 = none
+        int32_t* o0 = D.obs + (size_t)slot0 * D.C * HW;
+        const __amdgpu_buffer_rsrc_t rs = bufRsrc(o0, (uint32_t)(2 * D.C * HW * 4));
+        const int npl = k == 0 ? 6 : 5;  // the static terrain plane: first write of the launch only
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            v[2] = own ? ((own - 1 + i) % 2) + 1 : 0;  // ((owner + player) % 2) + 1 (GameState.java:947-949)
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                if (q >= npl) break;
+                const uint32_t off = (uint32_t)((i * D.C + q) * HW + l);
+                if (SC1_OBS) __builtin_amdgcn_raw_buffer_store_b32(v[q], rs, (int)(off * 4u), 0, 16);
+                else st1<WT_OBS>(o0 + off, v[q]);
+            }
+            if (MRTS_UNLIKELY(D.obs16 != nullptr)) {
+                int16_t* h0 = D.obs16 + (size_t)(slot0 + i) * D.C * HW;
+#pragma unroll
+                for (int q = 0; q < 6; q++) h0[(size_t)q * HW + l] = (int16_t)v[q];
+            }
+        }
+    };
+    rowsOf(0);
+    __syncthreads();  // A_0
+    for (int k = 0; k < niter; k++) {
+        if (k + 1 < niter) rowsOf(k + 1);
+        __syncthreads();  // A_{k+1}: the game wave packed step k's cells; rows(k + 1) are in LDS
+        render(k);
+    }
+}
+
+template <int MODE, int FIX, int FCAP = 0, bool FPO = false, bool MULTI = false, bool HELP = false>
 // stateArg and PS lead the argument list so that kernarg preloading (-amdgpu-kernarg-preload-count,
 // Makefile) hands them over in SGPRs: the first memory round (state block, unit-type table) issues
 // without waiting for a scalar load of the kernel arguments.
-__global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, const KStatic* __restrict__ PS, KDyn D) {
+__global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ stateArg, const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
+    if (HELP && threadIdx.x >= 64) {
+        helperLoop(D, smem, (int)blockIdx.x, D.n_iter);
+        return;
+    }
     const KStatic& P = *PS;
     Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
            FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI);
@@ -3835,11 +3926,14 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
 #ifdef MRTS_PHASE_TIMING
     int nu0_ = 0;
 #endif
+    uint32_t* const helpBuf = HELP ? (uint32_t*)(smem + D.help_off) : nullptr;  // helperLoop's layout
+    if (HELP) __syncthreads();  // A_0: the helper drew step 0's rows
     for (int it = 0; it < niter; it++) {
     if (it > 0) {
         G.nextStep();
         freshObs = true;
     }
+    if (HELP) G.helpRows = helpBuf + (it & 1) * 2 * 64;
     G.lastIt = it == niter - 1;
     G.firstIt = it == 0;
     if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
@@ -3903,7 +3997,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
         const size_t rowStride = (size_t)G.HW * 7;
         // fused uniform policy: this step's rows go out first (fire-and-forget stores, nothing in the
         // launch reads them back: fetchRow draws the idle units' rows again)
-        if (D.uni_actions) G.writeUniformRows(slot0, nslots);
+        if (D.uni_actions && !HELP) G.writeUniformRows(slot0, nslots);
         if (MRTS_UNLIKELY(D.reward_need & RN_COUNTS))
             if (lane_id() < 2 * RC_N) G.rwc[lane_id()] = 0;
         if (MRTS_UNLIKELY(D.reward_need & RN_CLOSER)) G.closerBefore();
@@ -4026,6 +4120,8 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
 #endif
                 G.writeObsPO(slot0 + i, p, ((valid >> p) & 1u) != 0);
             }
+        } else if (HELP) {
+            G.packObs(helpBuf + 2 * 2 * 64 + (it & 1) * 2 * 64);  // the helper wave renders it
         } else {
 #ifdef MRTS_ABLATE
             if (!G.ab(AB_SKIP_OBS))
@@ -4036,6 +4132,7 @@ __global__ __launch_bounds__(64) void k_env(int32_t* __restrict__ stateArg, cons
 #endif
         }
     }
+    if (HELP) __syncthreads();  // A_{it+1}: step it's cells packed; the helper's rows of step it + 1 ready
     PHASE(6);
     if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
     PHASE(7);
@@ -4494,7 +4591,13 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
     switch (mode) {
         case MODE_STEP:
             if (D.n_iter > 1 && is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false, true>), grid, block, lds, stream, D.state, ds, D);
-            else if (D.n_iter > 1 && is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true>), grid, block, lds, stream, D.state, ds, D);
+            else if (D.n_iter > 1 && is(8, 128, false) && D.uni_actions && !D.masks) {
+                // c2's fused uniform rollout: a helper wave per game (helperLoop)
+                KDyn D2 = D;
+                D2.help_off = (int32_t)((lds + 15) & ~(size_t)15);
+                hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true, true>), grid, dim3(128), (size_t)D2.help_off + 2048, stream,
+                                   D.state, ds, D2);
+            } else if (D.n_iter > 1 && is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true>), grid, block, lds, stream, D.state, ds, D);
             else if (D.n_iter > 1 && is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
             else if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
             else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, D.state, ds, D);
