@@ -133,6 +133,10 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_MULTI_NOPRIO
 #define MRTS_MULTI_NOPRIO 0
 #endif
+// 1: partially observable multi-step launches without the render helper wave (A/B builds)
+#ifndef MRTS_NO_PO_HELPER
+#define MRTS_NO_PO_HELPER 0
+#endif
 // issue-priority thresholds on a game's unit count (k_env): 1 / 2 / 3 from T1 / T2 / T3 units
 // (units + own idle units; measured against units alone at 24 / 30 / 36: c3 +1.8 % at K = 200,
 // +0.8 % at K = 20)
@@ -2966,6 +2970,219 @@ struct Game {
         wsync();
     }
     DEV bool poFast2() const { return (W & 3) == 0 && W <= 32 && H <= 32 && nu <= 64 && U.maxSight <= 15; }
+    // Helper-wave launch, partially observable self-play (k_env HELP && FPO, BASELINE c5): the game
+    // wave hands this step's render inputs to the helper wave instead of rendering (writeObsPOFast2's
+    // unit pass reads, per unit slot < 64: the unit word, hp | resources, the snapshot byte, and the
+    // previous record's position / key / snapshot byte), and the helper renders while the game runs
+    // its compaction, masks, policy and the next step.  pk = [5][64] words, ph = [4] header words:
+    // unit count, the previous record's unit count, flags (bits 0-1 delta per view, bit 2 render).
+    DEV void packPO(uint32_t* pk, uint32_t* ph, uint32_t delta) {
+        const int l = lid();
+        const bool live = l < nu;
+        pk[l] = live ? uc[l] : 0u;
+        pk[64 + l] = live ? ((uint32_t)(uint16_t)hp[l] | ((uint32_t)(uint16_t)res[l] << 16)) : 0u;
+        pk[128 + l] = (live ? (uint32_t)snap[l] : 0u) | ((lsnap & 0xFFu) << 8);
+        pk[192 + l] = lcu;
+        pk[256 + l] = lkey;
+        if (l == 0) {
+            ph[0] = (uint32_t)nu;
+            ph[1] = (uint32_t)hget(H_NU);
+            ph[2] = (delta & 3u) | 4u;
+        }
+        poLds = D.po_prev != nullptr;  // the helper keeps the record's LDS copies, as writeObsPOFast2 does
+    }
+    // writeObsPOFast2 as run by the helper wave (lane l = threadIdx.x - 64) from a packed step (packPO):
+    // the same passes and stores.  What the game wave's live LDS state gave it comes from the pack:
+    // the units' fields, and the live occupant of a cell from hcell (slot, or 0xFF), a per-step map
+    // built here from the packed positions (a unit in the list and not dead = the game's cell map);
+    // walls from the game's cell map (WALL entries are static: units never stand on walls).  rowsV0 =
+    // the helper's own view-0 sight rows (the game wave's snapshots use `vis` meanwhile).  last: the
+    // launch's last iteration stores the record's sight rows and pending chunks globally.
+    DEV void renderPOPacked(const uint32_t* pk, const uint32_t* ph, uint32_t* rowsV0, uint8_t* hcell, bool last) {
+        const int l = (int)threadIdx.x - 64;
+        const int NCW = poChunkWords(HW), NC = HW >> 2;
+        uint32_t* const rowsV1 = vis2;
+        int32_t* pr = D.po_prev ? D.po_prev + (size_t)g * D.po_words : nullptr;
+        int32_t* const prG = last ? pr : nullptr;
+        const int SW = poSnapWords(CAP);
+        const int nuP = (int)ph[0], nu0 = (int)ph[1];
+        const uint32_t delta = ph[2] & 3u;
+        const bool d0 = delta & 1u, d1 = (delta >> 1) & 1u;
+        if (l < 2 * H) {
+            rowsV0[l] = 0;
+            rowsV1[l] = 0;
+        }
+        if (l < NCW) {
+            poDirty[l] = d0 ? poPend[l] : 0u;
+            poDirty[NCW + l] = 0u;
+            poDirty[2 * NCW + l] = d1 ? poPend[NCW + l] : 0u;
+            poDirty[3 * NCW + l] = 0u;
+        }
+        for (int i = l; i < HW / 8; i += 64) ((uint2*)hcell)[i] = make_uint2(~0u, ~0u);  // (8-byte aligned)
+        const bool live = l < nuP;
+        const uint32_t cu = pk[l], kv = pk[64 + l], sw = pk[128 + l];
+        const uint32_t lcuP = pk[192 + l], lkeyP = pk[256 + l];
+        const uint32_t sb = sw & 0xFFu, lsnapP = (sw >> 8) & 0xFFu;
+        const int hv = (int)(int16_t)(kv & 0xFFFFu), rv = (int)(int16_t)(kv >> 16);
+        const bool in0 = live && snap_in(sb, 0), in1 = live && snap_in(sb, 1);
+        const bool isDead = (cu & UC_DEAD) != 0;
+        const bool dead0 = in0 && isDead, dead1 = in1 && isDead;
+        const int cc = uy(cu) * W + ux(cu);
+        const int own = uplay(cu);
+        wsync();
+        if (live && !isDead) hcell[cc] = (uint8_t)l;
+        {
+            const bool pt0 = in0 && own >= 0, pt1 = in1 && own >= 0;
+            if (ballot(pt0 || pt1))
+                paintDisks2(pt0, own == 0 ? rowsV0 : rowsV0 + H, pt1, own == 1 ? rowsV1 : rowsV1 + H, cu);
+        }
+        const uint64_t deadM0 = ballot(dead0), deadM1 = ballot(dead1);
+        if (pr && dead0) atomicOr(&poDirty[NCW + (cc >> 7)], 1u << ((cc >> 2) & 31));
+        if (pr && dead1) atomicOr(&poDirty[3 * NCW + (cc >> 7)], 1u << ((cc >> 2) & 31));
+        if (delta && (live || l < nu0)) {
+            const int cp = uy(lcuP) * W + ux(lcuP);
+            const uint32_t key = (uint32_t)(uint16_t)hv | ((uint32_t)(uint16_t)rv << 16);
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                if (!(v ? d1 : d0)) continue;
+                const bool in = v ? in1 : in0;
+                const bool inP = l < nu0 && ((lsnapP >> v) & 1u);
+                bool chg = in != inP;
+                if (in && inP)
+                    chg = cc != cp || key != lkeyP || snap_act(sb, v) != (int)((lsnapP >> (2 + 3 * v)) & 7u);
+                uint32_t* dirty = poDirty + 2 * v * NCW;
+                if (chg && inP) atomicOr(&dirty[cp >> 7], 1u << ((cp >> 2) & 31));
+                if (chg && in) atomicOr(&dirty[cc >> 7], 1u << ((cc >> 2) & 31));
+            }
+        }
+        wsync();
+        if (l < 2 * H) {  // sight rows: changed columns -> chunk bits of that row; the record's copies
+            const int y = l < H ? l : l - H;
+            const int k0 = y * (W >> 2);
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const uint32_t row = (v ? rowsV1 : rowsV0)[l];
+                if (v ? d1 : d0) {
+                    const uint32_t d = row ^ poVis[v * 2 * H + l];
+                    if (d) {
+                        uint32_t gbits = 0;  // bit j = column group 4j..4j+3 changed
+#pragma unroll
+                        for (int j = 0; j < 8; j++) gbits |= ((d >> (4 * j)) & 0xFu) ? (1u << j) : 0u;
+                        uint32_t* dirty = poDirty + 2 * v * NCW;
+                        if ((k0 & 31) + (W >> 2) <= 32) {
+                            atomicOr(&dirty[k0 >> 5], gbits << (k0 & 31));
+                        } else {
+                            for (uint32_t gg = gbits; gg; gg &= gg - 1) {
+                                const int k = k0 + __builtin_ctz(gg);
+                                atomicOr(&dirty[k >> 5], 1u << (k & 31));
+                            }
+                        }
+                    }
+                }
+                poVis[v * 2 * H + l] = row;  // the record's LDS copy (the next render)
+                if (prG) prG[1 + SW + v * 2 * H + l] = (int32_t)row;
+            }
+        }
+        wsync();
+        int n = 0;  // (view << 15 | chunk) items: view 0's dirty chunks (all, without delta), then view 1's
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const bool dv = v ? d1 : d0;
+            const uint32_t* dirty = poDirty + 2 * v * NCW;
+#pragma unroll
+            for (int c0 = 0; c0 < 256; c0 += 64) {  // NC <= 256 (H, W <= 32)
+                if (c0 < NC) {
+                    const int k = c0 + l;
+                    const bool dk = k < NC && (!dv || ((dirty[k >> 5] >> (k & 31)) & 1u));
+                    const uint64_t m = ballot(dk);
+                    if (dk) poList[n + lanes_below(m)] = (uint16_t)((v << 15) | k);
+                    n += __popcll(m);
+                }
+            }
+        }
+        if (pr && l < NCW) {
+            if (prG) {
+                prG[1 + SW + 4 * H + l] = (int32_t)poDirty[NCW + l];
+                prG[1 + SW + 4 * H + NCW + l] = (int32_t)poDirty[3 * NCW + l];
+            }
+            poPend[l] = poDirty[NCW + l];
+            poPend[NCW + l] = poDirty[3 * NCW + l];
+        }
+        wsync();
+        int32_t* out = D.obs + (size_t)(2 * g) * D.C * HW;
+        const __amdgpu_buffer_rsrc_t rs = bufRsrc(out, (uint32_t)(2 * D.C * HW * 4));
+        const uint64_t deadAny = deadM0 | deadM1;
+        for (int it = l; it < n; it += 64) {
+            const uint32_t e = poList[it];
+            const int v = (int)(e >> 15), c4 = (int)(e & 0x7FFFu);  // lane = 4 consecutive cells of one row
+            const uint64_t deadM = v ? deadM1 : deadM0;
+            const int y = (4 * c4) / W, x0 = (4 * c4) % W;
+            const uint32_t* rows = v ? rowsV1 : rowsV0;
+            const uint32_t occ4 = ((const uint32_t*)hcell)[c4];
+            int cs[4], sl[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t o = (occ4 >> (8 * j)) & 0xFFu;
+                cs[j] = o != 0xFFu ? (int)o : (cell[4 * c4 + j] == WALL ? (int)WALL : (int)EMPTY);
+            }
+            const uint32_t mr = rows[y], tr = rows[H + y];
+            uint32_t ocu[4], osb[4];
+            int ohp[4], ors[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {  // the live occupant's fields (an empty cell reads slot 0, masked)
+                const int s = cs[j] < CAP ? cs[j] : 0;
+                ocu[j] = pk[s];
+                const uint32_t k2 = pk[64 + s];
+                osb[j] = pk[128 + s] & 0xFFu;
+                ohp[j] = (int)(int16_t)(k2 & 0xFFFFu);
+                ors[j] = (int)(int16_t)(k2 >> 16);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) sl[j] = (cs[j] < CAP && snap_in(osb[j], v)) ? cs[j] : -1;
+            for (uint64_t m = deadAny; m; m &= m - 1) {  // the view's dead units: a later list position wins
+                const int ds = __builtin_ctzll(m);
+                const uint32_t dcu = uniu((uint32_t)rl((int)cu, ds));
+                const int dcell = uy(dcu) * W + ux(dcu);
+                const int dh = rl(hv, ds), dr = rl(rv, ds);
+                const uint32_t dsb = uniu((uint32_t)rl((int)sb, ds));
+                const bool mine = (deadM >> ds) & 1ull;
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (mine && dcell == 4 * c4 + j && ds > sl[j]) {
+                        sl[j] = ds;
+                        ocu[j] = dcu;
+                        osb[j] = dsb;
+                        ohp[j] = dh;
+                        ors[j] = dr;
+                    }
+            }
+            int vv[4][8];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const bool occ = sl[j] >= 0;
+                const int pl = uplay(ocu[j]);
+                const int sa = snap_act(osb[j], v);
+                vv[j][0] = occ ? ohp[j] : 0;
+                vv[j][1] = occ ? ors[j] : 0;
+                vv[j][2] = (occ && pl >= 0) ? ((pl + v) % 2) + 1 : 0;
+                vv[j][3] = occ ? utyp(ocu[j]) + 1 : 0;
+                vv[j][4] = (occ && sa) ? sa - 1 : 0;
+                vv[j][5] = cs[j] == WALL ? 1 : 0;
+                vv[j][6] = (int)((mr >> (x0 + j)) & 1u);
+                vv[j][7] = (int)((tr >> (x0 + j)) & 1u);
+            }
+            const uint32_t base = (uint32_t)(v * D.C * HW + 4 * c4) * 4u;
+            if (SC1_POOBS) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) st4sc1(rs, base + (uint32_t)(k * HW) * 4u, vv[0][k], vv[1][k], vv[2][k], vv[3][k]);
+            } else {
+                int32_t* o = out + base / 4;
+#pragma unroll
+                for (int k = 0; k < 8; k++) st4<WT_POOBS>(o + k * HW, vv[0][k], vv[1][k], vv[2][k], vv[3][k]);
+            }
+        }
+        wsync();
+    }
     DEV void writeObsPO(int slot, int p, bool delta = false) {
         if ((W & 3) == 0 && W <= 32 && H <= 32 && nu <= 64 && U.maxSight <= 15) {
             writeObsPOFast(slot, p, delta);
@@ -3858,19 +4075,65 @@ DEV void helperLoop(const KDyn& D, uint8_t* smem, int g, int niter) {
     }
 }
 
+// Workgroup barrier for an LDS handoff: the release / acquire fences cover LDS only, so a wave does
+// not drain its outstanding global stores at every step (a __syncthreads fence would).
+DEV void ldsBarrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+DEV void drainStores() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // s_waitcnt vmcnt(0): this wave's stores done
+
+// The helper wave of a partially observable HELP launch (32x32 self-play multi-step rollouts, BASELINE
+// c5: two games per SIMD, the SIMD's vector issue half idle while the games run their dependent
+// chains).  The render of both views (writeObsPOFast2, a third of the step's instructions) reads the
+// state after the cycle and writes only the observation and the render record, so it moves to the
+// helper: at step k the game wave packs the render inputs (packPO, double-buffered by step parity)
+// and passes barrier B_k; the helper renders step k (renderPOPacked) while the game compacts, writes
+// masks and the next rows and runs step k + 1, and is back at B_{k+1} before the game packs over
+// the buffer it read.  The render record (sight rows, pending chunks) stays with the helper between
+// steps; the game keeps the per-slot part (poRecordSnaps, the lane registers) as before.  A step the
+// fast render cannot take (more than 64 units, sight > 15) the game renders itself after a second
+// barrier B'_k, which the helper reaches only after its stores of step k - 1 have completed (both
+// waves store to the same observation buffer), and the game drains its own stores before the next
+// barrier.  Header flags: bit 2 = helper renders, bit 3 = the game renders.  Layout: hdr [2][4]
+// words + the helper's view-0 sight rows [2][H] at KDyn.help_off; the packs [2][5][64] words and the
+// per-step occupant map (u8 per cell) in the game's `scell` area, which only the generic render uses.
+DEV void helperLoopPO(Game& G, uint32_t* hdr, int niter) {
+    uint32_t* const rows0 = hdr + 8;
+    uint8_t* const hcell = (uint8_t*)(G.scell + 2 * 5 * 64);
+    for (int k = 0; k < niter; k++) {
+        ldsBarrier();  // B_k
+        const uint32_t* ph = hdr + (k & 1) * 4;
+        const uint32_t f = uniu(ph[2]);
+        if (f & 4u) {
+            G.renderPOPacked(G.scell + (k & 1) * 5 * 64, ph, rows0, hcell, k == niter - 1);
+        } else if (f & 8u) {
+            drainStores();
+            ldsBarrier();  // B'_k: the game renders step k now
+        }
+    }
+}
+
 template <int MODE, int FIX, int FCAP = 0, bool FPO = false, bool MULTI = false, bool HELP = false>
 // stateArg and PS lead the argument list so that kernarg preloading (-amdgpu-kernarg-preload-count,
 // Makefile) hands them over in SGPRs: the first memory round (state block, unit-type table) issues
 // without waiting for a scalar load of the kernel arguments.
-__global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ stateArg, const KStatic* __restrict__ PS, KDyn D) {
+__global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* __restrict__ stateArg, const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
-    if (HELP && threadIdx.x >= 64) {
+    if (HELP && !FPO && threadIdx.x >= 64) {
         helperLoop(D, smem, (int)blockIdx.x, D.n_iter);
         return;
     }
     const KStatic& P = *PS;
     Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
            FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI);
+    // the partially observable helper wave: one packed render per step (helperLoopPO)
+    uint32_t* const poHelpHdr = (HELP && FPO) ? (uint32_t*)(smem + D.help_off) : nullptr;
+    if (HELP && FPO && threadIdx.x >= 64) {
+        helperLoopPO(G, poHelpHdr, D.n_iter);
+        return;
+    }
 #ifdef MRTS_ABLATE
     G.G_AB = g_ablate;
 #endif
@@ -3926,14 +4189,14 @@ __global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ s
 #ifdef MRTS_PHASE_TIMING
     int nu0_ = 0;
 #endif
-    uint32_t* const helpBuf = HELP ? (uint32_t*)(smem + D.help_off) : nullptr;  // helperLoop's layout
-    if (HELP) __syncthreads();  // A_0: the helper drew step 0's rows
+    uint32_t* const helpBuf = (HELP && !FPO) ? (uint32_t*)(smem + D.help_off) : nullptr;  // helperLoop's layout
+    if (HELP && !FPO) __syncthreads();  // A_0: the helper drew step 0's rows
     for (int it = 0; it < niter; it++) {
     if (it > 0) {
         G.nextStep();
         freshObs = true;
     }
-    if (HELP) G.helpRows = helpBuf + (it & 1) * 2 * 64;
+    if (HELP && !FPO) G.helpRows = helpBuf + (it & 1) * 2 * 64;
     G.lastIt = it == niter - 1;
     G.firstIt = it == 0;
     if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
@@ -3997,7 +4260,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ s
         const size_t rowStride = (size_t)G.HW * 7;
         // fused uniform policy: this step's rows go out first (fire-and-forget stores, nothing in the
         // launch reads them back: fetchRow draws the idle units' rows again)
-        if (D.uni_actions && !HELP) G.writeUniformRows(slot0, nslots);
+        if (D.uni_actions && !(HELP && !FPO)) G.writeUniformRows(slot0, nslots);
         if (MRTS_UNLIKELY(D.reward_need & RN_COUNTS))
             if (lane_id() < 2 * RC_N) G.rwc[lane_id()] = 0;
         if (MRTS_UNLIKELY(D.reward_need & RN_CLOSER)) G.closerBefore();
@@ -4090,6 +4353,8 @@ __global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ s
         PHASE(5);
     }
 
+    uint32_t poHelpFlags = 0;  // HELP && FPO: bit 2 = the helper renders this step, bit 3 = the game does
+    uint32_t poValid = 0;
     if (MODE != MODE_MASKS && D.obs && external) {
         if (G.po) {
             // persistent buffer: the views the previous write rendered for this game can be updated
@@ -4097,6 +4362,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ s
             const bool canDelta = MODE == MODE_STEP && !freshObs && D.obs_delta && D.po_prev && poDeltaShape(G.H, G.W) &&
                                   G.nu <= 64 && G.hget(H_NU) <= 64;
             const uint32_t valid = canDelta ? (uint32_t)G.hget(Game::HX_POVALID) : 0u;
+            poValid = valid;
             if (selfplay && G.poFast2()) {
                 if (freshObs) {  // PO views of the reset state (snapshot(p) touches only view p's bits)
                     if (G.snapBothOk()) {
@@ -4107,10 +4373,16 @@ __global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ s
                         G.snapshot(1);
                     }
                 }
+                if (HELP && FPO) {
+                    G.packPO(G.scell + (it & 1) * 5 * 64, poHelpHdr + (it & 1) * 4, valid & 3u);
+                    poHelpFlags = 4u;
+                } else
 #ifdef MRTS_ABLATE
                 if (!G.ab(AB_SKIP_OBS))
 #endif
                 G.writeObsPOFast2(slot0, valid & 3u);
+            } else if (HELP && FPO) {
+                poHelpFlags = 8u;  // rendered by this wave after B'_it (below)
             } else
             for (int i = 0; i < nslots; i++) {
                 const int p = selfplay ? i : side;
@@ -4132,7 +4404,19 @@ __global__ __launch_bounds__(HELP ? 128 : 64) void k_env(int32_t* __restrict__ s
 #endif
         }
     }
-    if (HELP) __syncthreads();  // A_{it+1}: step it's cells packed; the helper's rows of step it + 1 ready
+    if (HELP && !FPO) __syncthreads();  // A_{it+1}: step it's cells packed; the helper's rows of step it + 1 ready
+    if (HELP && FPO) {
+        if (poHelpFlags != 4u && G.lid() == 0) poHelpHdr[(it & 1) * 4 + 2] = poHelpFlags;
+        ldsBarrier();  // B_it: the helper takes step it's pack (helperLoopPO)
+        if (poHelpFlags == 8u) {
+            ldsBarrier();  // B'_it: the helper's earlier stores are done; it is idle this step
+            for (int p = 0; p < 2; p++) {
+                if (freshObs) G.snapshot(p);
+                G.writeObsPO(slot0 + p, p, ((poValid >> p) & 1u) != 0);
+            }
+            drainStores();  // before the helper renders step it + 1 into the same buffer
+        }
+    }
     PHASE(6);
     if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
     PHASE(7);
@@ -4598,7 +4882,13 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
                 hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true, true>), grid, dim3(128), (size_t)D2.help_off + 2048, stream,
                                    D.state, ds, D2);
             } else if (D.n_iter > 1 && is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true>), grid, block, lds, stream, D.state, ds, D);
-            else if (D.n_iter > 1 && is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
+            else if (D.n_iter > 1 && is(32, 320, true) && D.obs && !MRTS_NO_PO_HELPER) {
+                // c5's partially observable rollout: a helper wave per game renders the views (helperLoopPO)
+                KDyn D2 = D;
+                D2.help_off = (int32_t)((lds + 15) & ~(size_t)15);
+                hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true, true>), grid, dim3(128), (size_t)D2.help_off + 4 * (8 + 2 * 32),
+                                   stream, D.state, ds, D2);
+            } else if (D.n_iter > 1 && is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
             else if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
             else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, D.state, ds, D);
             else if (is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, D.state, ds, D);

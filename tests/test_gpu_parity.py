@@ -768,6 +768,67 @@ def test_multi_step_rollout_matches_single_launches(mp, n_sp, max_steps, po):
     B.close()
 
 
+def _crowded_32x32(tmp_path, per_player):
+    """BWDistantResources32x32 plus `per_player` extra Workers per player:
+    the map file is written by the test (the reference's XML layout, PhysicalGameState.java:700-726)."""
+    import re
+
+    src = open("maps/BWDistantResources32x32.xml").read()
+    terrain = re.search(r"<terrain>([01]+)</terrain>", src).group(1)
+    taken = {(int(x), int(y)) for x, y in re.findall(r'x="(\d+)" y="(\d+)"', src)}
+    free = [(x, y) for y in range(32) for x in range(32) if terrain[y * 32 + x] == "0" and (x, y) not in taken]
+    left = [c for c in free if c[0] < 12 and 8 <= c[1] < 24]
+    right = [c for c in free if c[0] >= 20 and 8 <= c[1] < 24]
+    extra, uid = [], 1000
+    for p, cells in ((0, left), (1, right)):
+        for x, y in cells[:per_player]:
+            extra.append(f'    <rts.units.Unit type="Worker" ID="{uid}" player="{p}" x="{x}" y="{y}" resources="0" '
+                         f'hitpoints="1" >\n    </rts.units.Unit>\n')
+            uid += 1
+    path = tmp_path / "crowded32x32.xml"
+    path.write_text(src.replace("  </units>", "".join(extra) + "  </units>"))
+    return str(path)
+
+
+def test_po_helper_wave_over_64_units(tmp_path):
+    """The partially observable multi-step launch renders through a helper wave (helperLoopPO) only while
+    the game's units fit one wave; a step with more than 64 units is rendered by the game wave itself
+    (after the second barrier) and the helper takes over again after the auto-reset.  The crowded map
+    starts at 60 units and the games produce past 64 (oracle: steps ~249-298 of 300): multi-step = one
+    launch per step, bit for bit, across both transitions."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mp = _crowded_32x32(tmp_path, 22)
+    n_sp = 16
+    mk = lambda: DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=9, partial_obs=True, max_units=256)  # noqa: E731
+    A, B = mk(), mk()
+    A.set_multi_step(False)
+    assert B.multi_step_capable
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+    assert int(B.dump_state(0)[4]) <= 64
+    names = ("obs", "reward", "done", "masks", "actions", "source")
+    k, high = 0, 0
+    for n in (1, 3, 40, 60, 60, 60, 60, 80, 60):
+        A.rollout_fused(SEED, k + 1, n)
+        B.rollout_fused(SEED, k + 1, n)
+        k += n
+        A.synchronize()
+        B.synchronize()
+        for name in names:
+            assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
+        for s in range(0, n_sp, 2):
+            d = B.dump_state(s)
+            high = max(high, int(d[4]))
+            assert np.array_equal(A.dump_state(s), d), f"state slot {s} after {k}"
+    assert high > 64, f"no game grew past 64 units (most {high})"
+    assert not A.error_flags().any() and not B.error_flags().any()
+    A.close()
+    B.close()
+
+
 @pytest.mark.parametrize("mp,n_sp,n_bot,rows,max_units", [
     ("maps/BWDistantResources32x32.xml", 8, 4, False, 256),
     ("maps/16x16/basesWorkers16x16.xml", 16, 4, False, 0),
