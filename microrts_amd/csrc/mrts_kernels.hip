@@ -451,6 +451,8 @@ struct Game {
     DEV void freshLane() {
         if (iter) asm volatile("" : "=v"(lidv) : "0"((int)threadIdx.x));
     }
+    // the helper wave of a HELP launch (threads 64..127) runs Game methods as lanes 0..63
+    DEV void helperLane() { asm volatile("" : "=v"(lidv) : "0"((int)threadIdx.x - 64)); }
     bool ixValid;
     bool anyMP;
     uint32_t lcu, lua;     // load(): lane l's unit core / assignment words (units 0..63) as loaded
@@ -2973,23 +2975,62 @@ struct Game {
     // Helper-wave launch, partially observable self-play (k_env HELP && FPO, BASELINE c5): the game
     // wave hands this step's render inputs to the helper wave instead of rendering (writeObsPOFast2's
     // unit pass reads, per unit slot < 64: the unit word, hp | resources, the snapshot byte, and the
-    // previous record's position / key / snapshot byte), and the helper renders while the game runs
-    // its compaction, masks, policy and the next step.  pk = [5][64] words, ph = [4] header words:
-    // unit count, the previous record's unit count, flags (bits 0-1 delta per view, bit 2 render).
-    DEV void packPO(uint32_t* pk, uint32_t* ph, uint32_t delta) {
+    // previous record's position / key / snapshot byte; the assignment type + 1 for the next step's
+    // snapshot, snapFromPack), and the helper renders while the game runs its compaction, masks,
+    // policy and the next step.  pk = [5][64] words, ph = [4] header words:
+    // unit count, the previous record's unit count, flags (bits 0-1 delta per view, `how`: bit 2 =
+    // render the pack, bit 3 = render the live state with writeObsPO, the game waiting).
+    DEV void packPO(uint32_t* pk, uint32_t* ph, uint32_t delta, uint32_t how) {
         const int l = lid();
         const bool live = l < nu;
         pk[l] = live ? uc[l] : 0u;
         pk[64 + l] = live ? ((uint32_t)(uint16_t)hp[l] | ((uint32_t)(uint16_t)res[l] << 16)) : 0u;
-        pk[128 + l] = (live ? (uint32_t)snap[l] : 0u) | ((lsnap & 0xFFu) << 8);
+        const uint32_t a = live ? ua[l] : 0u;
+        pk[128 + l] = (live ? (uint32_t)snap[l] : 0u) | ((lsnap & 0xFFu) << 8) |
+                      ((a & UA_PRESENT) ? (uint32_t)(ua_type(a) + 1) << 16 : 0u);
         pk[192 + l] = lcu;
         pk[256 + l] = lkey;
         if (l == 0) {
             ph[0] = (uint32_t)nu;
             ph[1] = (uint32_t)hget(H_NU);
-            ph[2] = (delta & 3u) | 4u;
+            ph[2] = (delta & 3u) | how;
         }
-        poLds = D.po_prev != nullptr;  // the helper keeps the record's LDS copies, as writeObsPOFast2 does
+        // how = 4: the helper keeps the record's LDS copies, as writeObsPOFast2 does; 8: the general
+        // render stores it globally only, and nextStep re-reads it
+        poLds = how == 4u && D.po_prev != nullptr;
+    }
+    // snapshotBoth of the NEXT step, by the helper wave from step k's pack: the state the next step
+    // starts from is the packed one after the end-of-step compaction (dead units leave, the rest keep
+    // their order and positions, assignments and liveness do not change in between), so each live
+    // unit paints its sight disk into its player's rows and takes the membership bits and view 0's
+    // assignment bits at its compacted index.  hsnap[slot] = the snapshot byte.
+    DEV void snapFromPack(const uint32_t* pk, const uint32_t* ph, uint32_t* rows, uint8_t* hsnap) {
+        const int l = (int)threadIdx.x - 64;
+        const int nuP = (int)uniu(ph[0]);
+        uint32_t* const r0 = rows;
+        uint32_t* const r1 = rows + H;
+        if (l < 2 * H) rows[l] = 0;
+        const uint32_t cu = l < nuP ? pk[l] : UC_DEAD;
+        const bool live = !(cu & UC_DEAD);
+        const int own = uplay(cu);
+        const uint32_t at = (pk[128 + l] >> 16) & 15u;  // assignment type + 1 (0 = none)
+        wsync();
+        paintDisks2(live && own == 0, r0, live && own == 1, r1, cu);
+        wsync();
+        const uint64_t m = ballot(live);
+        if (live) {
+            const int x = ux(cu), y = uy(cu);
+            const bool in0 = (r0[y] >> x) & 1u, in1 = (r1[y] >> x) & 1u;
+            hsnap[lanes_below(m)] = (uint8_t)((in0 ? 1u : 0u) | (in1 ? 2u : 0u) | (in0 ? at << 2 : 0u));
+        }
+        wsync();
+    }
+    // the game wave's side: the helper's snapshot bytes instead of snapshotBoth (same bytes, same header)
+    DEV void takeSnap(const uint8_t* hsnap) {
+        const int l = lid();
+        if (l < nu) snap[l] = hsnap[l];
+        hset(HX_SNAP + 0, seq);
+        wsync();
     }
     // writeObsPOFast2 as run by the helper wave (lane l = threadIdx.x - 64) from a packed step (packPO):
     // the same passes and stores.  What the game wave's live LDS state gave it comes from the pack:
@@ -4093,24 +4134,44 @@ DEV void drainStores() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // s_waitcnt vmc
 // masks and the next rows and runs step k + 1, and is back at B_{k+1} before the game packs over
 // the buffer it read.  The render record (sight rows, pending chunks) stays with the helper between
 // steps; the game keeps the per-slot part (poRecordSnaps, the lane registers) as before.  A step the
-// fast render cannot take (more than 64 units, sight > 15) the game renders itself after a second
-// barrier B'_k, which the helper reaches only after its stores of step k - 1 have completed (both
-// waves store to the same observation buffer), and the game drains its own stores before the next
-// barrier.  Header flags: bit 2 = helper renders, bit 3 = the game renders.  Layout: hdr [2][4]
-// words + the helper's view-0 sight rows [2][H] at KDyn.help_off; the packs [2][5][64] words and the
-// per-step occupant map (u8 per cell) in the game's `scell` area, which only the generic render uses.
+// fast render cannot take (more than 64 units, sight > 15) the helper renders with the general
+// writeObsPO straight from the game's live state while the game waits at a second barrier B'_k
+// (the helper's stores, the global render record included, complete before it: the game re-reads
+// that record in nextStep).  Only the helper ever writes the observation buffer, in step order; the
+// game wave carries no render code.  The next step's snapshotBoth comes from the same pack: after
+// B_k the helper first computes it (snapFromPack) and passes S_k, where the game, back from its
+// compaction, masks and policy, takes the bytes (takeSnap), then renders step k.  Header flags: bit 2
+// = packed render, bit 3 = general render from the live state.  Layout: hdr [2][4] words, the
+// helper's view-0 sight rows [2][H] (the snapshot's rows before the render) and the snapshot bytes
+// [64] at KDyn.help_off; the packs [2][5][64] words and the per-step occupant map (u8 per cell) in the
+// game's `scell` area, which only the general render uses.
 DEV void helperLoopPO(Game& G, uint32_t* hdr, int niter) {
     uint32_t* const rows0 = hdr + 8;
+    uint8_t* const hsnap = (uint8_t*)(rows0 + 2 * G.H);
     uint8_t* const hcell = (uint8_t*)(G.scell + 2 * 5 * 64);
+    G.helperLane();
+    const int l = G.lid();
     for (int k = 0; k < niter; k++) {
         ldsBarrier();  // B_k
         const uint32_t* ph = hdr + (k & 1) * 4;
         const uint32_t f = uniu(ph[2]);
+        const uint32_t* pk = G.scell + (k & 1) * 5 * 64;
         if (f & 4u) {
-            G.renderPOPacked(G.scell + (k & 1) * 5 * 64, ph, rows0, hcell, k == niter - 1);
+            if (k + 1 < niter) {
+                G.snapFromPack(pk, ph, rows0, hsnap);
+                ldsBarrier();  // S_k: the next step's snapshot bytes are ready
+            }
+            G.renderPOPacked(pk, ph, rows0, hcell, k == niter - 1);
         } else if (f & 8u) {
+            // the game's live state, as its own writeObsPO call would see it (the general render
+            // overwrites `scell`, so the pack's record words are taken first)
+            G.nu = (int)uniu(ph[0]);
+            G.lcu = pk[192 + l];
+            G.lkey = pk[256 + l];
+            G.lsnap = (pk[128 + l] >> 8) & 0xFFu;
+            for (int p = 0; p < 2; p++) G.writeObsPO(2 * G.g + p, p, ((f >> p) & 1u) != 0);
             drainStores();
-            ldsBarrier();  // B'_k: the game renders step k now
+            ldsBarrier();  // B'_k: the game continues (compaction)
         }
     }
 }
@@ -4190,6 +4251,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
     int nu0_ = 0;
 #endif
     uint32_t* const helpBuf = (HELP && !FPO) ? (uint32_t*)(smem + D.help_off) : nullptr;  // helperLoop's layout
+    bool poPacked = false;  // HELP && FPO: the previous iteration handed its render to the helper (packPO, flag 4)
     if (HELP && !FPO) __syncthreads();  // A_0: the helper drew step 0's rows
     for (int it = 0; it < niter; it++) {
     if (it > 0) {
@@ -4199,6 +4261,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
     if (HELP && !FPO) G.helpRows = helpBuf + (it & 1) * 2 * 64;
     G.lastIt = it == niter - 1;
     G.firstIt = it == 0;
+    bool snapTaken = false;
     if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
@@ -4221,6 +4284,11 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
     if (it == 0) nu0_ = G.nu;
 #endif
     if (G.po) G.clearSnap();
+    if (HELP && FPO && poPacked) {  // S_{it-1}: the helper's snapshot of this step (snapFromPack)
+        ldsBarrier();
+        G.takeSnap((const uint8_t*)(poHelpHdr + 8 + 2 * G.H));
+        snapTaken = true;
+    }
     PHASE(0);
 
     if (MODE == MODE_PLAYOUT) {
@@ -4290,7 +4358,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
             const bool snapBoth = G.po && G.snapBothOk();
             for (int p = 0; p < 2; p++) {
                 if (snapBoth) {
-                    if (p == 0) G.snapshotBoth();
+                    if (p == 0 && !snapTaken) G.snapshotBoth();
                     else G.snapshotActions(1);
                 } else if (G.po) {
                     G.snapshot(p);
@@ -4354,7 +4422,6 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
     }
 
     uint32_t poHelpFlags = 0;  // HELP && FPO: bit 2 = the helper renders this step, bit 3 = the game does
-    uint32_t poValid = 0;
     if (MODE != MODE_MASKS && D.obs && external) {
         if (G.po) {
             // persistent buffer: the views the previous write rendered for this game can be updated
@@ -4362,7 +4429,6 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
             const bool canDelta = MODE == MODE_STEP && !freshObs && D.obs_delta && D.po_prev && poDeltaShape(G.H, G.W) &&
                                   G.nu <= 64 && G.hget(H_NU) <= 64;
             const uint32_t valid = canDelta ? (uint32_t)G.hget(Game::HX_POVALID) : 0u;
-            poValid = valid;
             if (selfplay && G.poFast2()) {
                 if (freshObs) {  // PO views of the reset state (snapshot(p) touches only view p's bits)
                     if (G.snapBothOk()) {
@@ -4374,7 +4440,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
                     }
                 }
                 if (HELP && FPO) {
-                    G.packPO(G.scell + (it & 1) * 5 * 64, poHelpHdr + (it & 1) * 4, valid & 3u);
+                    G.packPO(G.scell + (it & 1) * 5 * 64, poHelpHdr + (it & 1) * 4, valid & 3u, 4u);
                     poHelpFlags = 4u;
                 } else
 #ifdef MRTS_ABLATE
@@ -4382,7 +4448,13 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
 #endif
                 G.writeObsPOFast2(slot0, valid & 3u);
             } else if (HELP && FPO) {
-                poHelpFlags = 8u;  // rendered by this wave after B'_it (below)
+                // the helper renders from the live state while this wave waits at B'_it (below)
+                if (freshObs) {
+                    G.snapshot(0);
+                    G.snapshot(1);
+                }
+                G.packPO(G.scell + (it & 1) * 5 * 64, poHelpHdr + (it & 1) * 4, valid & 3u, 8u);
+                poHelpFlags = 8u;
             } else
             for (int i = 0; i < nslots; i++) {
                 const int p = selfplay ? i : side;
@@ -4406,16 +4478,10 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
     }
     if (HELP && !FPO) __syncthreads();  // A_{it+1}: step it's cells packed; the helper's rows of step it + 1 ready
     if (HELP && FPO) {
-        if (poHelpFlags != 4u && G.lid() == 0) poHelpHdr[(it & 1) * 4 + 2] = poHelpFlags;
+        if (poHelpFlags == 0u && G.lid() == 0) poHelpHdr[(it & 1) * 4 + 2] = 0u;
         ldsBarrier();  // B_it: the helper takes step it's pack (helperLoopPO)
-        if (poHelpFlags == 8u) {
-            ldsBarrier();  // B'_it: the helper's earlier stores are done; it is idle this step
-            for (int p = 0; p < 2; p++) {
-                if (freshObs) G.snapshot(p);
-                G.writeObsPO(slot0 + p, p, ((poValid >> p) & 1u) != 0);
-            }
-            drainStores();  // before the helper renders step it + 1 into the same buffer
-        }
+        if (poHelpFlags == 8u) ldsBarrier();  // B'_it: the helper rendered from this wave's live state
+        poPacked = poHelpFlags == 4u;
     }
     PHASE(6);
     if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
@@ -4886,7 +4952,7 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
                 // c5's partially observable rollout: a helper wave per game renders the views (helperLoopPO)
                 KDyn D2 = D;
                 D2.help_off = (int32_t)((lds + 15) & ~(size_t)15);
-                hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true, true>), grid, dim3(128), (size_t)D2.help_off + 4 * (8 + 2 * 32),
+                hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true, true>), grid, dim3(128), (size_t)D2.help_off + 4 * (8 + 2 * 32) + 64,
                                    stream, D.state, ds, D2);
             } else if (D.n_iter > 1 && is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
             else if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
