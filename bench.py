@@ -474,23 +474,17 @@ def main():
     multi = native and ((fused and env.fused_multi_step) or (uniform and mode["uni_fused"] and env.multi_step_capable))
     roll_ev = (_FenceFreeEvent(), _FenceFreeEvent()) if multi and event_kind.startswith("hipEvent") else None
     run_steps(a.burnin, a.warmup)  # the W untimed warmup steps, immediately before the window
+    if roll_ev is not None:  # the library records them around the window's launch (mrts_set_rollout_events)
+        env.set_rollout_events(roll_ev[0].h, roll_ev[1].h)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(env.device)
     env.synchronize()
     t0 = time.perf_counter()
     if native and uniform:
-        if roll_ev is not None:
-            roll_ev[0].record(stream)
         env.rollout_uniform(SEED, base, a.steps, fused=mode["uni_fused"])
-        if roll_ev is not None:
-            roll_ev[1].record(stream)
     elif native:
-        if roll_ev is not None:
-            roll_ev[0].record(stream)
         env.rollout_fused(SEED, base + 1, a.steps)
-        if roll_ev is not None:
-            roll_ev[1].record(stream)
     elif graph is not None:
         graph.replay()
     else:
@@ -685,7 +679,8 @@ def main():
                        "timed window)" if uniform
                        else "fused into the step kernel (mrts_step_fused_dev)" if fused
                        else "separate masked-uniform policy kernel before each step (mrts_policy_dev)"),
-            "kernel_timing": (f"{event_kind} around the multi-step launch in the timed window, / K" if launch_ms is not None
+            "kernel_timing": (f"{event_kind} recorded on the launch stream right before / after the multi-step launch "
+                              "in the timed window (by the library: mrts_set_rollout_events), / K" if launch_ms is not None
                               else f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
                               if (native or graph is not None) else f"{event_kind} around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (

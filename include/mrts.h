@@ -176,6 +176,12 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
                            uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
                            int32_t n_steps, void* stream);
 #define MRTS_MAX_ITER 1024
+/* Timing hook (no Java counterpart): the NEXT mrts_rollout_fused_dev / mrts_rollout_uniform_dev call
+ * records `start` (a hipEvent_t) on its stream right before its first kernel launch and `end` right
+ * after its last, so that a benchmark's events bracket exactly the rollout's kernels without two extra
+ * host calls in its timed window.  One shot: the handle forgets both events when that call begins.
+ * Either may be NULL. */
+int mrts_set_rollout_events(mrts_env* env, void* start, void* end);
 /* Every later observation write of this handle (any step / reset call with an observation buffer)
  * also writes the planes as int16 into d_obs16 [n_slots][C][H][W] (every value fits: hp, unit
  * types, action types, 0..2 owner, terrain, resources <= 32767 by map validation) — the compact

@@ -499,6 +499,8 @@ struct mrts_env {
     const int32_t* lastPolicyActions = nullptr;
     bool polValid = false;
     const int32_t* fusedActions = nullptr;  // buffer the last fused-policy step wrote (delta base), or null
+    // mrts_set_rollout_events: HIP events the next native rollout records around its launches (one shot)
+    hipEvent_t evStart = nullptr, evEnd = nullptr;
     mutable uint32_t launchStamp = 0;       // KDyn.fwd_stamp of the last k_env launch (never 0)
     int polParity = 0;
     // the kernels store observations and mask chunks as 16-byte vectors
@@ -913,16 +915,43 @@ int mrts_step_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_play
     }
 }
 
+namespace {
+// the one-shot rollout events (mrts_set_rollout_events): recorded on the rollout's stream right
+// before its first launch / right after its last, then forgotten
+struct RolloutEvents {
+    mrts_env* env;
+    hipStream_t s;
+    hipEvent_t end = nullptr;
+    RolloutEvents(mrts_env* e, void* stream) : env(e), s(pickStream(e, stream)) {
+        if (env->evStart) HIPCHK(hipEventRecord(env->evStart, s));
+        end = env->evEnd;
+        env->evStart = env->evEnd = nullptr;
+    }
+    void done() {
+        if (end) HIPCHK(hipEventRecord(end, s));
+    }
+};
+}  // namespace
+
+int mrts_set_rollout_events(mrts_env* env, void* start, void* end) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    env->evStart = (hipEvent_t)start;
+    env->evEnd = (hipEvent_t)end;
+    return 0;
+}
+
 int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward,
                            uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
                            int32_t n_steps, void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
+        RolloutEvents ev(env, stream);
         for (int32_t k = 0; k < n_steps;) {
             const int32_t n = std::min<int32_t>(n_steps - k, env->multiStep ? MRTS_MAX_ITER : 1);
             k += stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
                            first_next_step + (uint32_t)k, n, stream);
         }
+        ev.done();
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1085,11 +1114,13 @@ int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     if (fused) {
         try {
+            RolloutEvents ev(env, stream);
             for (int32_t k = 0; k < n_steps;) {
                 const int32_t n = std::min<int32_t>(n_steps - k, env->multiStep ? MRTS_MAX_ITER : 1);
                 k += stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, n,
                                  stream);
             }
+            ev.done();
             return 0;
         } catch (const Fail& f) {
             return fail(f);

@@ -390,6 +390,7 @@ class DeviceVecEnv:
         self._policy_out, self._policy_version = None, -1
         _lib.check(h.L.mrts_set_obs_delta(h.h, int(bool(obs_delta))))
         self._obs_version = -1
+        self._ptr_cache = None
         torch.cuda.synchronize(dev)
 
     @staticmethod
@@ -397,8 +398,24 @@ class DeviceVecEnv:
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
     def _s(self, stream):
-        s = stream if stream is not None else self.torch.cuda.current_stream(self.device)
-        return ctypes.c_void_p(s.cuda_stream)
+        if stream is None:  # torch's current stream, without building a Stream object per call
+            return ctypes.c_void_p(self.torch._C._cuda_getCurrentRawStream(self.device.index))
+        return ctypes.c_void_p(stream.cuda_stream)
+
+    def _bufs(self):
+        """actions, players, obs, reward, done, masks as ctypes pointers, cached while the same tensor
+        objects stay attached (the rollout calls' per-call host cost)."""
+        key = (self.actions, self.players, self.obs, self.reward, self.done, self.masks)
+        c = self._ptr_cache
+        if c is None or any(a is not b for a, b in zip(c[0], key)):
+            c = self._ptr_cache = (key, tuple(self._p(t) for t in key))
+        return c[1]
+
+    def set_rollout_events(self, start, end):
+        """The next rollout_fused / rollout_uniform call records these hipEvent_t handles (ints or
+        ctypes pointers, None = skip) right before its first and after its last kernel launch
+        (mrts_set_rollout_events): a benchmark's events bracket exactly the rollout's kernels."""
+        _lib.check(self._h.L.mrts_set_rollout_events(self._h.h, start, end))
 
     def _obs_guard(self):
         """Before a call that writes `obs`: a torch in-place write since our last one voids the delta base."""
@@ -450,9 +467,9 @@ class DeviceVecEnv:
         step_uniform launch per step (same results) instead of a policy launch + a step launch."""
         h = self._h
         self._obs_guard()
-        _lib.check(h.L.mrts_rollout_uniform_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
-                                                self._p(self.reward), self._p(self.done), seed, first_step, n_steps,
-                                                1 if fused else 0, self._s(stream)))
+        a, pl, o, r, d, _ = self._bufs()
+        _lib.check(h.L.mrts_rollout_uniform_dev(h.h, a, pl, o, r, d, seed, first_step, n_steps, 1 if fused else 0,
+                                                self._s(stream)))
         self._obs_written()
 
     def step_fused(self, seed, next_step, stream=None):
@@ -505,9 +522,9 @@ class DeviceVecEnv:
         if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
             _lib.check(h.L.mrts_policy_invalidate(h.h))
         self._obs_guard()
-        _lib.check(h.L.mrts_rollout_fused_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
-                                              self._p(self.reward), self._p(self.done), self._p(self.masks),
-                                              self.mask_player, seed, first_next_step, n_steps, self._s(stream)))
+        a, pl, o, r, d, m = self._bufs()
+        _lib.check(h.L.mrts_rollout_fused_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, first_next_step, n_steps,
+                                              self._s(stream)))
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 

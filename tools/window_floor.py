@@ -5,7 +5,8 @@ synchronize, t1), c3 workload after a 1000-step burn-in, medians of 15 windows:
   tiny_kernel     one 1-element torch fill + synchronize — launch + completion floor
   rollout0        rollout_fused(n_steps=0): the Python wrapper + ctypes call, no launch
   rollout_K       rollout_fused(K) for K in 1, 20, 200 (one multi-step launch)
-  rollout_K_ev    the same bracketed by two fence-free events (bench.py's roll_ev)
+  rollout_K_ev    the same bracketed by two fence-free events recorded from Python
+  rollout_libev   the events recorded by the library around its launch (bench.py's form since round 3)
   raw_K           the same C call through prebuilt ctypes arguments (no wrapper checks)
 Prints one JSON line per form."""
 import ctypes
@@ -27,6 +28,10 @@ def main():
 
     SEED = 0x5EEDC0DE
     E = 4096
+    if os.environ.get("SPIN") == "1":  # host waits spin instead of sleeping (hipDeviceScheduleSpin)
+        hip = bench._FenceFreeEvent.runtime()
+        assert hip.hipSetDevice(0) == 0 and hip.hipSetDeviceFlags(1) == 0
+        print(json.dumps({"schedule": "spin"}), flush=True)
     env = DeviceVecEnv(2 * E, 0, 2000, ["maps/16x16/basesWorkers16x16.xml"] * (2 * E), seed=SEED)
     env.reset()
     env.random_policy(SEED, 0)
@@ -86,9 +91,25 @@ def main():
             k[0] += K
         return f
 
+    def roll_libev(K):  # bench.py's form: the library records the events (mrts_set_rollout_events)
+        def f():
+            env.rollout_fused(SEED, k[0] + 1, K)
+            k[0] += K
+        return f
+
+    def report_libev(name, K, n=15):
+        ts = []
+        for _ in range(n):
+            env.set_rollout_events(ev[0].h, ev[1].h)
+            ts.append(window(roll_libev(K)))
+        d = {"form": name, "K": K, "median_us": float(np.median(ts)) * 1e6, "min_us": float(np.min(ts)) * 1e6}
+        d["us_per_step"] = d["median_us"] / K
+        print(json.dumps(d), flush=True)
+
     for K in (1, 20, 200):
         report("rollout", roll(K), K=K)
         report("rollout_ev", roll_ev(K), K=K)
+        report_libev("rollout_libev", K)
         report("raw", raw(K), K=K)
     assert not env.error_flags().any()
     env.close()
