@@ -220,8 +220,10 @@ def cpu_baseline_c1(map_path, runs=5, steps=200_000, burnin=1000):
 
 def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, dist):
     """K steps with the observation all-gather after every step (xg["buf"] makes one_step run it),
-    one step launch per step, the K steps and their collectives captured in one hipGraph; the
-    barrier + synchronize bracket and max over ranks of the headline window.  -> the JSON block."""
+    one step launch per step, enqueued eagerly; the barrier + synchronize bracket and max over ranks of
+    the headline window.  -> the JSON block.  (Round 3: no hipGraph capture of the collectives any
+    more — a capture that fails leaves RCCL work events recorded in a capturing stream, and the
+    process group's watchdog thread then aborts the whole process.)"""
     gb = mdist.ObservationGather(env.obs.shape, env.device, mode="allgather")
     xg["buf"] = gb
     try:
@@ -229,21 +231,12 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
             one_step(base + k)
         gb.wait()
         torch.cuda.synchronize(env.device)
-        gb.fired = [False, False]
-        graph = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream(env.device)
-        cap.wait_stream(torch.cuda.current_stream(env.device))
-        with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
-            for k in range(a.steps):
-                one_step(base + 3 + k)
-            gb.wait()  # the comm stream joins the capture: the last exchange is in the graph
-        torch.cuda.synchronize(env.device)
-        graph.replay()  # warm replay (first replays carry one-off costs)
-        torch.cuda.synchronize(env.device)
         dist.barrier()
         torch.cuda.synchronize(env.device)
         t0 = time.perf_counter()
-        graph.replay()
+        for k in range(a.steps):
+            one_step(base + 3 + k)
+        gb.wait()  # the last step's exchange belongs to the window
         torch.cuda.synchronize(env.device)
         dist.barrier()
         t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
@@ -257,8 +250,7 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
                       "overlapping the next step; " + ("int16 written by the step kernel" if not a.po else
                                                        "narrowing copy (partially observable planes)"),
         "payload_bytes_per_rank": env.obs.numel() * 2,  # int16 observation of one rank's slots, per step
-        "launch": "one step launch per step (a per-step consumer cannot use multi-step launches), the K steps and "
-                  "their collectives in one hipGraph",
+        "launch": "one step launch per step (a per-step consumer cannot use multi-step launches), enqueued eagerly",
     }
 
 

@@ -478,6 +478,7 @@ struct mrts_env {
     int multiStep = 1;  // mrts_rollout_fused_dev may run several steps per launch (mrts_set_multi_step)
     const int32_t* lastObsPtr = nullptr;
     int32_t* d_poPrev = nullptr;
+    uint32_t* d_prioTab = nullptr;  // multi-step launches: per-SIMD issue-rank table (KDyn.prio_tab)
     int poWords = 0;
     // delta mask writes: which buffer / player the last mask write went to
     int maskDelta = 0;
@@ -570,6 +571,7 @@ struct mrts_env {
         for (int j = 0; j < hstatic.n_rewards; j++) D.reward_kinds4 |= (uint32_t)hstatic.reward_kinds[j] << (4 * j);
         if (++launchStamp == 0) ++launchStamp;  // H_FWD = 0 means "no forwarded rows"
         D.fwd_stamp = launchStamp;
+        D.prio_tab = D.n_iter > 1 ? d_prioTab : nullptr;
         return launchEnv(mode, hstatic, d_static, D, s);
     }
     int gameOfSlot(int slot, int* player) const {
@@ -792,6 +794,10 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         env->buildStatic();
         HIPCHK(hipMalloc(&env->d_static, sizeof(KStatic)));
         HIPCHK(hipMemcpy(env->d_static, &env->hstatic, sizeof(KStatic), hipMemcpyHostToDevice));
+        if (envIterable(env->hstatic)) {  // entries carry a launch stamp: stale ones are ignored, zero = empty
+            HIPCHK(hipMalloc(&env->d_prioTab, (size_t)PRIO_KEYS * 16 * 4));
+            HIPCHK(hipMemset(env->d_prioTab, 0, (size_t)PRIO_KEYS * 16 * 4));
+        }
         // initial state = reset (the Java constructor loads the maps)
         KDyn D;
         std::memset(&D, 0, sizeof(D));
@@ -1434,6 +1440,7 @@ void mrts_destroy(mrts_env* env) {
     if (env->stream) (void)hipStreamSynchronize(env->stream);
     (void)hipFree(env->d_static);
     (void)hipFree(env->d_poPrev);
+    (void)hipFree(env->d_prioTab);
     (void)hipFree(env->d_state);
     (void)hipFree(env->d_polPrev);
     (void)hipFree(env->d_pairs);

@@ -164,7 +164,12 @@ struct KDyn {
     // helper-wave multi-step launches (8x8 fused uniform rollouts, BASELINE c2): byte offset of the
     // LDS handoff area (rows of the next step, packed observation cells) after the game's own LDS
     int32_t help_off;
+    // multi-step launches: per-SIMD issue-rank table [PRIO_KEYS][16] (mrts_kernels.hip, simdRank):
+    // each wave posts its game's remaining-work estimate and takes its s_setprio from its rank among
+    // the waves sharing its SIMD; null = the unit-count thresholds only
+    uint32_t* prio_tab;
 };
+constexpr int PRIO_KEYS = 8 * 8 * 2 * 16 * 4;  // XCC x SE x SH x CU x SIMD (HW_ID / XCC_ID fields)
 // PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);
 // snapshot bytes of the unit slots (after the end-of-step compaction); per view p the sight rows
 // (own, other) the render used; per view the 4-cell chunks of rendered units that died (they leave

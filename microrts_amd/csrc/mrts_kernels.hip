@@ -133,6 +133,15 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_MULTI_NOPRIO
 #define MRTS_MULTI_NOPRIO 0
 #endif
+// 0: multi-step launches take the unit-count thresholds only, not the rank among the SIMD's waves (A/B)
+#ifndef MRTS_SIMD_RANK
+#define MRTS_SIMD_RANK 1
+#endif
+// 1: the rank also on c5's partially observable kernel (measured -4 %: its games outrank their own
+// helper waves, which then reach the handoff barriers late; round3q)
+#ifndef MRTS_SIMD_RANK_PO
+#define MRTS_SIMD_RANK_PO 0
+#endif
 // 1: partially observable multi-step launches without the render helper wave (A/B builds)
 #ifndef MRTS_NO_PO_HELPER
 #define MRTS_NO_PO_HELPER 0
@@ -4116,6 +4125,47 @@ DEV void helperLoop(const KDyn& D, uint8_t* smem, int g, int niter) {
     }
 }
 
+// Issue priority by rank among the waves that share a SIMD (multi-step launches, KDyn.prio_tab).  A
+// launch ends with its slowest SIMD, and a SIMD with its last game: the four games of a SIMD finish
+// far apart (round 3 span build: 1.6-2.9 ms in a 200-step c3 launch), while the heaviest game alone
+// needs ~2.2 ms and the SIMD's whole issue work ~2.0 ms.  So the game with the most remaining work
+// (longest processing time first) should issue first, the next one second, and so on — a ranking
+// the absolute unit-count thresholds only approximate.  Each wave posts, once per step, its game's
+// remaining-work estimate (units + own idle units, times the steps left in the launch) with the
+// launch stamp into its SIMD's row of the table (key from HW_ID / XCC_ID, slot = wave id), reads the
+// row back, and at its next step sets s_setprio 3 - rank.  The reads may be a step old or see a
+// neighbour's entry mid-update: priority never changes what a game computes, only when it issues.
+struct SimdRank {
+    uint32_t* row;  // this SIMD's 16 entries (stamp << 24 | estimate; 0 = free)
+    int me;         // this wave's slot in the row
+    uint32_t tag;   // this launch's stamp byte, never 0
+    uint32_t seen;  // lane l < 16: entry l as last read
+};
+DEV SimdRank simdRankInit(uint32_t* tab, uint32_t stamp) {
+    const uint32_t hw = (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));        // HW_ID
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)) & 7u;  // XCC_ID
+    const uint32_t simd = (hw >> 4) & 3u, cu = (hw >> 8) & 15u, sh = (hw >> 12) & 1u, se = (hw >> 13) & 7u;
+    const uint32_t key = (((xcc * 8u + se) * 2u + sh) * 16u + cu) * 4u + simd;
+    SimdRank r;
+    r.row = tab + (size_t)key * 16;
+    r.me = (int)(hw & 15u);
+    r.tag = (stamp & 0x7Fu) | 0x80u;
+    r.seen = 0;
+    return r;
+}
+// rank of estimate `est` among the entries read last time (ties: lower slot first), then post `est`
+// and read the row again for the next call
+DEV int simdRankStep(SimdRank& r, uint32_t est) {
+    const int l = lane_id();
+    est = est > 0xFFFFFFu ? 0xFFFFFFu : est;
+    const uint32_t e = r.seen, ee = e & 0xFFFFFFu;
+    const bool higher = l < 16 && l != r.me && (e >> 24) == r.tag && (ee > est || (ee == est && l < r.me));
+    const int rank = __popcll(ballot(higher));
+    if (l == 0) r.row[r.me] = (r.tag << 24) | est;
+    r.seen = l < 16 ? __builtin_nontemporal_load(r.row + l) : 0u;
+    return rank;
+}
+
 // Workgroup barrier for an LDS handoff: the release / acquire fences cover LDS only, so a wave does
 // not drain its outstanding global stores at every step (a __syncthreads fence would).
 DEV void ldsBarrier() {
@@ -4252,6 +4302,11 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
 #endif
     uint32_t* const helpBuf = (HELP && !FPO) ? (uint32_t*)(smem + D.help_off) : nullptr;  // helperLoop's layout
     bool poPacked = false;  // HELP && FPO: the previous iteration handed its render to the helper (packPO, flag 4)
+    // c3 (four games per SIMD) and c5 (two games + their helper waves, which keep priority 0)
+    const bool ranked = MULTI && MRTS_SIMD_RANK && (FIX == 16 || (FIX == 32 && FPO && MRTS_SIMD_RANK_PO)) &&
+                        D.prio_tab != nullptr && niter > 1;
+    SimdRank srank;
+    if (ranked) srank = simdRankInit(D.prio_tab, D.fwd_stamp);
     if (HELP && !FPO) __syncthreads();  // A_0: the helper drew step 0's rows
     for (int it = 0; it < niter; it++) {
     if (it > 0) {
@@ -4271,8 +4326,17 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
             // mask / policy work grows with the idle ones)
             const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
             q = wq >= MRTS_PRIO_T3 ? 3 : wq >= MRTS_PRIO_T2 ? 2 : wq >= MRTS_PRIO_T1 ? 1 : 0;
+            if (ranked) {  // from the second step on: the rank among the SIMD's waves by remaining work
+                const int rk = simdRankStep(srank, (uint32_t)wq * (uint32_t)(niter - it));
+                if (it > 0) q = 3 - (rk < 3 ? rk : 3);
+            }
         } else {  // units (the idle count's ballot costs the latency-bound one-game-per-SIMD c2 4.5 %)
             q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
+            if (ranked) {
+                const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
+                const int rk = simdRankStep(srank, (uint32_t)wq * (uint32_t)(niter - it));
+                if (it > 0) q = 3 - (rk < 3 ? rk : 3);
+            }
         }
         if (q == 0) {
             if (it > 0) __builtin_amdgcn_s_setprio(0);
@@ -4512,6 +4576,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
         G.poRecordSnaps(selfplay ? 3u : (1u << side));
     }
     }  // iterations
+    if (ranked && lane_id() == 0) srank.row[srank.me] = 0u;  // this game no longer competes on its SIMD
     if (MODE != MODE_MASKS) {
         wsync();
         G.store();

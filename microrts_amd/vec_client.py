@@ -480,9 +480,8 @@ class DeviceVecEnv:
         if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
             _lib.check(h.L.mrts_policy_invalidate(h.h))  # written by someone else since
         self._obs_guard()
-        _lib.check(h.L.mrts_step_fused_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
-                                           self._p(self.reward), self._p(self.done), self._p(self.masks), self.mask_player,
-                                           seed, next_step, self._s(stream)))
+        a, pl, o, r, d, m = self._bufs()
+        _lib.check(h.L.mrts_step_fused_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, next_step, self._s(stream)))
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 

@@ -52,6 +52,8 @@ for rep in range(3):
     simd_last = np.zeros(len(uniq))
     np.maximum.at(simd_last, inv, end)
     simd_units = np.bincount(inv, weights=nu_end)
+    if os.environ.get("DUMP"):  # raw per-game arrays for offline analysis
+        np.savez(f"{os.environ['DUMP']}_E{E}_K{K}_rep{rep}.npz", end=end, dur=dur, nu_end=nu_end, key=key)
     print(json.dumps({"K": K, "rep": rep, "launch_us": round(float(end.max()), 1),
                       "per_step_us": round(float(end.max()) / K, 3),
                       "game_end_us": {"min": round(float(end.min()), 1), "mean": round(float(end.mean()), 1),
