@@ -142,6 +142,9 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SIMD_RANK_PO
 #define MRTS_SIMD_RANK_PO 0
 #endif
+#ifndef MRTS_HELPER_PRIO
+#define MRTS_HELPER_PRIO 0
+#endif
 // 1: partially observable multi-step launches without the render helper wave (A/B builds)
 #ifndef MRTS_NO_PO_HELPER
 #define MRTS_NO_PO_HELPER 0
@@ -4201,6 +4204,7 @@ DEV void helperLoopPO(Game& G, uint32_t* hdr, int niter) {
     uint8_t* const hcell = (uint8_t*)(G.scell + 2 * 5 * 64);
     G.helperLane();
     const int l = G.lid();
+    if (MRTS_HELPER_PRIO) __builtin_amdgcn_s_setprio(3);  // the games wait for it at the handoff barriers
     for (int k = 0; k < niter; k++) {
         ldsBarrier();  // B_k
         const uint32_t* ph = hdr + (k & 1) * 4;
