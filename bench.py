@@ -218,31 +218,63 @@ def cpu_baseline_c1(map_path, runs=5, steps=200_000, burnin=1000):
             "runs": rates, "host": host_info()}
 
 
-def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, dist):
-    """K steps with the observation all-gather after every step (xg["buf"] makes one_step run it),
-    one step launch per step, enqueued eagerly; the barrier + synchronize bracket and max over ranks of
-    the headline window.  -> the JSON block.  (Round 3: no hipGraph capture of the collectives any
-    more — a capture that fails leaves RCCL work events recorded in a capturing stream, and the
-    process group's watchdog thread then aborts the whole process.)"""
-    gb = mdist.ObservationGather(env.obs.shape, env.device, mode="allgather")
-    xg["buf"] = gb
-    try:
-        for k in range(3):  # untimed: the first collectives set up the communicator's channels
-            one_step(base + k)
-        gb.wait()
+def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, dist, mode=None):
+    """K steps with the observation all-gather after every step, one step launch per step (a per-step
+    consumer cannot use multi-step launches); the barrier + synchronize bracket and max over ranks of
+    the headline window.  -> the JSON block.  Full observability over RCCL: the native form
+    (mdist.NativeExchange: the K steps and their all-gathers enqueued by libmrts, the step kernel
+    writing the int16 transport, the collectives on the handle's own stream).  Otherwise (partially
+    observable views, gloo) one_step with xg["buf"] (Python enqueues each step and its collective).
+    No hipGraph capture: a capture that fails leaves RCCL work events recorded in a capturing stream,
+    and the process group's watchdog thread then aborts the whole process."""
+    native_ok = (mode is not None and dist.get_backend() != "gloo" and not a.po and a.launch == "native"
+                 and (mode["fused"] or mode["uni_fused"]))
+    if native_ok:
+        nx = mdist.NativeExchange(env)
+
+        def run(first, n):
+            if mode["fused"]:
+                nx.rollout_fused(SEED, first + 1, n)
+            else:
+                nx.rollout_uniform(SEED, first, n)
+
+        run(base, 3)  # untimed: the first collectives set up the communicator's channels
+        # the K steps and their collectives as one graph (RCCL's host cost per call would pace the
+        # steps otherwise: ~30 us of host work per step against a 9-22 us step)
+        nx.capture(lambda: run(base + 3, a.steps))
+        torch.cuda.synchronize(env.device)
+        nx.replay()  # warm replay (the first replay carries one-off costs)
         torch.cuda.synchronize(env.device)
         dist.barrier()
         torch.cuda.synchronize(env.device)
         t0 = time.perf_counter()
-        for k in range(a.steps):
-            one_step(base + 3 + k)
-        gb.wait()  # the last step's exchange belongs to the window
+        nx.replay()
         torch.cuda.synchronize(env.device)
         dist.barrier()
         t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
-    finally:
-        xg["buf"] = None
-        env.set_obs16(None)
+        how = ("native: mrts_rollout_*_exchange_dev enqueues each step launch and its ncclAllGather on the handle's own "
+               "RCCL communicator, captured once as a graph by libmrts (mrts_capture_begin / _end) and replayed")
+    else:
+        gb = mdist.ObservationGather(env.obs.shape, env.device, mode="allgather")
+        xg["buf"] = gb
+        try:
+            for k in range(3):  # untimed: the first collectives set up the communicator's channels
+                one_step(base + k)
+            gb.wait()
+            torch.cuda.synchronize(env.device)
+            dist.barrier()
+            torch.cuda.synchronize(env.device)
+            t0 = time.perf_counter()
+            for k in range(a.steps):
+                one_step(base + 3 + k)
+            gb.wait()  # the last step's exchange belongs to the window
+            torch.cuda.synchronize(env.device)
+            dist.barrier()
+            t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
+        finally:
+            xg["buf"] = None
+            env.set_obs16(None)
+        how = "eager: Python enqueues each step and its collective (torch.distributed)"
     return {
         "value": total_games * a.steps / t,
         "ms_per_step": 1e3 * t / a.steps,
@@ -250,7 +282,7 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
                       "overlapping the next step; " + ("int16 written by the step kernel" if not a.po else
                                                        "narrowing copy (partially observable planes)"),
         "payload_bytes_per_rank": env.obs.numel() * 2,  # int16 observation of one rank's slots, per step
-        "launch": "one step launch per step (a per-step consumer cannot use multi-step launches), enqueued eagerly",
+        "launch": "one step launch per step (a per-step consumer cannot use multi-step launches); " + how,
     }
 
 
@@ -768,7 +800,7 @@ def main():
         else:
             try:
                 out["with_gather"] = gather_window(env, a, xg, one_step, base + 3 * a.steps + 20, E * world, world,
-                                                   mdist, torch, dist)
+                                                   mdist, torch, dist, mode)
             except Exception as ex:  # the headline line must survive a failed exchange window
                 print(f"bench: exchange window failed: {ex!r}", file=sys.stderr)
                 out["with_gather"] = {"error": repr(ex)}

@@ -176,6 +176,39 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
                            uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t first_next_step,
                            int32_t n_steps, void* stream);
 #define MRTS_MAX_ITER 1024
+/* Native observation exchange over RCCL (BASELINE configs[3] "RCCL obs all-gather"; no
+ * Java counterpart — MicroRTS-Py gathers the envs' Responses.observation arrays in one process,
+ * Responses.java:12-30).  One process per GPU; every rank's handle joins one RCCL communicator:
+ * rank 0 calls mrts_rccl_unique_id, the id (128 bytes) travels to every rank by the caller's own
+ * means (torch.distributed), and each rank calls mrts_exchange_init with its rank.  rccl_path names
+ * the RCCL library the process already loaded (NULL or "" = "librccl.so"); its entry points are taken
+ * with dlopen / dlsym, so libmrts has no link-time dependency on RCCL. */
+int mrts_rccl_unique_id(const char* rccl_path, void* out);
+int mrts_exchange_init(mrts_env* env, const char* rccl_path, int32_t nranks, int32_t rank, const void* unique_id);
+/* n_steps fused steps (mrts_rollout_fused_dev's, but one launch per step: every step's observation is
+ * exchanged) each followed by an all-gather of that step's observation as int16 [n_slots][C][H][W]
+ * (the step kernel writes it into d_send0 / d_send1 alternately, mrts_set_obs16's transport) from every
+ * rank into d_recv [nranks][n_slots][C][H][W], on the handle's own communication stream: the collective
+ * of step k overlaps step k + 1, and a send buffer is rewritten only after the collective that read it
+ * two steps earlier finished.  All collectives of the call are complete when `stream` reaches the end
+ * of the call's work.  Full observability only (-ENOTSUP otherwise). */
+int mrts_rollout_fused_exchange_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                    double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed,
+                                    uint32_t first_next_step, int32_t n_steps, int16_t* d_send0, int16_t* d_send1,
+                                    int16_t* d_recv, void* stream);
+/* The same for BASELINE config c2's unmasked uniform rollout (mrts_rollout_uniform_dev, fused form). */
+int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                      double* d_reward, uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps,
+                                      int16_t* d_send0, int16_t* d_send1, int16_t* d_recv, void* stream);
+/* Graph form of a handle's calls (no Java counterpart): everything this handle enqueues on `stream`
+ * between mrts_capture_begin and mrts_capture_end (stream capture, thread-local mode; the exchange
+ * stream of an exchange rollout is joined inside the call) is instantiated as one graph, which
+ * mrts_replay launches on any stream with no host work per step.  A replay repeats the captured calls
+ * verbatim — the same step indices, seeds and buffers; the handle's bookkeeping advanced at capture
+ * time, as if the calls had run then.  Used to time the per-step exchange without host overhead. */
+int mrts_capture_begin(mrts_env* env, void* stream);
+int mrts_capture_end(mrts_env* env, void* stream);
+int mrts_replay(mrts_env* env, void* stream);
 /* Timing hook (no Java counterpart): the NEXT mrts_rollout_fused_dev / mrts_rollout_uniform_dev call
  * records `start` (a hipEvent_t) on its stream right before its first kernel launch and `end` right
  * after its last, so that a benchmark's events bracket exactly the rollout's kernels without two extra

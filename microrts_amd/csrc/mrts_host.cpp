@@ -1,7 +1,9 @@
 // mrts_host.cpp — host runtime behind include/mrts.h: map parsing, unit-type tables, per-game
 // state allocation in HBM, kernel launches, the Java-compatible host-pointer API and the
 // canonical state dump.  Compiled by hipcc into microrts_amd/libmrts.so.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: the entry points are taken from the RCCL library the process loaded
 
 #include <algorithm>
 #include <cerrno>
@@ -479,6 +481,15 @@ struct mrts_env {
     const int32_t* lastObsPtr = nullptr;
     int32_t* d_poPrev = nullptr;
     uint32_t* d_prioTab = nullptr;  // multi-step launches: per-SIMD issue-rank table (KDyn.prio_tab)
+    // native observation exchange (mrts_exchange_init): an RCCL communicator over this handle's ranks,
+    // its own communication stream, and per send buffer the step-ready / collective-done events
+    ncclComm_t exComm = nullptr;
+    int exRanks = 0;
+    hipStream_t exStream = nullptr;
+    hipEvent_t exReady[2] = {nullptr, nullptr}, exDone[2] = {nullptr, nullptr};
+    // mrts_capture_begin / _end / mrts_replay: the calls enqueued in between, as one instantiated graph
+    hipGraph_t capGraph = nullptr;
+    hipGraphExec_t capExec = nullptr;
     int poWords = 0;
     // delta mask writes: which buffer / player the last mask write went to
     int maskDelta = 0;
@@ -1140,6 +1151,180 @@ int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d
     return 0;
 }
 
+}  // extern "C" (the exchange loop below is a template)
+namespace {
+// RCCL entry points, resolved by dlopen / dlsym from the library path the caller names (the one its
+// process group already loaded: one RCCL instance per process)
+struct Rccl {
+    ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*allGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+    const char* (*errorString)(ncclResult_t) = nullptr;
+};
+Rccl g_rccl;
+void loadRccl(const char* path) {
+    if (g_rccl.allGather) return;
+    void* h = dlopen(path && *path ? path : "librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) throw Fail{-ENOENT, std::string("cannot load RCCL: ") + dlerror()};
+    Rccl r;
+    r.getUniqueId = (decltype(r.getUniqueId))dlsym(h, "ncclGetUniqueId");
+    r.commInitRank = (decltype(r.commInitRank))dlsym(h, "ncclCommInitRank");
+    r.allGather = (decltype(r.allGather))dlsym(h, "ncclAllGather");
+    r.commDestroy = (decltype(r.commDestroy))dlsym(h, "ncclCommDestroy");
+    r.errorString = (decltype(r.errorString))dlsym(h, "ncclGetErrorString");
+    if (!r.getUniqueId || !r.commInitRank || !r.allGather || !r.commDestroy || !r.errorString)
+        throw Fail{-ENOENT, "the RCCL library lacks an entry point"};
+    g_rccl = r;
+}
+void ncclChk(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess) throw Fail{-EIO, std::string(what) + ": " + g_rccl.errorString(r)};
+}
+// per step: wait until the collective that last read send buffer k % 2 is done, run the step (it
+// writes its int16 observation there), then all-gather it into recv on the exchange stream
+template <class StepFn>
+void exchangeLoop(mrts_env* env, int32_t n_steps, int16_t* d_send0, int16_t* d_send1, int16_t* d_recv, void* stream,
+                  StepFn step) {
+    if (!env->exComm) throw Fail{-EINVAL, "mrts_exchange_init first"};
+    if (env->partialObs) throw Fail{-ENOTSUP, "the int16 transport is written for full observability only"};
+    if (!d_send0 || !d_send1 || !d_recv || (((uintptr_t)d_send0 | (uintptr_t)d_send1) & 7))
+        throw Fail{-EINVAL, "send buffers must be 8-byte aligned, recv non-null"};
+    HIPCHK(hipSetDevice(env->device));
+    hipStream_t s = pickStream(env, stream);
+    int16_t* send[2] = {d_send0, d_send1};
+    const size_t bytes = (size_t)env->nSlots * env->C * env->HW * 2;
+    bool pending[2] = {false, false};
+    int16_t* const saved = env->obs16;
+    try {
+        for (int32_t k = 0; k < n_steps; k++) {
+            const int b = k & 1;
+            if (pending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
+            env->obs16 = send[b];
+            step(k);
+            HIPCHK(hipEventRecord(env->exReady[b], s));
+            HIPCHK(hipStreamWaitEvent(env->exStream, env->exReady[b], 0));
+            ncclChk(g_rccl.allGather(send[b], d_recv, bytes, ncclUint8, env->exComm, env->exStream), "ncclAllGather");
+            HIPCHK(hipEventRecord(env->exDone[b], env->exStream));
+            pending[b] = true;
+        }
+        for (int b = 0; b < 2; b++)  // the caller's stream covers every collective of the call
+            if (pending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
+    } catch (...) {
+        env->obs16 = saved;
+        throw;
+    }
+    env->obs16 = saved;
+}
+}  // namespace
+extern "C" {
+
+int mrts_capture_begin(mrts_env* env, void* stream) {
+    try {
+        if (!env || !stream) throw Fail{-EINVAL, "capture needs a handle and a non-default stream"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(hipStreamBeginCapture((hipStream_t)stream, hipStreamCaptureModeThreadLocal));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_capture_end(mrts_env* env, void* stream) {
+    try {
+        if (!env || !stream) throw Fail{-EINVAL, "capture needs a handle and a non-default stream"};
+        hipGraph_t g = nullptr;
+        HIPCHK(hipStreamEndCapture((hipStream_t)stream, &g));
+        if (env->capExec) (void)hipGraphExecDestroy(env->capExec);
+        if (env->capGraph) (void)hipGraphDestroy(env->capGraph);
+        env->capExec = nullptr;
+        env->capGraph = g;
+        HIPCHK(hipGraphInstantiate(&env->capExec, g, nullptr, nullptr, 0));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_replay(mrts_env* env, void* stream) {
+    try {
+        if (!env || !env->capExec) throw Fail{-EINVAL, "nothing captured"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(hipGraphLaunch(env->capExec, pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_rccl_unique_id(const char* rccl_path, void* out) {
+    try {
+        if (!out) throw Fail{-EINVAL, "null argument"};
+        loadRccl(rccl_path);
+        ncclUniqueId id;
+        ncclChk(g_rccl.getUniqueId(&id), "ncclGetUniqueId");
+        std::memcpy(out, &id, sizeof(id));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_exchange_init(mrts_env* env, const char* rccl_path, int32_t nranks, int32_t rank, const void* unique_id) {
+    try {
+        if (!env || !unique_id || nranks < 1 || rank < 0 || rank >= nranks) throw Fail{-EINVAL, "bad exchange arguments"};
+        if (env->exComm) throw Fail{-EINVAL, "the exchange is already initialised"};
+        loadRccl(rccl_path);
+        HIPCHK(hipSetDevice(env->device));
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof(id));
+        ncclChk(g_rccl.commInitRank(&env->exComm, nranks, id, rank), "ncclCommInitRank");
+        env->exRanks = nranks;
+        HIPCHK(hipStreamCreateWithFlags(&env->exStream, hipStreamNonBlocking));
+        for (int b = 0; b < 2; b++) {
+            HIPCHK(hipEventCreateWithFlags(&env->exReady[b], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&env->exDone[b], hipEventDisableTiming));
+        }
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_rollout_fused_exchange_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                    double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed,
+                                    uint32_t first_next_step, int32_t n_steps, int16_t* d_send0, int16_t* d_send1,
+                                    int16_t* d_recv, void* stream) {
+    if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
+    try {
+        RolloutEvents ev(env, stream);
+        exchangeLoop(env, n_steps, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
+            stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
+                      first_next_step + (uint32_t)k, 1, stream);
+        });
+        ev.done();
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                      double* d_reward, uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps,
+                                      int16_t* d_send0, int16_t* d_send1, int16_t* d_recv, void* stream) {
+    if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
+    try {
+        RolloutEvents ev(env, stream);
+        exchangeLoop(env, n_steps, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
+            stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, 1,
+                        stream);
+        });
+        ev.done();
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
 int mrts_policy_invalidate(mrts_env* env) {
     if (!env) return fail(Fail{-EINVAL, "null handle"});
     env->polValid = false;
@@ -1463,6 +1648,17 @@ void mrts_destroy(mrts_env* env) {
     (void)hipHostFree(env->h_reward);
     (void)hipHostFree(env->h_done);
     if (env->stream) (void)hipStreamDestroy(env->stream);
+    if (env->exComm) {
+        (void)hipStreamSynchronize(env->exStream);
+        (void)g_rccl.commDestroy(env->exComm);
+    }
+    if (env->exStream) (void)hipStreamDestroy(env->exStream);
+    if (env->capExec) (void)hipGraphExecDestroy(env->capExec);
+    if (env->capGraph) (void)hipGraphDestroy(env->capGraph);
+    for (int b = 0; b < 2; b++) {
+        if (env->exReady[b]) (void)hipEventDestroy(env->exReady[b]);
+        if (env->exDone[b]) (void)hipEventDestroy(env->exDone[b]);
+    }
     delete env;
 }
 

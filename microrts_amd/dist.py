@@ -138,3 +138,64 @@ class ObservationGather:
             for b in range(2):
                 if self.fired[b]:
                     cur.wait_event(self.done[b])
+
+
+def rccl_library_path():
+    """The RCCL library this process loaded (torch's process group uses it; the native exchange takes
+    its entry points from the same instance), or "librccl.so" when none is mapped yet."""
+    import os
+
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "librccl.so" in line:
+                return line.split()[-1]
+    bundled = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return bundled if os.path.exists(bundled) else "librccl.so"
+
+
+class NativeExchange:
+    """The observation exchange of every step from native code (mrts_rollout_*_exchange_dev): one RCCL
+    communicator per rank's handle (its unique id broadcast over the torch process group), the step
+    kernel writing the int16 transport into send buffer t % 2, the all-gather of step t on the
+    handle's own stream overlapping step t + 1, no Python between steps and no graph capture.  Full
+    observability; every rank of `group` must construct it (ncclCommInitRank is collective)."""
+
+    def __init__(self, env, group=None):
+        import ctypes
+
+        from microrts_amd import _lib
+
+        self.env = env
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        L, h = env._h.L, env._h.h
+        path = rccl_library_path().encode()
+        uid = (ctypes.c_char * 128)()
+        if self.rank == 0:
+            _lib.check(L.mrts_rccl_unique_id(path, uid))
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = (ctypes.c_char * 128).from_buffer_copy(box[0])
+        _lib.check(L.mrts_exchange_init(h, path, self.world, self.rank, uid))
+        shape = tuple(env.obs.shape)
+        self.send = [torch.zeros(shape, dtype=torch.int16, device=env.device) for _ in range(2)]
+        self.recv = torch.zeros((self.world,) + shape, dtype=torch.int16, device=env.device)
+
+    def rollout_fused(self, seed, first_next_step, n_steps):
+        """env.rollout_fused(...) with every step's observation all-gathered into self.recv."""
+        self.env.rollout_fused_exchange(seed, first_next_step, n_steps, self.send, self.recv)
+
+    def rollout_uniform(self, seed, first_step, n_steps):
+        """env.rollout_uniform(...) (fused form) with every step's observation all-gathered."""
+        self.env.rollout_uniform_exchange(seed, first_step, n_steps, self.send, self.recv)
+
+    def capture(self, fn):
+        """Capture fn()'s exchange rollout calls as one graph on a side stream (env.capture: the
+        collectives are this handle's own RCCL communicator, not the process group's, so no watchdog
+        tracks them); replay() launches it — the same steps, verbatim, no host work per step."""
+        cap = torch.cuda.Stream(self.env.device)
+        cap.wait_stream(torch.cuda.current_stream(self.env.device))
+        self.env.capture(fn, cap)
+        torch.cuda.current_stream(self.env.device).wait_stream(cap)
+
+    def replay(self):
+        self.env.replay()

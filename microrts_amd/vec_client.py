@@ -527,6 +527,46 @@ class DeviceVecEnv:
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
+    def rollout_fused_exchange(self, seed, first_next_step, n_steps, send, recv, stream=None):
+        """rollout_fused with one launch per step and the all-gather of every step's int16 observation
+        into recv (mrts_rollout_fused_exchange_dev; microrts_amd.dist.NativeExchange sets it up)."""
+        h = self._h
+        if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
+            _lib.check(h.L.mrts_policy_invalidate(h.h))
+        self._obs_guard()
+        a, pl, o, r, d, m = self._bufs()
+        _lib.check(h.L.mrts_rollout_fused_exchange_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, first_next_step,
+                                                       n_steps, self._p(send[0]), self._p(send[1]), self._p(recv),
+                                                       self._s(stream)))
+        self._obs_written()
+        self._policy_out, self._policy_version = self.actions, self.actions._version
+
+    def capture(self, fn, stream):
+        """Capture the calls fn() makes on this handle on `stream` (a non-default torch stream, made
+        current during fn) as one graph (mrts_capture_begin / _end); replay() launches it."""
+        h = self._h
+        s = ctypes.c_void_p(stream.cuda_stream)
+        with self.torch.cuda.stream(stream):
+            _lib.check(h.L.mrts_capture_begin(h.h, s))
+            try:
+                fn()
+            finally:
+                _lib.check(h.L.mrts_capture_end(h.h, s))
+
+    def replay(self, stream=None):
+        """Launch the graph capture() built (the same calls, verbatim) on `stream` (default: current)."""
+        _lib.check(self._h.L.mrts_replay(self._h.h, self._s(stream)))
+
+    def rollout_uniform_exchange(self, seed, first_step, n_steps, send, recv, stream=None):
+        """rollout_uniform (fused form) with the all-gather of every step's int16 observation
+        (mrts_rollout_uniform_exchange_dev)."""
+        h = self._h
+        self._obs_guard()
+        a, pl, o, r, d, _ = self._bufs()
+        _lib.check(h.L.mrts_rollout_uniform_exchange_dev(h.h, a, pl, o, r, d, seed, first_step, n_steps, self._p(send[0]),
+                                                         self._p(send[1]), self._p(recv), self._s(stream)))
+        self._obs_written()
+
     def step_rows(self, rows, stream=None):
         """gameStep with Java rows: int32 [slots][n_rows][8] on this device (any order, duplicates ok)."""
         h = self._h

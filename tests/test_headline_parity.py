@@ -234,3 +234,108 @@ def test_c_abi_fused_write_needs_invalidate():
         "without invalidate the written rows should have been ignored"
     for e in (A, B, C):
         e.close()
+
+
+def _exchange_env(env, world=1, rank=0):
+    import ctypes
+
+    from microrts_amd import _lib
+    from microrts_amd.dist import rccl_library_path
+
+    L, h = env._h.L, env._h.h
+    path = rccl_library_path().encode()
+    uid = (ctypes.c_char * 128)()
+    _lib.check(L.mrts_rccl_unique_id(path, uid))
+    _lib.check(L.mrts_exchange_init(h, path, world, rank, uid))
+    return path, uid
+
+
+@pytest.mark.parametrize("mp,uniform", [("maps/16x16/basesWorkers16x16.xml", False), ("maps/8x8/basesWorkers8x8.xml", True)])
+def test_native_exchange_one_rank(mp, uniform):
+    """mrts_rollout_{fused,uniform}_exchange_dev on a one-rank RCCL communicator: every output equals the
+    same rollout with one launch per step and no exchange (observations, rewards, dones, masks, next
+    actions, states), the last step's int16 observation arrived in recv[0], and the send buffers alternate
+    (the last step's in send[(n - 1) % 2]); a second mrts_exchange_init and a partially observable
+    handle are refused."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n_sp = 64
+    A = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=21, with_masks=not uniform)
+    B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=21, with_masks=not uniform)
+    A.set_multi_step(False)
+    for e in (A, B):
+        e.reset()
+        if not uniform:
+            e.random_policy(SEED, 0)
+    path, uid = _exchange_env(B)
+    send = [torch.zeros(tuple(B.obs.shape), dtype=torch.int16, device=B.device) for _ in range(2)]
+    recv = torch.zeros((1,) + tuple(B.obs.shape), dtype=torch.int16, device=B.device)
+    k = 0
+    for n in (1, 2, 7, 120):
+        if uniform:
+            A.rollout_uniform(SEED, k, n)
+            B.rollout_uniform_exchange(SEED, k, n, send, recv)
+        else:
+            A.rollout_fused(SEED, k + 1, n)
+            B.rollout_fused_exchange(SEED, k + 1, n, send, recv)
+        k += n
+        A.synchronize()
+        B.synchronize()
+        for name in ("obs", "reward", "done", "actions") + (() if uniform else ("masks",)):
+            assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
+        for s in range(0, n_sp, 2):
+            assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
+        o16 = B.obs.to(torch.int16)
+        assert torch.equal(recv[0], o16), f"recv after {k}"
+        assert torch.equal(send[(n - 1) % 2], o16), f"send buffer after {k}"
+    assert B._h.L.mrts_exchange_init(B._h.h, path, 1, 0, uid) != 0  # already initialised
+    P = DeviceVecEnv(8, 0, 300, ["maps/BWDistantResources32x32.xml"] * 8, seed=1, partial_obs=True, max_units=256)
+    P.reset()
+    P.random_policy(SEED, 0)
+    _exchange_env(P)
+    with pytest.raises(Exception):
+        P.rollout_fused_exchange(SEED, 1, 2, [torch.zeros(tuple(P.obs.shape), dtype=torch.int16, device=P.device)] * 2,
+                                 torch.zeros((1,) + tuple(P.obs.shape), dtype=torch.int16, device=P.device))
+    for e in (A, B, P):
+        assert not e.error_flags().any()
+        e.close()
+
+
+def test_native_exchange_graph_replay():
+    """mrts_capture_begin / _end / mrts_replay around an exchange rollout: the replay reruns the
+    captured steps verbatim — from the same start state it produces the same buffers as the eager call
+    (observations, masks, next actions, states, and the all-gathered int16 observation)."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mp, n_sp = "maps/16x16/basesWorkers16x16.xml", 32
+    A = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=4)
+    B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=4)
+    bufs = []
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+        e.rollout_fused(SEED, 1, 30)
+        _exchange_env(e)
+        bufs.append(([torch.zeros(tuple(e.obs.shape), dtype=torch.int16, device=e.device) for _ in range(2)],
+                     torch.zeros((1,) + tuple(e.obs.shape), dtype=torch.int16, device=e.device)))
+    A.rollout_fused_exchange(SEED, 31, 12, *bufs[0])
+    ck = B.checkpoint()
+    cap = torch.cuda.Stream(B.device)
+    cap.wait_stream(torch.cuda.current_stream(B.device))
+    B.capture(lambda: B.rollout_fused_exchange(SEED, 31, 12, *bufs[1]), cap)
+    torch.cuda.current_stream(B.device).wait_stream(cap)
+    torch.cuda.synchronize()
+    B.restore(ck)  # capture ran nothing: the replay starts from the same state
+    B.replay()
+    A.synchronize()
+    B.synchronize()
+    for name in ("obs", "reward", "done", "masks", "actions"):
+        assert torch.equal(getattr(A, name), getattr(B, name)), name
+    for s in range(0, n_sp, 2):
+        assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s}"
+    assert torch.equal(bufs[0][1], bufs[1][1])
+    for e in (A, B):
+        assert not e.error_flags().any()
+        e.close()
