@@ -139,6 +139,13 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #endif
 // 1: the rank also on c5's partially observable kernel (measured -4 %: its games outrank their own
 // helper waves, which then reach the handoff barriers late; round3q)
+// the rank's remaining-work estimate: (units + own idle units + MRTS_RANK_C) x steps left.  One game
+// alone on a SIMD takes ~ a + b x units per step with a / b ~ 75 units (E = 1024 span data), so the
+// steps left dominate: the games that fell behind issue first (c3, same box, 3 runs each: C = 0
+// 315.5 / 285.3 M at K = 200 / 20, C = 75 334.4 / 285.5 M, C = 150 334.1 / 280.7, C = 400 333.6 / 284.5)
+#ifndef MRTS_RANK_C
+#define MRTS_RANK_C 400
+#endif
 #ifndef MRTS_SIMD_RANK_PO
 #define MRTS_SIMD_RANK_PO 0
 #endif
@@ -4331,14 +4338,14 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
             const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
             q = wq >= MRTS_PRIO_T3 ? 3 : wq >= MRTS_PRIO_T2 ? 2 : wq >= MRTS_PRIO_T1 ? 1 : 0;
             if (ranked) {  // from the second step on: the rank among the SIMD's waves by remaining work
-                const int rk = simdRankStep(srank, (uint32_t)wq * (uint32_t)(niter - it));
+                const int rk = simdRankStep(srank, (uint32_t)(wq + MRTS_RANK_C) * (uint32_t)(niter - it));
                 if (it > 0) q = 3 - (rk < 3 ? rk : 3);
             }
         } else {  // units (the idle count's ballot costs the latency-bound one-game-per-SIMD c2 4.5 %)
             q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
             if (ranked) {
                 const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
-                const int rk = simdRankStep(srank, (uint32_t)wq * (uint32_t)(niter - it));
+                const int rk = simdRankStep(srank, (uint32_t)(wq + MRTS_RANK_C) * (uint32_t)(niter - it));
                 if (it > 0) q = 3 - (rk < 3 ? rk : 3);
             }
         }
