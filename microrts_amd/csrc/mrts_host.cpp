@@ -481,6 +481,7 @@ struct mrts_env {
     const int32_t* lastObsPtr = nullptr;
     int32_t* d_poPrev = nullptr;
     uint32_t* d_prioTab = nullptr;  // multi-step launches: per-SIMD issue-rank table (KDyn.prio_tab)
+    int32_t* d_bal = nullptr;       // multi-step launches: balanced game placement (KDyn.bal)
     // native observation exchange (mrts_exchange_init): an RCCL communicator over this handle's ranks,
     // its own communication stream, and per send buffer the step-ready / collective-done events
     ncclComm_t exComm = nullptr;
@@ -583,6 +584,7 @@ struct mrts_env {
         if (++launchStamp == 0) ++launchStamp;  // H_FWD = 0 means "no forwarded rows"
         D.fwd_stamp = launchStamp;
         D.prio_tab = D.n_iter > 1 ? d_prioTab : nullptr;
+        D.bal = D.n_iter > 1 ? d_bal : nullptr;
         return launchEnv(mode, hstatic, d_static, D, s);
     }
     int gameOfSlot(int slot, int* player) const {
@@ -808,6 +810,8 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         if (envIterable(env->hstatic)) {  // entries carry a launch stamp: stale ones are ignored, zero = empty
             HIPCHK(hipMalloc(&env->d_prioTab, (size_t)PRIO_KEYS * 16 * 4));
             HIPCHK(hipMemset(env->d_prioTab, 0, (size_t)PRIO_KEYS * 16 * 4));
+            HIPCHK(hipMalloc(&env->d_bal, ((size_t)BAL_COST + 2 * (size_t)env->nGames) * 4));
+            HIPCHK(hipMemset(env->d_bal, 0, ((size_t)BAL_COST + 2 * (size_t)env->nGames) * 4));
         }
         // initial state = reset (the Java constructor loads the maps)
         KDyn D;
@@ -1626,6 +1630,7 @@ void mrts_destroy(mrts_env* env) {
     (void)hipFree(env->d_static);
     (void)hipFree(env->d_poPrev);
     (void)hipFree(env->d_prioTab);
+    (void)hipFree(env->d_bal);
     (void)hipFree(env->d_state);
     (void)hipFree(env->d_polPrev);
     (void)hipFree(env->d_pairs);

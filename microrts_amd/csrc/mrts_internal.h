@@ -168,7 +168,11 @@ struct KDyn {
     // each wave posts its game's remaining-work estimate and takes its s_setprio from its rank among
     // the waves sharing its SIMD; null = the unit-count thresholds only
     uint32_t* prio_tab;
+    // multi-step launches: balanced game placement (mrts_kernels.hip, balancePerm): [1] the stamp of the launch that wrote perm, [2 + c] finished waves of block class c (b % 8), [BAL_COST + g] game g's cost as posted by the
+    // launch (stamp << 16 | units), [BAL_COST + n + b] the game block b of the NEXT launch runs; null = off
+    int32_t* bal;
 };
+constexpr int BAL_COST = 16;
 constexpr int PRIO_KEYS = 8 * 8 * 2 * 16 * 4;  // XCC x SE x SH x CU x SIMD (HW_ID / XCC_ID fields)
 // PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);
 // snapshot bytes of the unit slots (after the end-of-step compaction); per view p the sight rows

@@ -146,6 +146,13 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_RANK_C
 #define MRTS_RANK_C 400
 #endif
+// 0: multi-step launches keep game g on block g (no balanced placement, A/B builds)
+#ifndef MRTS_BALANCE
+#define MRTS_BALANCE 1
+#endif
+#ifndef MRTS_BAL_MIN_ITER
+#define MRTS_BAL_MIN_ITER 64
+#endif
 #ifndef MRTS_SIMD_RANK_PO
 #define MRTS_SIMD_RANK_PO 0
 #endif
@@ -499,8 +506,8 @@ struct Game {
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
     // array offset then folds to an immediate), else the kernel arguments
     DEV Game(const KStatic& p, const KDyn& d, int32_t* stb, int stw, uint8_t* smem, int h, int w, int hw, int cap, bool partial,
-             int k, int nt, int r, bool iterating = false)
-        : P(p), D(d), U(*(const DevUtt*)smem), g((int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
+             int k, int nt, int r, bool iterating = false, int game = -1)
+        : P(p), D(d), U(*(const DevUtt*)smem), g(game >= 0 ? game : (int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
           po(partial), iter(iterating), stBase(stb), stWords(stw) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
@@ -4176,6 +4183,79 @@ DEV int simdRankStep(SimdRank& r, uint32_t est) {
     return rank;
 }
 
+// Balanced game placement (multi-step c3 launches, KDyn.bal).  With the rank priority above the four
+// games of a SIMD finish together, and a launch ends with its slowest SIMD: round 3 span data, a SIMD's
+// end time correlates 0.86-0.96 with its games' total unit count and the slowest SIMD ends 8 % after the
+// mean.  The dispatcher places blocks b, b + n/4, b + 2n/4, b + 3n/4 on one SIMD (one dispatch round of
+// four waves per SIMD; identical in every launch and process measured), so a permutation of games over
+// blocks that gives each such group a heavy-to-light mix balances the SIMDs.  Each game posts its unit
+// count at the end of a launch; the last wave of each XCD class counting-sorts that class's posted
+// counts and writes its part of the permutation for the next launches — snake order over the groups,
+// so a group gets one game from each quarter of the order, heavy paired with light — and the stamp.  A launch whose predecessor on the
+// handle left a permutation uses it (block b runs game perm[b]), else identity.  The permutation is
+// sticky: only launches of at least MRTS_BAL_MIN_ITER steps post costs and write a new one, shorter
+// ones reuse the last (a game that changes CU pays cold TLB misses for its output pages: moving games
+// at every launch cost a 20-step launch ~12 us, round 3 span data).  Which block runs a
+// game never changes what the game computes: correctness needs only that perm is a permutation
+// (a counting sort's output is one), and a missing or stale posted cost leaves the old stamp in place.
+DEV int balancedGame(const KDyn& D) {
+    const int n = (int)gridDim.x;
+    const int32_t hdr1 = __builtin_nontemporal_load(D.bal + 1);
+    const int32_t pg = __builtin_nontemporal_load(D.bal + BAL_COST + n + (int)blockIdx.x);
+    return hdr1 != 0 ? pg : (int)blockIdx.x;
+}
+DEV void balancePerm(const KDyn& D, uint32_t* hist, int c) {
+    // games stay on their XCD: block b runs on XCD b % 8 and the four blocks of a SIMD group share b % 8,
+    // so the permutation only moves games between blocks of the same residue class c (the state a game
+    // left in that XCD's L2 stays near), and each class's LAST wave sorts that class alone: n / 8
+    // games, n / 32 SIMD groups, the snake order as above (1/8 of the work on the launch's tail)
+    const int n = (int)gridDim.x, l = lane_id(), Q = n >> 5, per = n >> 9;  // per: games per lane
+    int32_t* const cost = D.bal + BAL_COST;
+    int32_t* const perm = cost + n;
+    const uint32_t tag = D.fwd_stamp & 0xFFFFu;
+#pragma unroll
+    for (int j = 0; j < 4; j++) hist[l + 64 * j] = 0;
+    // this lane's games c + 8 * (l * per + i): all loads in flight at once, system scope (the costs
+    // came through other XCDs' L2s)
+    const __amdgpu_buffer_rsrc_t rs = bufRsrc(cost, (uint32_t)(n * 4));
+    uint32_t cv[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (i < per) cv[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((c + 8 * (l * per + i)) * 4), 0, 17);
+    wsync();
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (i < per) {
+            ok = ok && (cv[i] >> 16) == tag;
+            atomicAdd(&hist[255u - (cv[i] & 255u)], 1u);  // heaviest first
+        }
+    if (ballot(!ok)) return;  // a game has not posted (cannot happen: every wave posts before it counts): keep the old
+    wsync();
+    uint32_t v[4], sum = 0;  // exclusive prefix over the 256 bins: 4 per lane, then a wave scan
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        v[j] = hist[4 * l + j];
+        sum += v[j];
+    }
+    const uint32_t incl = (uint32_t)wave_incl_sum((int)sum);
+    uint32_t run = incl - sum;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        hist[4 * l + j] = run;
+        run += v[j];
+    }
+    wsync();
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (i < per) {
+            const int r = (int)atomicAdd(&hist[255u - (cv[i] & 255u)], 1u);  // rank in the class
+            const int q = r / Q, j = r - q * Q;
+            perm[c + 8 * (q * Q + ((q & 1) ? Q - 1 - j : j))] = c + 8 * (l * per + i);
+        }
+    if (l == 0) D.bal[1] = (int32_t)D.fwd_stamp;  // (every class writes the same) the next launches take it
+}
+
 // Workgroup barrier for an LDS handoff: the release / acquire fences cover LDS only, so a wave does
 // not drain its outstanding global stores at every step (a __syncthreads fence would).
 DEV void ldsBarrier() {
@@ -4248,8 +4328,14 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
         return;
     }
     const KStatic& P = *PS;
+    // balanced placement (c3's multi-step kernel): this block's game from the previous launch's permutation
+    // (balancePerm: a multiple of 512 games, at most 8 per lane and class)
+    const bool balanced = MULTI && MRTS_BALANCE && FIX == 16 && !FPO && D.bal != nullptr && (gridDim.x & 511) == 0 &&
+                          gridDim.x <= 4096;
+    const bool rebalance = balanced && D.n_iter >= MRTS_BAL_MIN_ITER;  // this launch writes the next permutation
+    const int game = balanced ? balancedGame(D) : -1;
     Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
-           FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI);
+           FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI, game);
     // the partially observable helper wave: one packed render per step (helperLoopPO)
     uint32_t* const poHelpHdr = (HELP && FPO) ? (uint32_t*)(smem + D.help_off) : nullptr;
     if (HELP && FPO && threadIdx.x >= 64) {
@@ -4594,6 +4680,25 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
 #ifdef MRTS_ABLATE
         if (G.ab(AB_STORE)) G.store();
 #endif
+    }
+    if (rebalance) {  // post this game's final unit count; the launch's LAST wave writes the next placement
+        const uint32_t tag = D.fwd_stamp & 0xFFFFu;
+        uint32_t last = 0;
+        if (lane_id() == 0) {
+            // agent scope, written through: the last wave may sit on another XCD (another L2)
+            __hip_atomic_store(D.bal + BAL_COST + G.g, (int32_t)((tag << 16) | (uint32_t)(G.nu < 255 ? G.nu : 255)),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            drainStores();  // the cost is in memory before this wave counts itself
+            // waves of this block's class (b % 8) finished in this launch, wrapping to 0 at the last
+            // (atomicInc): no reset needed, and no compare-and-swap retries (4096 contending CAS loops
+            // at device scope took milliseconds)
+            const uint32_t old = atomicInc((uint32_t*)D.bal + 2 + (blockIdx.x & 7u), gridDim.x / 8u - 1u);
+            last = old == gridDim.x / 8u - 1u ? 1u : 0u;
+        }
+        if (uniu(last)) {
+            wsync();
+            balancePerm(D, (uint32_t*)smem, (int)(blockIdx.x & 7u));
+        }
     }
     PHASE(10);
 #ifdef MRTS_PHASE_TIMING
