@@ -703,8 +703,8 @@ def main():
                        "timed window)" if uniform
                        else "fused into the step kernel (mrts_step_fused_dev)" if fused
                        else "separate masked-uniform policy kernel before each step (mrts_policy_dev)"),
-            "kernel_timing": (f"{event_kind} recorded on the launch stream right before / after the multi-step launch "
-                              "in the timed window (by the library: mrts_set_rollout_events), / K" if launch_ms is not None
+            "kernel_timing": (f"{event_kind} recorded by the multi-step launch's own dispatch in the timed window "
+                              "(mrts_set_rollout_events: hipExtLaunchKernelGGL start / stop events), / K" if launch_ms is not None
                               else f"{event_kind} around each step-kernel launch, eager pass over the next K steps"
                               if (native or graph is not None) else f"{event_kind} around each step-kernel launch in the timed window"),
             "parallelism": f"dp{world} (independent env shards)" + (

@@ -210,10 +210,11 @@ int mrts_capture_begin(mrts_env* env, void* stream);
 int mrts_capture_end(mrts_env* env, void* stream);
 int mrts_replay(mrts_env* env, void* stream);
 /* Timing hook (no Java counterpart): the NEXT mrts_rollout_fused_dev / mrts_rollout_uniform_dev call
- * records `start` (a hipEvent_t) on its stream right before its first kernel launch and `end` right
- * after its last, so that a benchmark's events bracket exactly the rollout's kernels without two extra
- * host calls in its timed window.  One shot: the handle forgets both events when that call begins.
- * Either may be NULL. */
+ * records `start` (a hipEvent_t) with its first kernel launch and `end` with its last — as the kernel
+ * dispatches' own start / end timestamps (hipExtLaunchKernelGGL), so a benchmark's events bracket
+ * exactly the rollout's kernels with no extra host call or marker packet in its timed window (the
+ * exchange rollouts record them on their stream around the call's work).  One shot: the handle forgets
+ * both events when that call begins.  Either may be NULL. */
 int mrts_set_rollout_events(mrts_env* env, void* start, void* end);
 /* Every later observation write of this handle (any step / reset call with an observation buffer)
  * also writes the planes as int16 into d_obs16 [n_slots][C][H][W] (every value fits: hp, unit

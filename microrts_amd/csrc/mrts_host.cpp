@@ -23,7 +23,8 @@ using namespace mrts;
 
 namespace mrts {
 size_t ldsBytes(int HW, int W, int CAP, int po);
-hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream);
+hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream, hipEvent_t e0 = nullptr,
+                     hipEvent_t e1 = nullptr);
 bool envIterable(const KStatic& hs);
 hipError_t launchPolicyUniform(int32_t* actions, int n_slots, int HW, int ntypes, int natt, uint64_t seed, uint32_t step,
                                uint32_t slot_base, hipStream_t stream);
@@ -566,7 +567,7 @@ struct mrts_env {
         hstatic.tmpl_off = d_tmplOff;
         hstatic.game_kind = d_gameKind;
     }
-    hipError_t launch(int mode, const KDyn& Din, hipStream_t s) const {
+    hipError_t launch(int mode, const KDyn& Din, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) const {
         KDyn D = Din;
         D.state = d_state;
         D.state_words = stateWords(CAP, HW);
@@ -585,7 +586,7 @@ struct mrts_env {
         D.fwd_stamp = launchStamp;
         D.prio_tab = D.n_iter > 1 ? d_prioTab : nullptr;
         D.bal = D.n_iter > 1 ? d_bal : nullptr;
-        return launchEnv(mode, hstatic, d_static, D, s);
+        return launchEnv(mode, hstatic, d_static, D, s, e0, e1);
     }
     int gameOfSlot(int slot, int* player) const {
         if (slot < 2 * nSpGames) {
@@ -895,7 +896,8 @@ namespace {
 // launch was a fused step on these buffers: delta masks and policy rows, forwarded action words);
 // else one step.  Returns the number of steps enqueued.
 int stepFused(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
-              uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step, int32_t n_iter, void* stream) {
+              uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step, int32_t n_iter, void* stream,
+              hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     if (!d_actions || !d_masks) throw Fail{-EINVAL, "actions and masks are required"};
     if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
     HIPCHK(hipSetDevice(env->device));
@@ -918,7 +920,7 @@ int stepFused(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32
     D.fwd_read = env->fusedActions == d_actions ? 1 : 0;  // games check H_FWD == this stamp - 1
     const bool steady = D.pol_delta && D.fwd_read && D.mask_delta && envIterable(env->hstatic);
     D.n_iter = (steady && n_iter > 1) ? n_iter : 1;
-    HIPCHK(env->launch(0, D, pickStream(env, stream)));
+    HIPCHK(env->launch(0, D, pickStream(env, stream), e0, e1));
     env->fusedActions = d_actions;
     if (env->lastPolicyActions == d_actions) env->polValid = false;  // the standalone policy's delta base is stale
     return D.n_iter;
@@ -966,13 +968,19 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
                            int32_t n_steps, void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
-        RolloutEvents ev(env, stream);
+        // the timing events ride on the launches: start with the first, end re-recorded by each (the last wins)
+        hipEvent_t e0 = env->evStart, e1 = env->evEnd;
+        env->evStart = env->evEnd = nullptr;
+        if (n_steps == 0) {
+            RolloutEvents ev(env, stream);
+            ev.done();
+        }
         for (int32_t k = 0; k < n_steps;) {
             const int32_t n = std::min<int32_t>(n_steps - k, env->multiStep ? MRTS_MAX_ITER : 1);
             k += stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
-                           first_next_step + (uint32_t)k, n, stream);
+                           first_next_step + (uint32_t)k, n, stream, e0, e1);
+            e0 = nullptr;
         }
-        ev.done();
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1089,7 +1097,8 @@ namespace {
 // n_iter fused uniform steps (step, step + 1, ...) as ONE launch on the multi-step shapes (the rows
 // are drawn in the kernel, so no steady state is needed), else one.  Returns the steps enqueued.
 int stepUniform(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
-                uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t step, int32_t n_iter, void* stream) {
+                uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t step, int32_t n_iter, void* stream,
+                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     if (!env || !d_actions) throw Fail{-EINVAL, "null argument"};
     if ((uintptr_t)d_actions & 3) throw Fail{-EINVAL, "misaligned buffer"};
     if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
@@ -1114,7 +1123,7 @@ int stepUniform(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int
     D.n_iter = (loopable && n_iter > 1) ? n_iter : 1;
     if (d_masks || env->fusedActions == d_actions) env->fusedActions = nullptr;
     if (env->lastPolicyActions == d_actions) env->polValid = false;
-    HIPCHK(env->launch(0, D, pickStream(env, stream)));
+    HIPCHK(env->launch(0, D, pickStream(env, stream), e0, e1));
     return D.n_iter;
 }
 }  // namespace
@@ -1135,13 +1144,14 @@ int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     if (fused) {
         try {
-            RolloutEvents ev(env, stream);
+            hipEvent_t e0 = env->evStart, e1 = env->evEnd;  // on the launches (see mrts_rollout_fused_dev)
+            env->evStart = env->evEnd = nullptr;
             for (int32_t k = 0; k < n_steps;) {
                 const int32_t n = std::min<int32_t>(n_steps - k, env->multiStep ? MRTS_MAX_ITER : 1);
                 k += stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, n,
-                                 stream);
+                                 stream, e0, e1);
+                e0 = nullptr;
             }
-            ev.done();
             return 0;
         } catch (const Fail& f) {
             return fail(f);

@@ -11,6 +11,7 @@
 // observation planes, legal-action masks) runs lane-parallel with ballots and DPP reductions.
 // No MFMA: integer/indexing work.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -5113,38 +5114,42 @@ hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, f
     return hipGetLastError();
 }
 
-hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream) {
+// e0 / e1 (may be null): timing events the launch records itself (hipExtLaunchKernelGGL: the kernel
+// dispatch's own start / end timestamps — no separate marker packets around it; mrts_set_rollout_events)
+hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn& D, hipStream_t stream, hipEvent_t e0, hipEvent_t e1) {
     const size_t lds = ldsBytes(hs.HW, hs.W, hs.CAP, hs.partial_obs);
     dim3 grid((unsigned)hs.n_games), block(64);
     const bool fixable = hs.n_sp_games == hs.n_games && D.rows == nullptr && hs.utt.K == 79 && hs.utt.ntypes == 7 &&
                          hs.utt.maxAttackRadius == 7 && hs.H == hs.W;
     auto is = [&](int w, int cap, bool po) { return fixable && hs.W == w && hs.CAP == cap && (hs.partial_obs != 0) == po; };
+#define LAUNCH(kern, g_, b_, l_, s_, ...) hipExtLaunchKernelGGL(kern, g_, b_, (uint32_t)(l_), s_, e0, e1, 0, __VA_ARGS__)
     switch (mode) {
         case MODE_STEP:
-            if (D.n_iter > 1 && is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false, true>), grid, block, lds, stream, D.state, ds, D);
+            if (D.n_iter > 1 && is(16, 320, false)) LAUNCH((k_env<MODE_STEP, 16, 320, false, true>), grid, block, lds, stream, D.state, ds, D);
             else if (D.n_iter > 1 && is(8, 128, false) && D.uni_actions && !D.masks) {
                 // c2's fused uniform rollout: a helper wave per game (helperLoop)
                 KDyn D2 = D;
                 D2.help_off = (int32_t)((lds + 15) & ~(size_t)15);
-                hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true, true>), grid, dim3(128), (size_t)D2.help_off + 2048, stream,
+                LAUNCH((k_env<MODE_STEP, 8, 128, false, true, true>), grid, dim3(128), (size_t)D2.help_off + 2048, stream,
                                    D.state, ds, D2);
-            } else if (D.n_iter > 1 && is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false, true>), grid, block, lds, stream, D.state, ds, D);
+            } else if (D.n_iter > 1 && is(8, 128, false)) LAUNCH((k_env<MODE_STEP, 8, 128, false, true>), grid, block, lds, stream, D.state, ds, D);
             else if (D.n_iter > 1 && is(32, 320, true) && D.obs && !MRTS_NO_PO_HELPER) {
                 // c5's partially observable rollout: a helper wave per game renders the views (helperLoopPO)
                 KDyn D2 = D;
                 D2.help_off = (int32_t)((lds + 15) & ~(size_t)15);
-                hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true, true>), grid, dim3(128), (size_t)D2.help_off + 4 * (8 + 2 * 32) + 64,
+                LAUNCH((k_env<MODE_STEP, 32, 320, true, true, true>), grid, dim3(128), (size_t)D2.help_off + 4 * (8 + 2 * 32) + 64,
                                    stream, D.state, ds, D2);
-            } else if (D.n_iter > 1 && is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
-            else if (is(16, 320, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
-            else if (is(8, 128, false)) hipLaunchKernelGGL((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, D.state, ds, D);
-            else if (is(32, 320, true)) hipLaunchKernelGGL((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, D.state, ds, D);
-            else hipLaunchKernelGGL((k_env<MODE_STEP, 0>), grid, block, lds, stream, D.state, ds, D);
+            } else if (D.n_iter > 1 && is(32, 320, true)) LAUNCH((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
+            else if (is(16, 320, false)) LAUNCH((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
+            else if (is(8, 128, false)) LAUNCH((k_env<MODE_STEP, 8, 128, false>), grid, block, lds, stream, D.state, ds, D);
+            else if (is(32, 320, true)) LAUNCH((k_env<MODE_STEP, 32, 320, true>), grid, block, lds, stream, D.state, ds, D);
+            else LAUNCH((k_env<MODE_STEP, 0>), grid, block, lds, stream, D.state, ds, D);
             break;
-        case MODE_RESET: hipLaunchKernelGGL((k_env<MODE_RESET, 0>), grid, block, lds, stream, D.state, ds, D); break;
-        case MODE_PLAYOUT: hipLaunchKernelGGL((k_env<MODE_PLAYOUT, 0>), grid, block, lds, stream, D.state, ds, D); break;
-        default:hipLaunchKernelGGL((k_env<MODE_MASKS, 0>), grid, block, lds, stream, D.state, ds, D); break;
+        case MODE_RESET: LAUNCH((k_env<MODE_RESET, 0>), grid, block, lds, stream, D.state, ds, D); break;
+        case MODE_PLAYOUT: LAUNCH((k_env<MODE_PLAYOUT, 0>), grid, block, lds, stream, D.state, ds, D); break;
+        default:LAUNCH((k_env<MODE_MASKS, 0>), grid, block, lds, stream, D.state, ds, D); break;
     }
+#undef LAUNCH
     return hipGetLastError();
 }
 // launchEnv(MODE_STEP) would run a specialised self-play kernel (16x16 / 8x8 full observability,
