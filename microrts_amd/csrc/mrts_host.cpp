@@ -812,7 +812,11 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
             HIPCHK(hipMalloc(&env->d_prioTab, (size_t)PRIO_KEYS * 16 * 4));
             HIPCHK(hipMemset(env->d_prioTab, 0, (size_t)PRIO_KEYS * 16 * 4));
             HIPCHK(hipMalloc(&env->d_bal, ((size_t)BAL_COST + 2 * (size_t)env->nGames) * 4));
-            HIPCHK(hipMemset(env->d_bal, 0, ((size_t)BAL_COST + 2 * (size_t)env->nGames) * 4));
+            // header and costs zero, the permutation the identity: a class slice no launch rewrote stays a
+            // permutation of its games (balancePerm writes each XCD class's slice on its own)
+            std::vector<int32_t> bal((size_t)BAL_COST + 2 * (size_t)env->nGames, 0);
+            for (int g = 0; g < env->nGames; g++) bal[(size_t)BAL_COST + env->nGames + g] = g;
+            HIPCHK(hipMemcpy(env->d_bal, bal.data(), bal.size() * 4, hipMemcpyHostToDevice));
         }
         // initial state = reset (the Java constructor loads the maps)
         KDyn D;
