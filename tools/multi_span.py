@@ -23,7 +23,10 @@ from microrts_amd import DeviceVecEnv  # noqa: E402
 E = int(os.environ.get("E", 4096))
 K = int(os.environ.get("K", 200))
 SEED = 0x5EEDC0DE
-env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, "maps/16x16/basesWorkers16x16.xml")] * (2 * E), seed=SEED)
+MAP = os.environ.get("MAP", "maps/16x16/basesWorkers16x16.xml")
+PO = os.environ.get("PO", "0") == "1"
+env = DeviceVecEnv(2 * E, 0, 2000, [os.path.join(ROOT, MAP)] * (2 * E), seed=SEED, partial_obs=PO,
+                   max_units=int(os.environ.get("MAXU", 0)))
 env.reset()
 env.random_policy(SEED, 0)
 env.rollout_fused(SEED, 1, 1000)
