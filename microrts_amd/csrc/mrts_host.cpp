@@ -483,6 +483,7 @@ struct mrts_env {
     int32_t* d_poPrev = nullptr;
     uint32_t* d_prioTab = nullptr;  // multi-step launches: per-SIMD issue-rank table (KDyn.prio_tab)
     int32_t* d_bal = nullptr;       // multi-step launches: balanced game placement (KDyn.bal)
+    int obsImg = 0;                 // KDyn.obs_img: every observation value fits a byte
     // native observation exchange (mrts_exchange_init): an RCCL communicator over this handle's ranks,
     // its own communication stream, and per send buffer the step-ready / collective-done events
     ncclComm_t exComm = nullptr;
@@ -586,6 +587,7 @@ struct mrts_env {
         D.fwd_stamp = launchStamp;
         D.prio_tab = D.n_iter > 1 ? d_prioTab : nullptr;
         D.bal = D.n_iter > 1 ? d_bal : nullptr;
+        D.obs_img = obsImg;
         return launchEnv(mode, hstatic, d_static, D, s, e0, e1);
     }
     int gameOfSlot(int slot, int* player) const {
@@ -722,6 +724,13 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         if (lds > 64 * 1024) HIPCHK(prepareLds(lds));
         for (auto& m : maps)
             if ((int)m.units.size() > maxUnits) throw Fail{-ENOSPC, "a map holds more units than max_units"};
+        {  // the largest hp / resources an observation plane can show: the maps' units, the table's types
+            int mx = 0;
+            for (auto& m : maps)
+                for (auto& u : m.units) mx = std::max(mx, std::max(u.hp, u.res));
+            for (int t = 0; t < env->utt.ntypes; t++) mx = std::max(mx, std::max(env->utt.hp[t], env->utt.harvestAmt[t]));
+            env->obsImg = mx <= 255 ? 1 : 0;
+        }
         // templates blob
         std::vector<int32_t> blob;
         std::vector<int> off;

@@ -171,6 +171,10 @@ struct KDyn {
     // multi-step launches: balanced game placement (mrts_kernels.hip, balancePerm): [1] the stamp of the launch that wrote perm, [2 + c] finished waves of block class c (b % 8), [BAL_COST + g] game g's cost as posted by the
     // launch (stamp << 16 | units), [BAL_COST + n + b] the game block b of the NEXT launch runs; null = off
     int32_t* bal;
+    // 1: every value a full-observability plane shows fits a byte (hp, resources of the maps' units and
+    // the unit-type table, mrts_create), so 16x16 observations render through the byte image
+    // (writeObsFullImg)
+    int32_t obs_img;
 };
 constexpr int BAL_COST = 16;
 constexpr int PRIO_KEYS = 8 * 8 * 2 * 16 * 4;  // XCC x SE x SH x CU x SIMD (HW_ID / XCC_ID fields)

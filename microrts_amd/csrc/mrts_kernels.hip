@@ -2468,7 +2468,85 @@ struct Game {
             v[4] = (a & UA_PRESENT) ? ua_type(a) : 0;
         }
     }
+    // 16x16 full observability with every value below 256 (KDyn.obs_img): the five dynamic planes are
+    // rendered as bytes into LDS by one pass over the unit list (lane = unit slot; a live unit owns its
+    // cell, the dead are off the cell map, as in the gather below), then each lane's 4 cells x 5 planes
+    // come back as zero-extended byte loads (LDS pipe, no VALU) straight into the dwordx4 stores.  The
+    // cell-map gather costs the VALU-issue-bound c3 kernel ~150 VALU instructions per game-step more.
+    // `snap` is the image (ldsBytes reserves 5 HW bytes there; snapshots exist only in PO games).
+    DEV void writeObsFullImg(int slot0, int nslots, int player0) {
+        uint8_t* const img = snap;
+        const int l = lid();
+        uint32_t* const iw = (uint32_t*)img;
+#pragma unroll
+        for (int i = 0; i < 5; i++) iw[l + 64 * i] = 0u;  // 5 x 256 bytes
+        wsync();
+        for (int s = l; s < nu; s += 64) {
+            const uint32_t cu = uc[s];
+            if (!(cu & UC_DEAD)) {
+                const int c = uy(cu) * W + ux(cu), pl = uplay(cu);
+                const uint32_t a = ua[s];
+                img[c] = (uint8_t)hp[s];
+                img[HW + c] = (uint8_t)res[s];
+                img[2 * HW + c] = (uint8_t)(pl >= 0 ? ((pl + player0) % 2) + 1 : 0);
+                img[3 * HW + c] = (uint8_t)(utyp(cu) + 1);
+                img[4 * HW + c] = (uint8_t)((a & UA_PRESENT) ? ua_type(a) : 0);
+            }
+        }
+        wsync();
+        const int c4 = 4 * l;
+        int v[6][4];
+#pragma unroll
+        for (int q = 0; q < 5; q++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[q][j] = img[q * HW + c4 + j];
+        const int npl = firstIt ? 6 : 5;  // the static terrain plane: first write of a launch only
+        if (firstIt)
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[5][j] = cell[c4 + j] == WALL ? 1 : 0;
+        else
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[5][j] = 0;
+        int32_t* o0 = D.obs + (size_t)slot0 * D.C * HW;
+        const __amdgpu_buffer_rsrc_t rs = bufRsrc(o0, (uint32_t)(nslots * D.C * HW * 4));
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            if (i >= nslots) break;
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                if (q >= npl) break;
+                int w[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) w[j] = (i && q == 2 && v[q][j]) ? 3 - v[q][j] : v[q][j];  // the other player's owners
+                const uint32_t off = (uint32_t)((i * D.C + q) * HW + c4);
+                if (SC1_OBS) st4sc1(rs, off * 4u, w[0], w[1], w[2], w[3]);
+                else st4<WT_OBS>(o0 + off, w[0], w[1], w[2], w[3]);
+            }
+        }
+        if (MRTS_UNLIKELY(D.obs16 != nullptr)) {  // the int16 transport copy (mrts_set_obs16): every plane
+            if (!firstIt)
+#pragma unroll
+                for (int j = 0; j < 4; j++) v[5][j] = cell[c4 + j] == WALL ? 1 : 0;
+            int16_t* h0 = D.obs16 + (size_t)slot0 * D.C * HW;
+            for (int i = 0; i < nslots; i++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) {
+                    int4 w4 = make_int4(v[q][0], v[q][1], v[q][2], v[q][3]);
+                    if (i && q == 2) {
+                        w4.x = w4.x ? 3 - w4.x : 0;
+                        w4.y = w4.y ? 3 - w4.y : 0;
+                        w4.z = w4.z ? 3 - w4.z : 0;
+                        w4.w = w4.w ? 3 - w4.w : 0;
+                    }
+                    *(uint2*)(h0 + (size_t)(i * D.C + q) * HW + c4) = pk16(w4);
+                }
+        }
+    }
     DEV void writeObsFull(int slot0, int nslots, int player0) {
+        if (HW == 256 && !po && D.obs_img && nslots <= 2) {
+            writeObsFullImg(slot0, nslots, player0);
+            return;
+        }
         int32_t* o0 = D.obs + (size_t)slot0 * D.C * HW;
         if (HW <= 64) {
             // small maps (8x8: c2): lane = cell, one LDS round for the cell entry and one for its
@@ -4956,7 +5034,9 @@ size_t ldsBytes(int HW, int W, int CAP, int po) {
     return (size_t)UTT_LDS + (size_t)16 * CAP + 4 * (size_t)((HW + 2 * W + 31) / 32) + 4 * 64 + 8 * (size_t)maskWords(HW) + 64 + 128 +
            (po ? 4 * (size_t)HW + 8 * (size_t)(HW / W) * (size_t)((W + 31) / 32) : 0) +
            (po && poDeltaShape(HW / W, W) ? 4 * (6 * (size_t)(HW / W) + 6 * (size_t)poChunkWords(HW)) + 4 * (size_t)((HW / 4 + 1) & ~1) : 0) +
-           6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 + (((size_t)CAP + 3) & ~(size_t)3);
+           6 * (size_t)CAP + 2 * (size_t)HW + 2 * 64 +
+           // the snapshot bytes (PO) — or, full observability on 16x16, the observation byte image (writeObsFullImg)
+           std::max((((size_t)CAP + 3) & ~(size_t)3), (!po && HW == 256) ? 5 * (size_t)HW : (size_t)0);
 }
 // MicroRTS-Py GridnetVecEnv observation encoding (gym_microrts `_encode_obs`: clip each plane to
 // [0, n_k - 1], one-hot, channels-last): int32 obs [S][C][H][W] -> uint8 [S][H][W][F] with plane sizes
