@@ -143,9 +143,11 @@ DEV int lane_id() { return (int)threadIdx.x; }
 // the rank's remaining-work estimate: (units + own idle units + MRTS_RANK_C) x steps left.  One game
 // alone on a SIMD takes ~ a + b x units per step with a / b ~ 75 units (E = 1024 span data), so the
 // steps left dominate: the games that fell behind issue first (c3, same box, 3 runs each: C = 0
-// 315.5 / 285.3 M at K = 200 / 20, C = 75 334.4 / 285.5 M, C = 150 334.1 / 280.7, C = 400 333.6 / 284.5)
+// 315.5 / 285.3 M at K = 200 / 20, C = 75 334.4 / 285.5 M, C = 150 334.1 / 280.7, C = 400 333.6 / 284.5;
+// later, with balanced placement and the byte image, C = 4000 vs 400: K = 20 kernel 11.95 vs 12.08 us
+// per step over 4 pairs, K = 200 equal — a game one step behind always outranks, units break ties)
 #ifndef MRTS_RANK_C
-#define MRTS_RANK_C 400
+#define MRTS_RANK_C 4000
 #endif
 // 0: multi-step launches keep game g on block g (no balanced placement, A/B builds)
 #ifndef MRTS_BALANCE
