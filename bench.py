@@ -229,8 +229,16 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
     and the process group's watchdog thread then aborts the whole process."""
     native_ok = (mode is not None and dist.get_backend() != "gloo" and not a.po and a.launch == "native"
                  and (mode["fused"] or mode["uni_fused"]))
+    nx = None
     if native_ok:
-        nx = mdist.NativeExchange(env)
+        try:
+            nx = mdist.NativeExchange(env)
+        except Exception as ex:  # e.g. no RCCL library to bind: every rank must take the same path
+            print(f"bench: native exchange unavailable ({ex!r}); torch collectives", file=sys.stderr)
+        flag = torch.tensor([1 if nx is not None else 0], device=env.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        native_ok = bool(flag.item())
+    if native_ok:
 
         def run(first, n):
             if mode["fused"]:

@@ -170,8 +170,14 @@ class NativeExchange:
         L, h = env._h.L, env._h.h
         path = rccl_library_path().encode()
         uid = (ctypes.c_char * 128)()
-        if self.rank == 0:
-            _lib.check(L.mrts_rccl_unique_id(path, uid))
+        # every rank binds RCCL first (drawing an id it may not use) and the ranks agree before anyone
+        # enters the collective init: a rank that failed alone would leave the others waiting in it
+        ok = L.mrts_rccl_unique_id(path, uid) == 0
+        flag = torch.tensor([1 if ok else 0], device=env.device if dist.get_backend(group) != "gloo" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if not bool(flag.item()):
+            why = L.mrts_last_error().decode() if not ok else "another rank"
+            raise RuntimeError(f"RCCL could not be bound on every rank: {why}")
         box = [bytes(uid)]
         dist.broadcast_object_list(box, src=0, group=group)
         uid = (ctypes.c_char * 128).from_buffer_copy(box[0])
