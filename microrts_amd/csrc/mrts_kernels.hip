@@ -156,6 +156,10 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_BAL_MIN_ITER
 #define MRTS_BAL_MIN_ITER 64
 #endif
+// 1: rollout timing events ride on the kernel dispatch (hipExtLaunchKernelGGL); 0: separate records
+#ifndef MRTS_EXT_EVENTS
+#define MRTS_EXT_EVENTS 1
+#endif
 #ifndef MRTS_SIMD_RANK_PO
 #define MRTS_SIMD_RANK_PO 0
 #endif
@@ -5204,7 +5208,16 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
     const bool fixable = hs.n_sp_games == hs.n_games && D.rows == nullptr && hs.utt.K == 79 && hs.utt.ntypes == 7 &&
                          hs.utt.maxAttackRadius == 7 && hs.H == hs.W;
     auto is = [&](int w, int cap, bool po) { return fixable && hs.W == w && hs.CAP == cap && (hs.partial_obs != 0) == po; };
+#if MRTS_EXT_EVENTS
 #define LAUNCH(kern, g_, b_, l_, s_, ...) hipExtLaunchKernelGGL(kern, g_, b_, (uint32_t)(l_), s_, e0, e1, 0, __VA_ARGS__)
+#else  // events as separate records around the launch (A/B builds)
+#define LAUNCH(kern, g_, b_, l_, s_, ...)                                 \
+    do {                                                                  \
+        if (e0) (void)hipEventRecord(e0, s_);                             \
+        hipLaunchKernelGGL(kern, g_, b_, (uint32_t)(l_), s_, __VA_ARGS__); \
+        if (e1) (void)hipEventRecord(e1, s_);                             \
+    } while (0)
+#endif
     switch (mode) {
         case MODE_STEP:
             if (D.n_iter > 1 && is(16, 320, false)) LAUNCH((k_env<MODE_STEP, 16, 320, false, true>), grid, block, lds, stream, D.state, ds, D);
