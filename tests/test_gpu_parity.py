@@ -1050,3 +1050,14 @@ def test_host_mask_views_match_copies():
             c = vc.getMasks(0, dtype=dt)
             assert v.dtype == dt and v.shape == c.shape and np.array_equal(v, c), f"step {step} {dt}"
     vc.close()
+
+
+def test_full_obs_without_byte_image(tmp_path):
+    """16x16 full observability renders through the LDS byte image only when every plane value fits a
+    byte (KDyn.obs_img); a resource pile of 300 sends the same maps through the cell-map gather — both
+    against the oracle, every step (observations, rewards, dones, masks, states every 10 steps)."""
+    src = open("maps/16x16/basesWorkers16x16.xml").read()
+    assert 'resources="25"' in src
+    big = tmp_path / "bigpile16x16.xml"
+    big.write_text(src.replace('resources="25"', 'resources="300"', 1))
+    _rollout([str(big)] * 8, 8, steps=120)
