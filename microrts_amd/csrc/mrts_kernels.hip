@@ -508,6 +508,9 @@ struct Game {
     // helper-wave launch (k_env HELP): this iteration's uniform rows, drawn by the helper wave,
     // packed (packFwd) per [player slot][cell]; null = draw them here (fetchRow)
     const uint32_t* helpRows = nullptr;
+    // helper-wave launch, partially observable (k_env HELP && FPO): where writeMasksLanes leaves this
+    // step's mask records, policy rows and vacated cells for the helper to store (null = store them here)
+    uint32_t* recOut = nullptr;
     int maxProd0, maxProd1, sumProd0, sumProd1;
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
@@ -3083,6 +3086,44 @@ struct Game {
         wsync();
     }
     DEV bool poFast2() const { return (W & 3) == 0 && W <= 32 && H <= 32 && nu <= 64 && U.maxSight <= 15; }
+    // the helper's part of a packed step's masks (writeMasksLanes with recOut): each own idle unit's
+    // mask record (79 bytes from its 3 bit words) and fused-policy row, and the zero record + zero row
+    // of every vacated cell — the same bytes the game wave would have stored.  Lane l = threadIdx.x - 64.
+    DEV void storeRecordsHelp(const uint32_t* rb) {
+        const int l = (int)threadIdx.x - 64;
+        const int total = HW * K, slot0 = 2 * g;
+        const uint8_t* mbase = D.masks + (size_t)slot0 * total;
+        const __amdgpu_buffer_rsrc_t mrs = bufRsrc((void*)mbase, (uint32_t)(2 * total));
+        if (!(uniu(rb[5 * 64]) >> 31)) return;  // the game wave stored this step's masks itself
+        const uint32_t e = rb[l];
+        if (e != ~0u) {
+            const int si = (int)(e >> 16), c = (int)(e & 0xFFFFu), slot = slot0 + si;
+            const uint64_t lo = (uint64_t)rb[64 + l] | ((uint64_t)rb[128 + l] << 32);
+            const uint32_t w2 = rb[192 + l];
+            if (SC1_MASK) storeRecordSc1(mrs, mbase, (uint32_t)(si * total + c * K), lo, w2);
+            else storeRecord(D.masks + (size_t)slot * total + (size_t)c * K, lo, w2);
+            if (D.pol_actions && D.pol_delta) {
+                int32_t a[7];
+                unpackFwd(rb[256 + l], a);
+                int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
+                st4u<WT_MASK>(dst, a[0], a[1], a[2], a[3]);
+                st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
+            }
+        }
+        const int ngone = (int)(uniu(rb[5 * 64]) & 0xFFFFu);
+        const uint16_t* gl = (const uint16_t*)(rb + 5 * 64 + 1);
+        if (l < ngone) {
+            const uint32_t ge = gl[l];
+            const int slot = slot0 + (int)(ge >> 15), cz = (int)(ge & 0x7FFFu);
+            if (SC1_MASK) storeRecordSc1(mrs, mbase, (uint32_t)((slot - slot0) * total + cz * K), 0ull, 0u);
+            else storeRecord(D.masks + (size_t)slot * total + (size_t)cz * K, 0ull, 0u);
+            if (D.pol_actions && D.pol_delta) {
+                int32_t* dst = D.pol_actions + ((size_t)slot * HW + cz) * 7;
+                st4u<WT_MASK>(dst, 0, 0, 0, 0);
+                st3u<WT_MASK>(dst + 4, 0, 0, 0);
+            }
+        }
+    }
     // Helper-wave launch, partially observable self-play (k_env HELP && FPO, BASELINE c5): the game
     // wave hands this step's render inputs to the helper wave instead of rendering (writeObsPOFast2's
     // unit pass reads, per unit slot < 64: the unit word, hp | resources, the snapshot byte, and the
@@ -4043,9 +4084,16 @@ struct Game {
             as[l] = (int32_t)w1;
             ua[l] = w2 & 0xFFFFu;
         }
+        if (recOut && si < 0) recOut[l] = ~0u;  // (no record from this lane)
         if (si >= 0) {
             const int slot = slot0 + si;
             const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
+            if (recOut) {  // the helper expands and stores it (storeRecordsHelp)
+                recOut[l] = ((uint32_t)si << 16) | (uint32_t)c;
+                recOut[64 + l] = w0;
+                recOut[128 + l] = w1;
+                recOut[192 + l] = w2;
+            } else
 #ifdef MRTS_ABLATE
             if (!ab(AB_SKIP_RECORD))
 #endif
@@ -4067,9 +4115,13 @@ struct Game {
 #endif
                 sampleBitsRaw(D.pol_seed, polStep, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
                               (uint64_t)(w2 >> 1), c, a);
-                int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
-                st4u<WT_MASK>(dst, a[0], a[1], a[2], a[3]);
-                st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
+                if (recOut) {
+                    recOut[256 + l] = packFwd(a);
+                } else {
+                    int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
+                    st4u<WT_MASK>(dst, a[0], a[1], a[2], a[3]);
+                    st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
+                }
                 if (fwdW) {
                     lfwd = packFwd(a);  // the next iteration of a multi-step launch decodes from it
                     if (lastIt) st1<WT_STATE>(st() + stateFwdOff(CAP, HW) + l, (int32_t)lfwd);  // the next launch's
@@ -4083,6 +4135,18 @@ struct Game {
         const int n = __popc(gone);
         const int incl = wave_incl_sum(n);
         const int ngone = rl(incl, 63);
+        if (recOut) {  // the vacated cells go to the helper too (up to 64 of them; more: stored here below)
+            uint16_t* gl = (uint16_t*)(recOut + 5 * 64 + 1);
+            if (ngone <= 64) {
+                int k = incl - n;
+                for (uint32_t d = gone; d; d &= d - 1, k++) gl[k] = (uint16_t)((i << 15) | (32 * w + __builtin_ctz(d)));
+            }
+            if (l == 0) recOut[5 * 64] = (1u << 31) | (uint32_t)(ngone <= 64 ? ngone : 0);  // (bit 31: records valid)
+            if (ngone <= 64) {
+                wsync();
+                return;
+            }
+        }
         if (ngone == 0) {
             wsync();
             return;
@@ -4370,10 +4434,15 @@ DEV void drainStores() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // s_waitcnt vmc
 // helper's view-0 sight rows [2][H] (the snapshot's rows before the render) and the snapshot bytes
 // [64] at KDyn.help_off; the packs [2][5][64] words and the per-step occupant map (u8 per cell) in the
 // game's `scell` area, which only the general render uses.
+// After the snapshot bytes, at PO_HELP_REC words: the game's mask records of a packed step
+// (writeMasksLanes with recOut: [5][64] words + a count word + 64 u16 vacated cells), stored by the
+// helper after S_k (S_last after the last step), so the game wave issues none of those stores.
+constexpr int PO_HELP_REC = 8 + 2 * 32 + 16, PO_HELP_REC_WORDS = 5 * 64 + 1 + 32;
 DEV void helperLoopPO(Game& G, uint32_t* hdr, int niter) {
     uint32_t* const rows0 = hdr + 8;
     uint8_t* const hsnap = (uint8_t*)(rows0 + 2 * G.H);
     uint8_t* const hcell = (uint8_t*)(G.scell + 2 * 5 * 64);
+    uint32_t* const recs = hdr + PO_HELP_REC;
     G.helperLane();
     const int l = G.lid();
     if (MRTS_HELPER_PRIO) __builtin_amdgcn_s_setprio(3);  // the games wait for it at the handoff barriers
@@ -4388,6 +4457,8 @@ DEV void helperLoopPO(Game& G, uint32_t* hdr, int niter) {
                 ldsBarrier();  // S_k: the next step's snapshot bytes are ready
             }
             G.renderPOPacked(pk, ph, rows0, hcell, k == niter - 1);
+            if (k + 1 == niter) ldsBarrier();  // S_last: the game's masks of the last step are out
+            G.storeRecordsHelp(recs);  // step k's mask records and policy rows (written before S_k)
         } else if (f & 8u) {
             // the game's live state, as its own writeObsPO call would see it (the general render
             // overwrites `scell`, so the pack's record words are taken first)
@@ -4732,6 +4803,10 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
     PHASE(6);
     if (MODE == MODE_STEP && !freshObs && G.deaths) G.compact();
     PHASE(7);
+    if (HELP && FPO) {  // a packed step's mask records go to the helper (storeRecordsHelp)
+        G.recOut = poHelpFlags == 4u ? poHelpHdr + PO_HELP_REC : nullptr;
+        if (poHelpFlags == 4u && G.lid() == 0) G.recOut[5 * 64] = 0u;  // none, unless writeMasksLanes hands them over
+    }
     if (D.masks && external) {
         const int nsl = selfplay ? 2 : 1;
         if (MRTS_LIKELY(D.mask_delta && G.nu <= 64 && nsl * maskWords(G.HW) <= 64 && G.K <= 96)) {
@@ -4757,6 +4832,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* 
         wsync();
         G.poRecordSnaps(selfplay ? 3u : (1u << side));
     }
+    if (HELP && FPO && poPacked && it == niter - 1) ldsBarrier();  // S_last (helperLoopPO)
     }  // iterations
     if (ranked && lane_id() == 0) srank.row[srank.me] = 0u;  // this game no longer competes on its SIMD
     if (MODE != MODE_MASKS) {
@@ -5232,7 +5308,7 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
                 // c5's partially observable rollout: a helper wave per game renders the views (helperLoopPO)
                 KDyn D2 = D;
                 D2.help_off = (int32_t)((lds + 15) & ~(size_t)15);
-                LAUNCH((k_env<MODE_STEP, 32, 320, true, true, true>), grid, dim3(128), (size_t)D2.help_off + 4 * (8 + 2 * 32) + 64,
+                LAUNCH((k_env<MODE_STEP, 32, 320, true, true, true>), grid, dim3(128), (size_t)D2.help_off + 4 * (PO_HELP_REC + PO_HELP_REC_WORDS),
                                    stream, D.state, ds, D2);
             } else if (D.n_iter > 1 && is(32, 320, true)) LAUNCH((k_env<MODE_STEP, 32, 320, true, true>), grid, block, lds, stream, D.state, ds, D);
             else if (is(16, 320, false)) LAUNCH((k_env<MODE_STEP, 16, 320, false>), grid, block, lds, stream, D.state, ds, D);
