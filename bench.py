@@ -505,6 +505,11 @@ def main():
     # kernel time — fence-free events around it inside the timed window
     multi = native and ((fused and env.fused_multi_step) or (uniform and mode["uni_fused"] and env.multi_step_capable))
     roll_ev = (_FenceFreeEvent(), _FenceFreeEvent()) if multi and event_kind.startswith("hipEvent") else None
+    if roll_ev is not None and a.warmup > 0:
+        # the warmup launch carries events too: the first event-carrying dispatch of a process pays a
+        # one-time runtime cost (~15 us), which belongs to the warmup, not to the window
+        warm_ev = (_FenceFreeEvent(), _FenceFreeEvent())
+        env.set_rollout_events(warm_ev[0].h, warm_ev[1].h)
     run_steps(a.burnin, a.warmup)  # the W untimed warmup steps, immediately before the window
     if roll_ev is not None:  # the library records them around the window's launch (mrts_set_rollout_events)
         env.set_rollout_events(roll_ev[0].h, roll_ev[1].h)
