@@ -82,6 +82,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather-window", action="store_true",
                     help="skip the second timed window with the per-step RCCL observation all-gather (with_gather)")
+    ap.add_argument("--gather-timeout", type=float, default=180.0,
+                    help="seconds the with_gather window may take on a rank before every rank gives it up: rank 0 "
+                         "prints the line with with_gather = {error} and all ranks exit 0 (a hung collective must "
+                         "not cost the headline line)")
     ap.add_argument("--no-compare", action="store_true", help="skip the other policy form's comparison window")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc-traffic", type=float, default=None,
@@ -811,12 +815,28 @@ def main():
         if not use_pg:
             out["with_gather"] = {"error": f"no process group: {pg_error}"}
         else:
+            import threading
+
+            def give_up():  # a collective that never completes (the exchange has no other way out)
+                print(f"bench: exchange window exceeded {a.gather_timeout:.0f} s; giving it up", file=sys.stderr)
+                if rank == 0:
+                    out["with_gather"] = {"error": f"timed out after {a.gather_timeout:.0f} s"}
+                    sys.stdout.flush()
+                    os.write(json_fd, (json.dumps(out) + "\n").encode())
+                sys.stderr.flush()
+                os._exit(0)
+
+            watchdog = threading.Timer(a.gather_timeout, give_up)
+            watchdog.daemon = True
+            watchdog.start()
             try:
                 out["with_gather"] = gather_window(env, a, xg, one_step, base + 3 * a.steps + 20, E * world, world,
                                                    mdist, torch, dist, mode)
             except Exception as ex:  # the headline line must survive a failed exchange window
                 print(f"bench: exchange window failed: {ex!r}", file=sys.stderr)
                 out["with_gather"] = {"error": repr(ex)}
+            finally:
+                watchdog.cancel()
             assert not env.error_flags().any()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin, uniform, po=a.po)
