@@ -163,6 +163,9 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SIMD_RANK_PO
 #define MRTS_SIMD_RANK_PO 0
 #endif
+#ifndef MRTS_SAMPLE_UNIFIED
+#define MRTS_SAMPLE_UNIFIED 1
+#endif
 #ifndef MRTS_HELPER_PRIO
 #define MRTS_HELPER_PRIO 0
 #endif
@@ -368,6 +371,22 @@ DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes
     const int t = pickBit(ctr[0], field(1, 6), 6);
     if (t < 0) return;
     a[0] = t;
+#if MRTS_SAMPLE_UNIFIED
+    // the parameter of type t from ONE pick over that type's field (move / harvest / return / produce
+    // direction: 4 slots at 7 + 4 (t - 1); attack: the K - 23 - ntypes slots after the unit types), not
+    // one pick per case: the lanes of a wave hold several types, and a switch runs its cases one after
+    // the other.  Same words of the same Philox block, same picks: identical rows.
+    if (t > 0) {
+        const int off = t == 5 ? 23 + ntypes : 3 + 4 * t, n = t == 5 ? K - 23 - ntypes : 4;
+        const int pv = pickBit(ctr[1], field(off, n), n);
+        a[1] = t == 1 ? pv : 0;
+        a[2] = t == 2 ? pv : 0;
+        a[3] = t == 3 ? pv : 0;
+        a[4] = t == 4 ? pv : 0;
+        a[6] = t == 5 ? pv : 0;
+    }
+    if (t == 4) a[5] = pickBit(ctr[2], field(23, ntypes), ntypes);
+#else
     switch (t) {
         case 1: a[1] = pickBit(ctr[1], field(7, 4), 4); break;
         case 2: a[2] = pickBit(ctr[1], field(11, 4), 4); break;
@@ -381,6 +400,7 @@ DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes
             a[6] = pickBit(ctr[1], field(off, n), n);
         } break;
     }
+#endif
 }
 
 // Unmasked uniform random row (BASELINE config c2) of cell c of slot id slotId:
@@ -4476,8 +4496,10 @@ DEV void helperLoopPO(Game& G, uint32_t* hdr, int niter) {
 template <int MODE, int FIX, int FCAP = 0, bool FPO = false, bool MULTI = false, bool HELP = false>
 // stateArg and PS lead the argument list so that kernarg preloading (-amdgpu-kernarg-preload-count,
 // Makefile) hands them over in SGPRs: the first memory round (state block, unit-type table) issues
-// without waiting for a scalar load of the kernel arguments.
-__global__ __launch_bounds__(HELP ? 128 : 64, HELP ? 4 : 1) void k_env(int32_t* __restrict__ stateArg, const KStatic* __restrict__ PS, KDyn D) {
+// without waiting for a scalar load of the kernel arguments.  The 16x16 instances (c3: four games per
+// SIMD, at the 128-VGPR edge) and the helper instances are held to 4 waves per SIMD: one VGPR more
+// silently halves nothing but drops a quarter of the games into a second dispatch round (1.7x slower).
+__global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void k_env(int32_t* __restrict__ stateArg, const KStatic* __restrict__ PS, KDyn D) {
     extern __shared__ __align__(16) uint8_t smem[];
     if (HELP && !FPO && threadIdx.x >= 64) {
         helperLoop(D, smem, (int)blockIdx.x, D.n_iter);
