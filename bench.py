@@ -222,6 +222,21 @@ def cpu_baseline_c1(map_path, runs=5, steps=200_000, burnin=1000):
             "runs": rates, "host": host_info()}
 
 
+def run_with_deadline(fn, seconds, on_timeout):
+    """fn() with a watchdog: if it has not returned after `seconds`, on_timeout() runs on the watchdog
+    thread (bench.py's: print the line without the window, exit every rank).  The timer is cancelled
+    when fn returns or raises."""
+    import threading
+
+    watchdog = threading.Timer(seconds, on_timeout)
+    watchdog.daemon = True
+    watchdog.start()
+    try:
+        return fn()
+    finally:
+        watchdog.cancel()
+
+
 def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, dist, mode=None):
     """K steps with the observation all-gather after every step, one step launch per step (a per-step
     consumer cannot use multi-step launches); the barrier + synchronize bracket and max over ranks of
@@ -815,8 +830,6 @@ def main():
         if not use_pg:
             out["with_gather"] = {"error": f"no process group: {pg_error}"}
         else:
-            import threading
-
             def give_up():  # a collective that never completes (the exchange has no other way out)
                 print(f"bench: exchange window exceeded {a.gather_timeout:.0f} s; giving it up", file=sys.stderr)
                 if rank == 0:
@@ -826,17 +839,13 @@ def main():
                 sys.stderr.flush()
                 os._exit(0)
 
-            watchdog = threading.Timer(a.gather_timeout, give_up)
-            watchdog.daemon = True
-            watchdog.start()
             try:
-                out["with_gather"] = gather_window(env, a, xg, one_step, base + 3 * a.steps + 20, E * world, world,
-                                                   mdist, torch, dist, mode)
+                out["with_gather"] = run_with_deadline(
+                    lambda: gather_window(env, a, xg, one_step, base + 3 * a.steps + 20, E * world, world, mdist, torch,
+                                          dist, mode), a.gather_timeout, give_up)
             except Exception as ex:  # the headline line must survive a failed exchange window
                 print(f"bench: exchange window failed: {ex!r}", file=sys.stderr)
                 out["with_gather"] = {"error": repr(ex)}
-            finally:
-                watchdog.cancel()
             assert not env.error_flags().any()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin, uniform, po=a.po)
