@@ -770,6 +770,36 @@ def test_multi_step_rollout_matches_single_launches(mp, n_sp, max_steps, po):
     B.close()
 
 
+def test_multi_step_uniform_po_matches_single_launches():
+    """The c5 helper-wave instance under the uniform rollout (mrts_rollout_uniform_dev: no masks, so
+    the game wave hands the helper no mask records): multi-step launches = one launch per step, bit for
+    bit — observations, rewards, dones, the drawn rows and every game's state."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mp, n_sp = "maps/BWDistantResources32x32.xml", 32
+    mk = lambda: DeviceVecEnv(n_sp, 0, 200, [mp] * n_sp, seed=7, partial_obs=True, max_units=256)  # noqa: E731
+    A, B = mk(), mk()
+    A.set_multi_step(False)
+    assert B.multi_step_capable
+    for e in (A, B):
+        e.reset()
+    k = 0
+    for n in (1, 3, 64, 180):
+        A.rollout_uniform(SEED, k, n)
+        B.rollout_uniform(SEED, k, n)
+        k += n
+        A.synchronize()
+        B.synchronize()
+        for name in ("obs", "reward", "done", "actions"):
+            assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
+        for s in range(0, n_sp, 2):
+            assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
+    assert not A.error_flags().any() and not B.error_flags().any()
+    A.close()
+    B.close()
+
+
 def _crowded_32x32(tmp_path, per_player):
     """BWDistantResources32x32 plus `per_player` extra Workers per player:
     the map file is written by the test (the reference's XML layout, PhysicalGameState.java:700-726)."""
