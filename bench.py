@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-gather-window", action="store_true",
                     help="skip the second timed window with the per-step RCCL observation all-gather (with_gather)")
+    ap.add_argument("--no-exchange-u8", dest="exchange_u8", action="store_false",
+                    help="exchange the observation as int16 even where every value fits a byte")
     ap.add_argument("--gather-timeout", type=float, default=180.0,
                     help="seconds the with_gather window may take on a rank before every rank gives it up: rank 0 "
                          "prints the line with with_gather = {error} and all ranks exit 0 (a hung collective must "
@@ -251,12 +253,14 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
     nx = None
     if native_ok:
         try:
-            nx = mdist.NativeExchange(env)
+            # uint8 transport where every observation value fits a byte (c3's 16x16 maps), else int16
+            nx = mdist.NativeExchange(env, u8="auto" if a.exchange_u8 else False)
         except Exception as ex:  # e.g. no RCCL library to bind: every rank must take the same path
             print(f"bench: native exchange unavailable ({ex!r}); torch collectives", file=sys.stderr)
         flag = torch.tensor([1 if nx is not None else 0], device=env.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         native_ok = bool(flag.item())
+    u8 = bool(native_ok and nx.u8)
     if native_ok:
 
         def run(first, n):
@@ -305,10 +309,11 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
     return {
         "value": total_games * a.steps / t,
         "ms_per_step": 1e3 * t / a.steps,
-        "collective": "all-gather of the int16 observation tensor every step (RCCL, ring over xGMI), comm stream "
-                      "overlapping the next step; " + ("int16 written by the step kernel" if not a.po else
-                                                       "narrowing copy (partially observable planes)"),
-        "payload_bytes_per_rank": env.obs.numel() * 2,  # int16 observation of one rank's slots, per step
+        "collective": f"all-gather of the {'uint8' if u8 else 'int16'} observation tensor every step (RCCL, ring over "
+                      "xGMI), comm stream overlapping the next step; " +
+                      ("uint8 written by the step kernel (every value < 256, checked at create)" if u8 else
+                       "int16 written by the step kernel" if not a.po else "narrowing copy (partially observable planes)"),
+        "payload_bytes_per_rank": env.obs.numel() * (1 if u8 else 2),  # one rank's observation, per step
         "launch": "one step launch per step (a per-step consumer cannot use multi-step launches); " + how,
     }
 

@@ -478,6 +478,8 @@ struct mrts_env {
     // after an invalidation) and the per-game render records (PO handles on delta-capable maps)
     int obsDelta = 0;
     int16_t* obs16 = nullptr;  // mrts_set_obs16: int16 copy of each observation write (full observability)
+    uint8_t* obs8 = nullptr;   // the exchange's uint8 transport (mrts_set_exchange_bytes(env, 1))
+    int exBytes = 2;           // bytes per value of the exchanged observation: 2 (int16) or 1 (uint8)
     int multiStep = 1;  // mrts_rollout_fused_dev may run several steps per launch (mrts_set_multi_step)
     const int32_t* lastObsPtr = nullptr;
     int32_t* d_poPrev = nullptr;
@@ -528,6 +530,7 @@ struct mrts_env {
     // host-pointer API is always persistent
     void prepObs(KDyn& D) {
         D.obs16 = D.obs ? obs16 : nullptr;
+        D.obs8 = D.obs ? obs8 : nullptr;
         D.obs_delta = (D.obs && D.obs == lastObsPtr && (obsDelta || D.obs == d_obs)) ? 1 : 0;
         D.po_prev = D.obs ? d_poPrev : nullptr;
         D.po_words = poWords;
@@ -1219,14 +1222,16 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, int16_t* d_send0, int16_t* d_s
     HIPCHK(hipSetDevice(env->device));
     hipStream_t s = pickStream(env, stream);
     int16_t* send[2] = {d_send0, d_send1};
-    const size_t bytes = (size_t)env->nSlots * env->C * env->HW * 2;
+    const bool u8 = env->exBytes == 1;  // the buffers then hold uint8 values (mrts_set_exchange_bytes)
+    const size_t bytes = (size_t)env->nSlots * env->C * env->HW * (u8 ? 1 : 2);
     bool pending[2] = {false, false};
     int16_t* const saved = env->obs16;
     try {
         for (int32_t k = 0; k < n_steps; k++) {
             const int b = k & 1;
             if (pending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
-            env->obs16 = send[b];
+            if (u8) env->obs8 = (uint8_t*)send[b];
+            else env->obs16 = send[b];
             step(k);
             HIPCHK(hipEventRecord(env->exReady[b], s));
             HIPCHK(hipStreamWaitEvent(env->exStream, env->exReady[b], 0));
@@ -1238,9 +1243,11 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, int16_t* d_send0, int16_t* d_s
             if (pending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
     } catch (...) {
         env->obs16 = saved;
+        env->obs8 = nullptr;
         throw;
     }
     env->obs16 = saved;
+    env->obs8 = nullptr;
 }
 }  // namespace
 extern "C" {
@@ -1363,6 +1370,21 @@ int mrts_set_obs_delta(mrts_env* env, int32_t on) {
     if (!env) return fail(Fail{-EINVAL, "null handle"});
     env->obsDelta = on ? 1 : 0;
     env->lastObsPtr = nullptr;
+    return 0;
+}
+
+int mrts_set_exchange_bytes(mrts_env* env, int32_t bytes_per_value) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    if (bytes_per_value == 2) {
+        env->exBytes = 2;
+        return 0;
+    }
+    if (bytes_per_value != 1) return fail(Fail{-EINVAL, "bytes per value: 1 or 2"});
+    // the uint8 transport is written by the byte-image render only: 16x16 full observability whose
+    // every value fits a byte (checked at create over the maps and the unit-type table)
+    if (env->partialObs || env->HW != 256 || !env->obsImg)
+        return fail(Fail{-ENOTSUP, "uint8 exchange: 16x16 full observability with every value < 256 only"});
+    env->exBytes = 1;
     return 0;
 }
 

@@ -2552,6 +2552,23 @@ struct Game {
                 else st4<WT_OBS>(o0 + off, w[0], w[1], w[2], w[3]);
             }
         }
+        if (MRTS_UNLIKELY(D.obs8 != nullptr)) {  // the uint8 transport (mrts_set_exchange_bytes): every plane
+            if (!firstIt)
+#pragma unroll
+                for (int j = 0; j < 4; j++) v[5][j] = cell[c4 + j] == WALL ? 1 : 0;
+            uint8_t* b0 = D.obs8 + (size_t)slot0 * D.C * HW;
+            for (int i = 0; i < nslots; i++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int x = (i && q == 2 && v[q][j]) ? 3 - v[q][j] : v[q][j];  // the other player's owners
+                        w |= (uint32_t)x << (8 * j);
+                    }
+                    *(uint32_t*)(b0 + (size_t)(i * D.C + q) * HW + c4) = w;
+                }
+        }
         if (MRTS_UNLIKELY(D.obs16 != nullptr)) {  // the int16 transport copy (mrts_set_obs16): every plane
             if (!firstIt)
 #pragma unroll

@@ -160,7 +160,10 @@ class NativeExchange:
     handle's own stream overlapping step t + 1, no Python between steps and no graph capture.  Full
     observability; every rank of `group` must construct it (ncclCommInitRank is collective)."""
 
-    def __init__(self, env, group=None):
+    def __init__(self, env, group=None, u8=False):
+        """u8: exchange the observation as uint8 (mrts_set_exchange_bytes: half the bytes) when the
+        handle allows it (16x16 full observability, every value < 256), else int16; "auto" = try.
+        Every rank decides the same way (the handles are built alike)."""
         import ctypes
 
         from microrts_amd import _lib
@@ -182,9 +185,16 @@ class NativeExchange:
         dist.broadcast_object_list(box, src=0, group=group)
         uid = (ctypes.c_char * 128).from_buffer_copy(box[0])
         _lib.check(L.mrts_exchange_init(h, path, self.world, self.rank, uid))
+        self.u8 = False
+        if u8:
+            rc = L.mrts_set_exchange_bytes(h, 1)
+            if rc != 0 and u8 != "auto":
+                _lib.check(rc)
+            self.u8 = rc == 0
+        dt = torch.uint8 if self.u8 else torch.int16
         shape = tuple(env.obs.shape)
-        self.send = [torch.zeros(shape, dtype=torch.int16, device=env.device) for _ in range(2)]
-        self.recv = torch.zeros((self.world,) + shape, dtype=torch.int16, device=env.device)
+        self.send = [torch.zeros(shape, dtype=dt, device=env.device) for _ in range(2)]
+        self.recv = torch.zeros((self.world,) + shape, dtype=dt, device=env.device)
 
     def rollout_fused(self, seed, first_next_step, n_steps):
         """env.rollout_fused(...) with every step's observation all-gathered into self.recv."""

@@ -250,12 +250,15 @@ def _exchange_env(env, world=1, rank=0):
     return path, uid
 
 
-@pytest.mark.parametrize("mp,uniform", [("maps/16x16/basesWorkers16x16.xml", False), ("maps/8x8/basesWorkers8x8.xml", True)])
-def test_native_exchange_one_rank(mp, uniform):
+@pytest.mark.parametrize("mp,uniform,u8", [("maps/16x16/basesWorkers16x16.xml", False, False),
+                                           ("maps/16x16/basesWorkers16x16.xml", False, True),
+                                           ("maps/8x8/basesWorkers8x8.xml", True, False)])
+def test_native_exchange_one_rank(mp, uniform, u8):
     """mrts_rollout_{fused,uniform}_exchange_dev on a one-rank RCCL communicator: every output equals the
     same rollout with one launch per step and no exchange (observations, rewards, dones, masks, next
     actions, states), the last step's int16 observation arrived in recv[0], and the send buffers alternate
-    (the last step's in send[(n - 1) % 2]); a second mrts_exchange_init and a partially observable
+    (the last step's in send[(n - 1) % 2]); with mrts_set_exchange_bytes(1) the same as uint8 (refused
+    on a shape the byte render does not write); a second mrts_exchange_init and a partially observable
     handle are refused."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
@@ -269,8 +272,13 @@ def test_native_exchange_one_rank(mp, uniform):
         if not uniform:
             e.random_policy(SEED, 0)
     path, uid = _exchange_env(B)
-    send = [torch.zeros(tuple(B.obs.shape), dtype=torch.int16, device=B.device) for _ in range(2)]
-    recv = torch.zeros((1,) + tuple(B.obs.shape), dtype=torch.int16, device=B.device)
+    dt = torch.uint8 if u8 else torch.int16
+    if u8:
+        assert B._h.L.mrts_set_exchange_bytes(B._h.h, 1) == 0
+    elif "8x8" in mp:
+        assert B._h.L.mrts_set_exchange_bytes(B._h.h, 1) != 0  # no byte render on 8x8
+    send = [torch.zeros(tuple(B.obs.shape), dtype=dt, device=B.device) for _ in range(2)]
+    recv = torch.zeros((1,) + tuple(B.obs.shape), dtype=dt, device=B.device)
     k = 0
     for n in (1, 2, 7, 120):
         if uniform:
@@ -286,11 +294,13 @@ def test_native_exchange_one_rank(mp, uniform):
             assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
         for s in range(0, n_sp, 2):
             assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
-        o16 = B.obs.to(torch.int16)
-        assert torch.equal(recv[0], o16), f"recv after {k}"
-        assert torch.equal(send[(n - 1) % 2], o16), f"send buffer after {k}"
+        assert int(B.obs.max()) < 256 and int(B.obs.min()) >= 0
+        ox = B.obs.to(dt)
+        assert torch.equal(recv[0], ox), f"recv after {k}"
+        assert torch.equal(send[(n - 1) % 2], ox), f"send buffer after {k}"
     assert B._h.L.mrts_exchange_init(B._h.h, path, 1, 0, uid) != 0  # already initialised
     P = DeviceVecEnv(8, 0, 300, ["maps/BWDistantResources32x32.xml"] * 8, seed=1, partial_obs=True, max_units=256)
+    assert P._h.L.mrts_set_exchange_bytes(P._h.h, 1) != 0
     P.reset()
     P.random_policy(SEED, 0)
     _exchange_env(P)
