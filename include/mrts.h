@@ -198,8 +198,9 @@ int mrts_rollout_fused_exchange_dev(mrts_env* env, int32_t* d_actions, const int
                                     int16_t* d_recv, void* stream);
 /* Bytes per exchanged observation value: 2 (int16, the default) or 1 (uint8: the send / recv buffers
  * of the two calls above and below then hold uint8 [..][n_slots][C][H][W], half the all-gather's bytes).
- * uint8 needs a handle whose every observation value fits a byte — 16x16 full observability, with the
- * maps' hp / resources and the unit-type table checked at mrts_create — else -ENOTSUP. */
+ * uint8 needs a handle whose every observation value fits a byte — full observability on 16x16 maps or
+ * maps of at most 64 cells, with the maps' hp / resources and the unit-type table checked at
+ * mrts_create — else -ENOTSUP. */
 int mrts_set_exchange_bytes(mrts_env* env, int32_t bytes_per_value);
 /* The same for BASELINE config c2's unmasked uniform rollout (mrts_rollout_uniform_dev, fused form). */
 int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,

@@ -1380,10 +1380,11 @@ int mrts_set_exchange_bytes(mrts_env* env, int32_t bytes_per_value) {
         return 0;
     }
     if (bytes_per_value != 1) return fail(Fail{-EINVAL, "bytes per value: 1 or 2"});
-    // the uint8 transport is written by the byte-image render only: 16x16 full observability whose
-    // every value fits a byte (checked at create over the maps and the unit-type table)
-    if (env->partialObs || env->HW != 256 || !env->obsImg)
-        return fail(Fail{-ENOTSUP, "uint8 exchange: 16x16 full observability with every value < 256 only"});
+    // the uint8 transport is written by the 16x16 byte-image render and the one-cell-per-lane render of
+    // maps of <= 64 cells: full observability whose every value fits a byte (checked at create over the
+    // maps and the unit-type table)
+    if (env->partialObs || !(env->HW == 256 || env->HW <= 64) || !env->obsImg)
+        return fail(Fail{-ENOTSUP, "uint8 exchange: full observability on 16x16 or <= 64-cell maps, every value < 256"});
     env->exBytes = 1;
     return 0;
 }

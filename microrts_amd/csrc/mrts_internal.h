@@ -157,7 +157,8 @@ struct KDyn {
     // of the observation exchange, mrts_set_obs16); null = off
     int16_t* obs16;
     // the uint8 form of that transport (mrts_set_exchange_bytes(env, 1)): written only by the 16x16
-    // byte-image render (writeObsFullImg), every value < 256; null = off
+    // byte-image render (writeObsFullImg) and the one-cell-per-lane render of maps of <= 64 cells,
+    // every value < 256; null = off
     uint8_t* obs8;
     // multi-step launch (mrts_rollout_fused_dev): > 1 = this launch runs n_iter consecutive fused steps
     // per game (pol_step, pol_step + 1, ...), the state kept in LDS in between (specialised

@@ -2636,6 +2636,13 @@ struct Game {
                         for (int q = 0; q < 6; q++)
                             h0[(size_t)(i * D.C + q) * HW + c] = (int16_t)((i && q == 2 && v[2]) ? 3 - v[2] : v[q]);
                 }
+                if (MRTS_UNLIKELY(D.obs8 != nullptr)) {  // the uint8 transport (mrts_set_exchange_bytes)
+                    uint8_t* b0 = D.obs8 + (size_t)slot0 * D.C * HW;
+                    for (int i = 0; i < nslots; i++)
+#pragma unroll
+                        for (int q = 0; q < 6; q++)
+                            b0[(size_t)(i * D.C + q) * HW + c] = (uint8_t)((i && q == 2 && v[2]) ? 3 - v[2] : v[q]);
+                }
             }
         } else if ((HW & 3) == 0) {
             for (int c4 = 4 * lid(); c4 < HW; c4 += 256) {

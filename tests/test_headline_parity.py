@@ -252,13 +252,14 @@ def _exchange_env(env, world=1, rank=0):
 
 @pytest.mark.parametrize("mp,uniform,u8", [("maps/16x16/basesWorkers16x16.xml", False, False),
                                            ("maps/16x16/basesWorkers16x16.xml", False, True),
-                                           ("maps/8x8/basesWorkers8x8.xml", True, False)])
+                                           ("maps/8x8/basesWorkers8x8.xml", True, False),
+                                           ("maps/8x8/basesWorkers8x8.xml", True, True)])
 def test_native_exchange_one_rank(mp, uniform, u8):
     """mrts_rollout_{fused,uniform}_exchange_dev on a one-rank RCCL communicator: every output equals the
     same rollout with one launch per step and no exchange (observations, rewards, dones, masks, next
     actions, states), the last step's int16 observation arrived in recv[0], and the send buffers alternate
     (the last step's in send[(n - 1) % 2]); with mrts_set_exchange_bytes(1) the same as uint8 (refused
-    on a shape the byte render does not write); a second mrts_exchange_init and a partially observable
+    on a shape no uint8 render writes); a second mrts_exchange_init and a partially observable
     handle are refused."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
@@ -275,8 +276,8 @@ def test_native_exchange_one_rank(mp, uniform, u8):
     dt = torch.uint8 if u8 else torch.int16
     if u8:
         assert B._h.L.mrts_set_exchange_bytes(B._h.h, 1) == 0
-    elif "8x8" in mp:
-        assert B._h.L.mrts_set_exchange_bytes(B._h.h, 1) != 0  # no byte render on 8x8
+    else:
+        assert B._h.L.mrts_set_exchange_bytes(B._h.h, 3) != 0  # 1 or 2 bytes only
     send = [torch.zeros(tuple(B.obs.shape), dtype=dt, device=B.device) for _ in range(2)]
     recv = torch.zeros((1,) + tuple(B.obs.shape), dtype=dt, device=B.device)
     k = 0
