@@ -299,6 +299,23 @@ int mrts_playout_dev(mrts_env* env, int32_t horizon, void* stream);
 int mrts_evaluate(mrts_env* env, int32_t maxplayer, float* out);
 int mrts_evaluate_dev(mrts_env* env, int32_t maxplayer, float* d_out, void* stream);
 
+/* Trace replay (test-facing; the replay rule of test/microrts/TestTracesIntegrity.java:72-127, which
+ * checks the engine against the reference's recorded games under data/traces): on every game of a
+ * forward-model handle (games never auto-reset), issueSafe of player 0's rows, then issueSafe of
+ * player 1's rows (:119-120; rts/GameState.java:338-408, each action judged on the unit at (x, y) and
+ * issued to it, :356-382), then GameState.cycle() until the game's time reaches until[g] (:83-86).
+ * pairs = int32 [n_games][n_pairs][8]: [player (-1 = padding), x, y, UnitAction type, parameter,
+ * target x, target y, unit type] (the fields of a trace action, rts/UnitAction.java:110-130), a
+ * player's rows in the entry's order.  out[g] (may be NULL) = MRTS_TRACE_* bits.  generic = 1 runs the
+ * generic kernel even on the 16x16 / 8x8 shapes that have specialised instances.  Synchronous. */
+enum {
+    MRTS_TRACE_ISSUED = 1,   /* issueSafe returned true for a player (TestTracesIntegrity.java:119-124) */
+    MRTS_TRACE_GAMEOVER = 2, /* a cycle was due after one that ended the game (the Java assertFalse, :84) */
+    MRTS_TRACE_NO_UNIT = 4   /* no unit at a pair's (x, y): Java prints "Inconsistent order" (:371-375) */
+};
+int mrts_trace_step(mrts_env* env, const int32_t* pairs, int32_t n_pairs, const int32_t* until, int32_t* out,
+                    int32_t generic);
+
 /* Canonical state dump of the game behind `slot` (same format as the CPU oracle's dumpState):
  * [time, 2, res0, res1, n_units, (type, player, x, y, hp, resources)*, n_assignments,
  *  (unit index, action type, parameter, x, y, unit type or -1, issue time)*] — units in

@@ -486,6 +486,7 @@ struct mrts_env {
     uint32_t* d_prioTab = nullptr;  // multi-step launches: per-SIMD issue-rank table (KDyn.prio_tab)
     int32_t* d_bal = nullptr;       // multi-step launches: balanced game placement (KDyn.bal)
     int obsImg = 0;                 // KDyn.obs_img: every observation value fits a byte
+    bool exPending[2] = {false, false};  // exDone[b] was recorded by an earlier exchange call
     // native observation exchange (mrts_exchange_init): an RCCL communicator over this handle's ranks,
     // its own communication stream, and per send buffer the step-ready / collective-done events
     ncclComm_t exComm = nullptr;
@@ -592,6 +593,17 @@ struct mrts_env {
         D.bal = D.n_iter > 1 ? d_bal : nullptr;
         D.obs_img = obsImg;
         return launchEnv(mode, hstatic, d_static, D, s, e0, e1);
+    }
+    // a state block about to be injected: if any live unit's hp or resources leaves 0..255, the byte
+    // renders (KDyn.obs_img, the uint8 exchange transport) can no longer show it — turn them off for
+    // good (300 would have rendered as 44, -5 as 251)
+    void noteValues(const int32_t* s) {
+        const int nu = s[H_NU];
+        const int32_t* A = s + H_WORDS;
+        for (int i = 0; i < nu && i < CAP; i++) {
+            const int hpv = A[A_HP * CAP + i], rv = A[A_RES * CAP + i];
+            if (hpv < 0 || hpv > 255 || rv < 0 || rv > 255) obsImg = 0;
+        }
     }
     int gameOfSlot(int slot, int* player) const {
         if (slot < 2 * nSpGames) {
@@ -727,12 +739,17 @@ int mrts_create(const mrts_config* cfg, mrts_env** out) {
         if (lds > 64 * 1024) HIPCHK(prepareLds(lds));
         for (auto& m : maps)
             if ((int)m.units.size() > maxUnits) throw Fail{-ENOSPC, "a map holds more units than max_units"};
-        {  // the largest hp / resources an observation plane can show: the maps' units, the table's types
-            int mx = 0;
+        {  // the hp / resources range an observation plane can show: the maps' units, the table's types
+            // (a unit's hp only falls; its resources fall, or rise by harvestAmount from 0).  A state
+            // injected later (mrts_set_state_json, mrts_restore) can hold other values: noteValues.
+            int mx = 0, mn = 0;
             for (auto& m : maps)
-                for (auto& u : m.units) mx = std::max(mx, std::max(u.hp, u.res));
+                for (auto& u : m.units) {
+                    mx = std::max(mx, std::max(u.hp, u.res));
+                    mn = std::min(mn, std::min(u.hp, u.res));
+                }
             for (int t = 0; t < env->utt.ntypes; t++) mx = std::max(mx, std::max(env->utt.hp[t], env->utt.harvestAmt[t]));
-            env->obsImg = mx <= 255 ? 1 : 0;
+            env->obsImg = (mx <= 255 && mn >= 0) ? 1 : 0;
         }
         // templates blob
         std::vector<int32_t> blob;
@@ -1213,9 +1230,12 @@ void ncclChk(ncclResult_t r, const char* what) {
 // per step: wait until the collective that last read send buffer k % 2 is done, run the step (it
 // writes its int16 observation there), then all-gather it into recv on the exchange stream
 template <class StepFn>
-void exchangeLoop(mrts_env* env, int32_t n_steps, int16_t* d_send0, int16_t* d_send1, int16_t* d_recv, void* stream,
-                  StepFn step) {
+void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t* d_send0, int16_t* d_send1, int16_t* d_recv,
+                  void* stream, StepFn step) {
     if (!env->exComm) throw Fail{-EINVAL, "mrts_exchange_init first"};
+    // the step kernel writes the transport as part of its observation write (prepObs)
+    if (!d_obs) throw Fail{-EINVAL, "the exchange needs an observation buffer (d_obs)"};
+    if (env->exBytes == 1 && !env->obsImg) throw Fail{-ENOTSUP, "uint8 exchange: an observation value no longer fits a byte"};
     if (env->partialObs) throw Fail{-ENOTSUP, "the int16 transport is written for full observability only"};
     if (!d_send0 || !d_send1 || !d_recv || (((uintptr_t)d_send0 | (uintptr_t)d_send1) & 7))
         throw Fail{-EINVAL, "send buffers must be 8-byte aligned, recv non-null"};
@@ -1226,6 +1246,10 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, int16_t* d_send0, int16_t* d_s
     const size_t bytes = (size_t)env->nSlots * env->C * env->HW * (u8 ? 1 : 2);
     bool pending[2] = {false, false};
     int16_t* const saved = env->obs16;
+    // a send buffer an earlier call's collective may still read (that call returned with the
+    // collectives enqueued on `stream` as it was then): wait for it here too, whatever the stream
+    for (int b = 0; b < 2; b++)
+        if (env->exPending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
     try {
         for (int32_t k = 0; k < n_steps; k++) {
             const int b = k & 1;
@@ -1238,6 +1262,7 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, int16_t* d_send0, int16_t* d_s
             ncclChk(g_rccl.allGather(send[b], d_recv, bytes, ncclUint8, env->exComm, env->exStream), "ncclAllGather");
             HIPCHK(hipEventRecord(env->exDone[b], env->exStream));
             pending[b] = true;
+            env->exPending[b] = true;
         }
         for (int b = 0; b < 2; b++)  // the caller's stream covers every collective of the call
             if (pending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
@@ -1331,7 +1356,7 @@ int mrts_rollout_fused_exchange_dev(mrts_env* env, int32_t* d_actions, const int
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
         RolloutEvents ev(env, stream);
-        exchangeLoop(env, n_steps, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
+        exchangeLoop(env, n_steps, d_obs, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
             stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
                       first_next_step + (uint32_t)k, 1, stream);
         });
@@ -1348,7 +1373,7 @@ int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const i
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
         RolloutEvents ev(env, stream);
-        exchangeLoop(env, n_steps, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
+        exchangeLoop(env, n_steps, d_obs, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
             stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, 1,
                         stream);
         });
@@ -1887,6 +1912,7 @@ int mrts_set_state_json(mrts_env* env, int32_t slot, const char* json) {
         std::vector<int32_t> s;
         readBlock(env, g, s);
         jsonToBlock(env, json, s);
+        env->noteValues(s.data());
         const size_t sw = s.size();
         HIPCHK(hipMemcpy(env->d_state + (size_t)g * sw, s.data(), sw * 4, hipMemcpyHostToDevice));
         env->lastMaskPtr = nullptr;  // the next mask and observation writes are full ones
@@ -1960,6 +1986,8 @@ int mrts_restore(mrts_env* env, const void* buf, int64_t size) {
             throw Fail{-EINVAL, "checkpoint of a different configuration (opponents, maps, max_steps, reward functions "
                                 "or partial observability differ)"};
         if (size != mrts_checkpoint_size(env)) throw Fail{-EINVAL, "checkpoint size mismatch"};
+        for (int g = 0; g < h.nGames; g++)
+            env->noteValues((const int32_t*)((const char*)buf + sizeof(h)) + (size_t)g * h.words);
         HIPCHK(hipDeviceSynchronize());
         HIPCHK(hipMemcpy(env->d_state, (const char*)buf + sizeof(h), (size_t)h.words * h.nGames * 4, hipMemcpyHostToDevice));
         env->lastMaskPtr = nullptr;
@@ -2054,6 +2082,55 @@ int mrts_playout(mrts_env* env, int32_t horizon) {
         int r = mrts_playout_dev(env, horizon, env ? env->stream : nullptr);
         if (r) return r;
         HIPCHK(hipStreamSynchronize(env->stream));
+        checkFlagsAfter(env);
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_trace_step(mrts_env* env, const int32_t* pairs, int32_t n_pairs, const int32_t* until, int32_t* out,
+                    int32_t generic) {
+    try {
+        if (!env || !env->forwardModel) throw Fail{-EINVAL, "not a forward-model handle"};
+        if (!until || (n_pairs > 0 && !pairs)) throw Fail{-EINVAL, "null argument"};
+        if (n_pairs < 0 || (size_t)n_pairs * env->nGames * 8 >= ((size_t)1 << 31)) throw Fail{-EINVAL, "bad n_pairs"};
+        const size_t nr = (size_t)env->nGames * n_pairs;
+        for (size_t i = 0; i < nr; i++) {  // what Java could not construct (TraceEntry.fromXML, UnitAction(...))
+            const int32_t* r = pairs + 8 * i;
+            if (r[0] < -1 || r[0] > 1) throw Fail{-EINVAL, "pair player must be 0, 1 or -1 (padding)"};
+            if (r[0] < 0) continue;
+            if (r[3] == 4 && (r[7] < 0 || r[7] >= env->utt.ntypes)) throw Fail{-EINVAL, "PRODUCE of an unknown unit type"};
+            if (r[4] < -32768 || r[4] > 32767) throw Fail{-EINVAL, "parameter out of the int16 range"};
+        }
+        for (int g = 0; g < env->nGames; g++)
+            if (until[g] < 0 || until[g] > (1 << 30)) throw Fail{-EINVAL, "until out of range"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(hipStreamSynchronize(env->stream));
+        const size_t need = nr * 8 + 2 * (size_t)env->nGames;
+        if (need > env->rowsStageInts) {
+            (void)hipFree(env->d_rowsStage);
+            env->d_rowsStage = nullptr;
+            HIPCHK(hipMalloc(&env->d_rowsStage, need * 4));
+            env->rowsStageInts = need;
+        }
+        int32_t* d_until = env->d_rowsStage + nr * 8;
+        if (nr) HIPCHK(hipMemcpyAsync(env->d_rowsStage, pairs, nr * 8 * 4, hipMemcpyHostToDevice, env->stream));
+        HIPCHK(hipMemcpyAsync(d_until, until, (size_t)env->nGames * 4, hipMemcpyHostToDevice, env->stream));
+        KDyn D;
+        std::memset(&D, 0, sizeof(D));
+        D.rows = env->d_rowsStage;
+        D.n_rows = n_pairs;
+        D.trace_until = d_until;
+        D.trace_out = d_until + env->nGames;
+        D.trace_generic = generic ? 1 : 0;
+        HIPCHK(env->launch(4, D, env->stream));
+        env->lastObsPtr = nullptr;
+        env->fusedActions = nullptr;
+        std::vector<int32_t> o((size_t)env->nGames);
+        HIPCHK(hipMemcpyAsync(o.data(), D.trace_out, (size_t)env->nGames * 4, hipMemcpyDeviceToHost, env->stream));
+        HIPCHK(hipStreamSynchronize(env->stream));
+        if (out) std::memcpy(out, o.data(), o.size() * 4);
         checkFlagsAfter(env);
         return 0;
     } catch (const Fail& f) {

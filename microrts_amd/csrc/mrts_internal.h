@@ -179,6 +179,13 @@ struct KDyn {
     // the unit-type table, mrts_create), so 16x16 observations render through the byte image
     // (writeObsFullImg)
     int32_t obs_img;
+    // trace replay (MODE_TRACE, mrts_trace_step): `rows` holds per game [n_rows] issue rows [player, x, y,
+    // type, parameter, target x, target y, unit type]; each game then cycles until its time reaches
+    // trace_until[g] and reports TR_* bits in trace_out[g]; trace_generic = 1 runs the generic kernel
+    // even where a specialised instance exists
+    const int32_t* trace_until;
+    int32_t* trace_out;
+    int32_t trace_generic;
 };
 constexpr int BAL_COST = 16;
 constexpr int PRIO_KEYS = 8 * 8 * 2 * 16 * 4;  // XCC x SE x SH x CU x SIMD (HW_ID / XCC_ID fields)

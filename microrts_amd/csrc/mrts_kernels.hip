@@ -28,7 +28,7 @@ namespace {
 constexpr uint16_t EMPTY = 0xFFFF, WALL = 0xFFFE;
 constexpr int INF = 0x7FFFFFFF;
 enum { T_NONE = 0, T_MOVE = 1, T_HARVEST = 2, T_RETURN = 3, T_PRODUCE = 4, T_ATTACK = 5 };
-enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2, MODE_PLAYOUT = 3 };
+enum { MODE_STEP = 0, MODE_RESET = 1, MODE_MASKS = 2, MODE_PLAYOUT = 3, MODE_TRACE = 4 };
 
 // Diagnostic build only (-DMRTS_PHASE_TIMING, tools/phase_timing.py): per-phase shader-clock cycles
 // summed over games; not compiled into libmrts.so.
@@ -114,6 +114,8 @@ enum : uint32_t {
     E_CAPACITY = 1u << 0, E_ADDUNIT = 1u << 1, E_PRODUCE_TYPE = 1u << 2, E_OLDER = 1u << 3,
     E_NEG_RES = 1u << 4, E_COLLISION = 1u << 5
 };
+// MODE_TRACE per-game result word (KDyn.trace_out)
+enum : uint32_t { TR_ISSUED = 1u, TR_GAMEOVER = 2u, TR_NO_UNIT = 4u };
 
 DEV int lane_id() { return (int)threadIdx.x; }
 // branch-probability hints: cold paths (more than 64 units, auto-reset, conflict resolution, the
@@ -1119,6 +1121,54 @@ struct Game {
         issueFills(p, fillDur);
     }
 
+    // ------------------------------------------------------------------ trace replay (MODE_TRACE)
+    // issueSafe(pa) (rts/GameState.java:338-408) of player p's pairs of a trace entry, as
+    // TestTracesIntegrity.testTrace builds them (test/microrts/TestTracesIntegrity.java:101-121): rows
+    // [player, x, y, type, parameter, target x, target y, unit type], the player's rows in the given
+    // order.  Each action's legality is judged on the trace's own Unit object, whose fields equal those
+    // of the state's unit at (x, y) whenever the replay is in sync; that unit is then the one issued —
+    // the first unit at (x, y) in list order (:356-382; one unit per cell).  No fillWithNones.
+    // Returns issue()'s value: a pair was put with a type other than NONE.
+    DEV bool traceIssue(int p, const int32_t* rows, int n, uint32_t& flags) {
+        curP = p;
+        bool put = false;
+        bool missing = false;
+        for (int r0 = 0; r0 < n; r0 += 64) {
+            const int r = r0 + lid();
+            int32_t a[8] = {-1, 0, 0, 0, 0, 0, 0, 0};
+            if (r < n)
+#pragma unroll
+                for (int k = 0; k < 8; k++) a[k] = rows[(size_t)r * 8 + k];
+            bool act = a[0] == p;
+            int s = 0;
+            if (act) {
+                s = inb(a[1], a[2]) ? (int)cell[a[2] * W + a[1]] : EMPTY;
+                if (s >= CAP) {  // no unit there: Java prints "Inconsistent order" and issues the trace's unit
+                    missing = true;
+                    act = false;
+                }
+            }
+            int t = a[3], prm = a[4], tx = 0, ty = 0, ut = 0;
+            if (act) {
+                if (t < T_NONE || t > T_ATTACK) t = ACT_INVALID;  // never in getUnitActions: NONE(0)
+                const bool dir = t >= T_MOVE && t <= T_PRODUCE;
+                if (dir && (prm < 0 || prm > 3)) prm = 4;  // not a direction: never legal
+                if (t == T_PRODUCE) ut = a[7];              // the host checked 0 <= ut < ntypes
+                if (t == T_ATTACK) {
+                    const bool on = inb(a[5], a[6]);
+                    tx = on ? a[5] : 255;
+                    ty = on ? a[6] : 255;
+                }
+                legality(s, t, prm, tx, ty, ut);
+            }
+            const uint64_t m = ballot(act);
+            wsync();
+            if (m) issueBatch(act, act ? lanes_below(m) : 0, __popcll(m), s, t, prm, tx, ty, ut, true, nullptr, &put);
+        }
+        if (ballot(missing)) flags |= TR_NO_UNIT;
+        return put;
+    }
+
     // Base reservations of every current assignment the deciding view holds (PlayerAction.java:387-394,
     // merged as ResourceUsage.java:92-97); in a PO view only snapshot units' assignments count.
     DEV void baseReservations(int p, int& r0, int& r1) {
@@ -1441,8 +1491,9 @@ struct Game {
         return false;
     }
 
-    // GameState.issue for one pair (rts/GameState.java:252-326), wave-uniform arguments.
-    DEV void issueOne(int s, int t, int prm, int tx, int ty, int ut) {
+    // GameState.issue for one pair (rts/GameState.java:252-326), wave-uniform arguments.  Returns the
+    // type of the action put into the map (NONE when a conflict cancelled the new one).
+    DEV int issueOne(int s, int t, int prm, int tx, int ty, int ut) {
         if (t == T_MOVE || t == T_PRODUCE) {
             const uint32_t cu = uniu(uc[s]);
             const int pl = uplay(cu), typ = utyp(cu);
@@ -1532,6 +1583,7 @@ struct Game {
         }
         if (!again) seq++;
         wsync();
+        return t;
     }
 
     // Issue index over ALL units (GameState.issue checks every present assignment, :255-262); under
@@ -1588,8 +1640,10 @@ struct Game {
     // checkDup (Java rows): a unit named by an earlier pair of this pa (same batch, or already issued)
     // forces the one-at-a-time path
     // cuKnown: the lane's unit core word uc[s] (already in a register), or null
+    // putAny (trace replay): set when a pair is put with a type other than NONE — GameState.issue's
+    // return value (:323-324)
     DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut, bool checkDup = false,
-                        const uint32_t* cuKnown = nullptr) {
+                        const uint32_t* cuKnown = nullptr, bool* putAny = nullptr) {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
         if (MRTS_UNLIKELY(D.reward_need & RN_COUNTS)) {  // the pairs as the TraceEntry records them (legality applied)
@@ -1639,6 +1693,7 @@ struct Game {
             }
         }
         if (MRTS_LIKELY(ballot(conf) == 0)) {
+            if (putAny && ballot(act && t != T_NONE)) *putAny = true;
             if (act) {
                 ua[s] = pack_ua(t, ut, tx, ty) | UA_PRESENT;
                 par[s] = (int16_t)prm;
@@ -1665,7 +1720,8 @@ struct Game {
 #endif
             for (int r = 0; r < n; r++) {
                 const int k = __builtin_ctzll(ballot(act && rank == r));
-                issueOne(rl(s, k), rl(t, k), rl(prm, k), rl(tx, k), rl(ty, k), rl(ut, k));
+                const int put = issueOne(rl(s, k), rl(t, k), rl(prm, k), rl(tx, k), rl(ty, k), rl(ut, k));
+                if (putAny && put != T_NONE) *putAny = true;
             }
             ixValid = false;
         }
@@ -4301,7 +4357,7 @@ DEV void helperLoop(const KDyn& D, uint8_t* smem, int g, int niter) {
         const uint32_t w0 = obsbuf[(k & 1) * 2 * HW + 2 * l], w1 = obsbuf[(k & 1) * 2 * HW + 2 * l + 1];
         int v[6];
         v[0] = (int)(int16_t)(w0 & 0xFFFFu);
-        v[1] = (int)(w0 >> 16);
+        v[1] = (int)(int16_t)(w0 >> 16);  // resources, signed as writeObsFull stores them
         v[3] = (int)((w1 >> 4) & 15u);
         v[4] = (int)((w1 >> 8) & 15u);
         v[5] = (int)((w1 >> 12) & 1u);
@@ -4323,6 +4379,11 @@ DEV void helperLoop(const KDyn& D, uint8_t* smem, int g, int niter) {
                 int16_t* h0 = D.obs16 + (size_t)(slot0 + i) * D.C * HW;
 #pragma unroll
                 for (int q = 0; q < 6; q++) h0[(size_t)q * HW + l] = (int16_t)v[q];
+            }
+            if (MRTS_UNLIKELY(D.obs8 != nullptr)) {  // the uint8 transport: every plane, every step
+                uint8_t* b0 = D.obs8 + (size_t)(slot0 + i) * D.C * HW;
+#pragma unroll
+                for (int q = 0; q < 6; q++) b0[(size_t)q * HW + l] = (uint8_t)v[q];
             }
         }
     };
@@ -4684,6 +4745,40 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
         }
         wsync();
         G.store();
+        return;
+    }
+
+    if (MODE == MODE_TRACE) {
+        // TestTracesIntegrity.testTrace (test/microrts/TestTracesIntegrity.java:72-127), one entry per
+        // launch: issueSafe(p0's pairs), issueSafe(p1's pairs) (:119-120), then GameState.cycle() until
+        // the next entry's time (:83-86).  The Java asserts that no cycle follows a cycle that ended the
+        // game; cycle() returns gameover() of the state it leaves, which is this state again before the
+        // next cycle (issuing moves no unit) — so a game over before any further cycle is that failure.
+        uint32_t flags = 0;
+        const int32_t* rows = D.rows + (size_t)G.g * D.n_rows * 8;
+        const bool i0 = G.traceIssue(0, rows, D.n_rows, flags);
+        const bool i1 = G.traceIssue(1, rows, D.n_rows, flags);
+        if (i0 || i1) flags |= TR_ISSUED;
+        const int until = uni(D.trace_until[G.g]);
+        while (G.time < until) {
+            if (G.time > 0) {
+                bool over;
+                int winner;
+                G.outcome(over, winner);
+                if (over) {
+                    flags |= TR_GAMEOVER;
+                    break;
+                }
+            }
+            G.cycle();
+            if (G.deaths) {
+                G.compact();
+                G.deaths = 0;
+            }
+        }
+        wsync();
+        G.store();
+        if (lane_id() == 0) D.trace_out[G.g] = (int32_t)flags;
         return;
     }
 
@@ -5364,6 +5459,15 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
             break;
         case MODE_RESET: LAUNCH((k_env<MODE_RESET, 0>), grid, block, lds, stream, D.state, ds, D); break;
         case MODE_PLAYOUT: LAUNCH((k_env<MODE_PLAYOUT, 0>), grid, block, lds, stream, D.state, ds, D); break;
+        case MODE_TRACE: {
+            // the specialised 16x16 / 8x8 step instances' dimensions (their games' code with constant
+            // sizes), else the generic kernel
+            const bool fix = !D.trace_generic && hs.utt.K == 79 && hs.utt.ntypes == 7 && hs.utt.maxAttackRadius == 7 &&
+                             hs.H == hs.W && !hs.partial_obs;
+            if (fix && hs.W == 16 && hs.CAP == 320) LAUNCH((k_env<MODE_TRACE, 16, 320>), grid, block, lds, stream, D.state, ds, D);
+            else if (fix && hs.W == 8 && hs.CAP == 128) LAUNCH((k_env<MODE_TRACE, 8, 128>), grid, block, lds, stream, D.state, ds, D);
+            else LAUNCH((k_env<MODE_TRACE, 0>), grid, block, lds, stream, D.state, ds, D);
+        } break;
         default:LAUNCH((k_env<MODE_MASKS, 0>), grid, block, lds, stream, D.state, ds, D); break;
     }
 #undef LAUNCH
@@ -5383,6 +5487,7 @@ hipError_t prepareLds(size_t bytes) {
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_RESET, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_MASKS, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_PLAYOUT, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_env<MODE_TRACE, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     return e;
 }
 // Unmasked uniform random policy (BASELINE config c2), uniformRow for every cell of

@@ -659,7 +659,8 @@ class ForwardModel:
     SimpleSqrtEvaluationFunction3.  Game j's java.util.Random streams are seeded from seed + j (see
     DESIGN.md).  Device calls are ordered on torch's current stream of the device."""
 
-    def __init__(self, n_games, map_path, policies=("RandomBiasedAI", "RandomBiasedAI"), utt=None, device=0, seed=0):
+    def __init__(self, n_games, map_path, policies=("RandomBiasedAI", "RandomBiasedAI"), utt=None, device=0, seed=0,
+                 max_units=0):
         import torch
 
         if not torch.cuda.is_available():
@@ -669,8 +670,9 @@ class ForwardModel:
         p0, p1 = policies
         p0 = p0 if isinstance(p0, (list, tuple)) else [p0] * n_games
         p1 = p1 if isinstance(p1, (list, tuple)) else [p1] * n_games
-        self._h = _Handle(0, n_games, 1 << 30, [_resolve("", map_path)] * n_games, p1, utt, False, device, seed, 0,
-                          ai1s=p0, forward_model=True)
+        maps = list(map_path) if isinstance(map_path, (list, tuple)) else [map_path] * n_games  # one per game, same size
+        self._h = _Handle(0, n_games, 1 << 30, [_resolve("", m) for m in maps], p1, utt, False, device, seed, 0,
+                          ai1s=p0, forward_model=True, max_units=max_units)
         self.n = n_games
         self.device = torch.device("cuda", device)
         self.value = torch.zeros(n_games, dtype=torch.float32, device=self.device)
@@ -706,6 +708,21 @@ class ForwardModel:
             raise ValueError("horizon out of range")
         h = self._h
         _lib.check(h.L.mrts_playout_dev(h.h, int(horizon), self._s()))
+
+    def trace_step(self, pairs, until, generic=False):
+        """One entry of TestTracesIntegrity.testTrace (test/microrts/TestTracesIntegrity.java:72-127) on
+        every game: issueSafe(player 0's rows), issueSafe(player 1's rows), then cycle() until time ==
+        until[g].  pairs: int32 [n_games, n_pairs, 8] rows [player (-1 = padding), x, y, type, parameter,
+        target x, target y, unit type].  Returns the MRTS_TRACE_* bits per game (int32 [n_games])."""
+        h = self._h
+        pr = np.ascontiguousarray(np.asarray(pairs, dtype=np.int32))
+        assert pr.ndim == 3 and pr.shape[0] == self.n and pr.shape[2] == 8
+        un = np.ascontiguousarray(np.asarray(until, dtype=np.int32).reshape(self.n))
+        out = np.zeros(self.n, dtype=np.int32)
+        self.synchronize()
+        _lib.check(h.L.mrts_trace_step(h.h, pr.ctypes.data_as(ctypes.c_void_p), pr.shape[1], un.ctypes.data_as(ctypes.c_void_p),
+                                       out.ctypes.data_as(ctypes.c_void_p), int(bool(generic))))
+        return out
 
     def evaluate(self, maxplayer=0, out=None):
         """SimpleSqrtEvaluationFunction3.evaluate(maxplayer, 1 - maxplayer, gs): float32 [n] on device."""

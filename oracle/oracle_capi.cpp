@@ -789,8 +789,12 @@ int oref_fm_errors(void* h, int game) { return ((FwdModel*)h)->games.at((size_t)
 // Fixture text (tests/golden/make_trace_fixtures.py): see that script's docstring.
 // Replays like TestTracesIntegrity.testTrace and additionally compares the full
 // PhysicalGameState with each entry's snapshot.  Returns #entries checked (>=0)
-// or -1 with a message.
-int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int msglen) {
+// or -1 with a message.  onEntry(e, gs) runs after the replay caught up with entry e (the state the
+// strict check just compared); onIssued(e, issued) after entry e's actions were issued.
+}  // extern "C"
+namespace {
+template <class OnEntry, class OnIssued>
+int replayTrace(const char* map_path, const char* fixture, char* msg, int msglen, OnEntry onEntry, OnIssued onIssued) {
     auto fail = [&](const std::string& s) {
         std::snprintf(msg, (size_t)msglen, "%s", s.c_str());
         return -1;
@@ -818,7 +822,6 @@ int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int 
             tp->terrain = gs.pgs->terrain;
             tp->players.push_back(std::make_shared<Player>(Player{0, r0}));
             tp->players.push_back(std::make_shared<Player>(Player{1, r1}));
-            std::vector<UnitP> tunits;
             for (int i = 0; i < nu; i++) {
                 auto u = std::make_shared<Unit>();
                 int t;
@@ -856,7 +859,9 @@ int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int 
                     }
                 }
             if (!why.str().empty()) return fail("time " + std::to_string(time) + ": " + why.str());
+            onEntry(e, gs);
             checked++;
+            bool issued = false;
             if (!tas.empty()) {  // :101-125
                 bool containsRealActions = false;
                 PlayerAction p1, p2;
@@ -874,15 +879,58 @@ int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int 
                     else return fail("action for a non-player unit");
                     containsRealActions = containsRealActions || ua->type != UnitAction::TYPE_NONE;
                 }
-                bool issued = gs.issueSafe(p1);
+                issued = gs.issueSafe(p1);
                 issued = gs.issueSafe(p2) || issued;
                 if (containsRealActions != issued) return fail("containsRealActions != issuedActions at time " + std::to_string(time));
             }
+            onIssued(e, issued);
         }
         return checked;
     } catch (std::exception& e) {
         return fail(std::string("exception: ") + e.what());
     }
+}
+}  // namespace
+extern "C" {
+
+int oref_trace_replay(const char* map_path, const char* fixture, char* msg, int msglen) {
+    return replayTrace(map_path, fixture, msg, msglen, [](int, const GameState&) {}, [](int, bool) {});
+}
+
+// The same replay, keeping the canonical dump (dumpState: units in list order, assignments in
+// LinkedHashMap order) of the state at every entry — what the GPU replay (tests/test_gpu_traces.py)
+// compares against beyond the trace's own snapshot — into buf (offsets[e] .. offsets[e + 1]), and
+// issueSafe's combined return value per entry into issued[e].  Returns #entries, -1 with a message,
+// or -2 when cap / max_entries is too small.
+int oref_trace_dumps(const char* map_path, const char* fixture, int32_t* buf, int64_t cap, int32_t* offsets, int32_t* issued,
+                     int32_t max_entries, char* msg, int msglen) {
+    int64_t used = 0;
+    bool overflow = false;
+    offsets[0] = 0;
+    const int n = replayTrace(
+        map_path, fixture, msg, msglen,
+        [&](int e, const GameState& gs) {
+            if (e >= max_entries) {
+                overflow = true;
+                return;
+            }
+            const auto d = dumpState(gs);
+            if (used + (int64_t)d.size() > cap) {
+                overflow = true;
+            } else {
+                std::memcpy(buf + used, d.data(), d.size() * 4);
+                used += (int64_t)d.size();
+            }
+            offsets[e + 1] = (int32_t)used;
+        },
+        [&](int e, bool is) {
+            if (e < max_entries) issued[e] = is ? 1 : 0;
+        });
+    if (n >= 0 && overflow) {
+        std::snprintf(msg, (size_t)msglen, "buffer too small");
+        return -2;
+    }
+    return n;
 }
 
 // ------------------------------------------------ CPU baseline: VecClient + random policy,

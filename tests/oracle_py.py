@@ -45,6 +45,7 @@ def load():
         L.oref_errors.argtypes = [P, I]
         L.oref_last_error.restype = ctypes.c_char_p
         L.oref_trace_replay.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, I]
+        L.oref_trace_dumps.argtypes = [ctypes.c_char_p, ctypes.c_char_p, P, ctypes.c_int64, P, P, I, ctypes.c_char_p, I]
         L.oref_policy.argtypes = [P, I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, P]
         L.oref_botclient_create.restype = P
         L.oref_botclient_create.argtypes = [ctypes.c_char_p, I, I, I, I, I, ctypes.c_int64, ctypes.c_char_p]
@@ -74,6 +75,23 @@ def load():
         L.oref_policy_uniform.argtypes = [I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, P]
         _lib = L
     return _lib
+
+
+def trace_dumps(map_path, fixture_text):
+    """Replay one converted reference trace (tests/golden/make_trace_fixtures.py) on the oracle with the
+    rule of TestTracesIntegrity.java:72-127: the canonical state dump at every entry (after catching up
+    with its time, before its actions) and issueSafe's combined return value per entry."""
+    L = load()
+    n = int(fixture_text.split(None, 2)[1])
+    cap = 1 << 22
+    buf = np.zeros(cap, dtype=np.int32)
+    off = np.zeros(n + 1, dtype=np.int32)
+    iss = np.zeros(max(n, 1), dtype=np.int32)
+    msg = ctypes.create_string_buffer(1024)
+    r = L.oref_trace_dumps(map_path.encode(), fixture_text.encode(), _ptr(buf), cap, _ptr(off), _ptr(iss), n, msg, 1024)
+    if r != n:
+        raise RuntimeError(f"oracle trace replay: {r}: {msg.value.decode()}")
+    return [buf[off[e]:off[e + 1]].copy() for e in range(n)], iss[:n].copy()
 
 
 def _ptr(a):

@@ -350,3 +350,63 @@ def test_native_exchange_graph_replay():
     for e in (A, B):
         assert not e.error_flags().any()
         e.close()
+
+
+def test_values_beyond_a_byte_after_injection():
+    """the 16x16 byte-image render and the uint8 exchange transport hold values 0..255
+    only.  A state injected by GameState.fromJSON (rts/GameState.java:897-915) may carry more: a Resource
+    with 300 resources and a Base with 1000 must still show exactly in the int32 observation — in single
+    steps and in multi-step launches — and the uint8 transport must then be refused."""
+    import json
+
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mp, n_sp = "maps/16x16/basesWorkers16x16.xml", 8
+    env = DeviceVecEnv(n_sp, 0, 2000, [mp] * n_sp, seed=9)
+    assert env.fused_multi_step
+    rep = _MaskedReplica(mp, list(range(n_sp)), 9)
+    assert env._h.L.mrts_set_exchange_bytes(env._h.h, 1) == 0  # every map value fits a byte
+    env.reset()
+    d = json.loads(rep.ref.state_json(0))
+    res = [u for u in d["pgs"]["units"] if u["type"] == "Resource"]
+    base = [u for u in d["pgs"]["units"] if u["type"] == "Base"]
+    res[0]["resources"] = 300
+    base[0]["hitpoints"] = 1000
+    j = json.dumps(d)
+    for s in (0, 4):
+        env.set_state_json(s, j)
+        rep.ref.set_state_json(s, j)
+    env.random_policy(SEED, 0)
+    env.rollout_fused(SEED, 1, 1)  # a single step, then multi-step launches
+    rep.run(1)
+    _compare_launch_end(env, rep, "after one step")
+    ob = env.obs.cpu().numpy()
+    assert ob[0, 1].max() == 300 and ob[0, 0].max() == 1000, "the injected values must show unclipped"
+    env.rollout_fused(SEED, 2, 40)
+    rep.run(40)
+    _compare_launch_end(env, rep, "after a 40-step launch")
+    assert env._h.L.mrts_set_exchange_bytes(env._h.h, 1) != 0, "uint8 transport after values > 255"
+    env.close()
+    rep.ref.close()
+
+
+def test_exchange_needs_an_observation_buffer():
+    """the exchange's send buffers are written by the step's observation write, so an
+    exchange rollout without d_obs would all-gather stale data — it is refused (-EINVAL)."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    mp, n_sp = "maps/16x16/basesWorkers16x16.xml", 4
+    B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=3)
+    B.reset()
+    B.random_policy(SEED, 0)
+    _exchange_env(B)
+    send = [torch.zeros(tuple(B.obs.shape), dtype=torch.int16, device=B.device) for _ in range(2)]
+    recv = torch.zeros((1,) + tuple(B.obs.shape), dtype=torch.int16, device=B.device)
+    p = DeviceVecEnv._p
+    st = ctypes.c_void_p(torch.cuda.current_stream(B.device).cuda_stream)
+    r = B._h.L.mrts_rollout_fused_exchange_dev(B._h.h, p(B.actions), p(B.players), None, p(B.reward), p(B.done), p(B.masks), 0,
+                                               SEED, 1, 2, p(send[0]), p(send[1]), p(recv), st)
+    assert r == -22
+    B.close()

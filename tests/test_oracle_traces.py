@@ -43,6 +43,26 @@ def test_trace_replay_detects_corruption(oracle_lib):
     assert n == -1 and b"hp" in msg.value
 
 
+def test_trace_dumps_follow_the_fixtures(oracle_lib):
+    """The per-entry oracle dumps the GPU replay compares against (oref_trace_dumps) hold the traces'
+    own snapshots, and issueSafe's return value equals "contains real actions" at every entry with
+    actions (TestTracesIntegrity.java:124) — which also checks tests/trace_fixtures.parse."""
+    from tests import trace_fixtures as T
+
+    n = 0
+    for e in IDX:
+        text = gzip.open(os.path.join(ROOT, "tests", "golden", "traces", e["fixture"]), "rt").read()
+        ents = T.parse(text)
+        dumps, issued = oracle_py.trace_dumps(os.path.join(ROOT, e["map"]), text)
+        assert len(ents) == len(dumps) == e["entries"]
+        for k, (ent, d) in enumerate(zip(ents, dumps)):
+            T.check_vs_trace(d, ent, f"{e['fixture']} entry {k}")
+            if ent[3]:
+                assert bool(issued[k]) == any(a[3] != 0 for a in ent[3])
+            n += 1
+    assert n == 17085
+
+
 MAPS = sorted(glob.glob(os.path.join(ROOT, "maps", "**", "*.xml"), recursive=True))
 
 
