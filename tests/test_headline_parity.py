@@ -3,8 +3,9 @@
 bench.py times each config as ONE native rollout call that runs K steps per `k_env` launch
 (multi-step launches).  Here the same calls run at the bench's sizes (c3: 4096
 self-play games on 16x16; c2: 1024 games on 8x8; c5: 2048 partially observable games on 32x32 with
-max_units 256) after a 1000-step burn-in, followed by K = 20 and K = 200 step launches.  Picked
-games are replayed by the oracle with its OWN policy stream: the oracle computes its masks
+max_units 256) after a 1000-step burn-in, followed by K = 20 and K = 200 step launches.  65-66
+picked games (two for each of the 8 XCD classes in each of the 4 SIMD slots of the launch's
+placement, plus the first and the last game; _pick_games) are replayed by the oracle with its OWN policy stream: the oracle computes its masks
 (JNIGridnetVecClient.getMasks, :307-316) and samples the same Philox masked-uniform (or unmasked
 uniform) rows from them, so no GPU-produced action ever enters the oracle.  UTT v1 + CANCEL_BOTH
 draws no Java random numbers, so such an oracle game is an exact replica of the picked GPU game.  At
@@ -38,10 +39,21 @@ def _torch():
     return torch
 
 
-def _picks(n_games, mid):
-    """Slots of the first, a middle and the last game (both players of each)."""
-    g = [0, mid, n_games - 1]
-    return [s for k in g for s in (2 * k, 2 * k + 1)]
+def _pick_games(n_games, per=2):
+    """64 games spread over the launch's placement classes: the dispatcher puts blocks
+    b, b + n/4, b + 2n/4, b + 3n/4 on one SIMD and block b on XCD b % 8, and balanced placement
+    (mrts_kernels.hip balancePerm) permutes games within their XCD class — so `per` games for each of
+    the 8 XCD classes in each of the 4 SIMD-slot quarters, at scattered offsets; plus the first and
+    the last game."""
+    q = n_games // 4
+    g = {k * q + 8 * ((37 * k + 101 * j + 11 * c + 3) % (q // 8)) + c for k in range(4) for c in range(8) for j in range(per)}
+    g |= {0, n_games - 1}
+    return sorted(g)
+
+
+def _picks(n_games):
+    """The slots (both players) of _pick_games."""
+    return [s for k in _pick_games(n_games) for s in (2 * k, 2 * k + 1)]
 
 
 class _MaskedReplica:
@@ -78,14 +90,14 @@ def _compare_launch_end(env, rep, tag):
         assert np.array_equal(env.dump_state(s), ref.dump(i)), f"{tag}: state of slot {s}"
 
 
-def _masked_multi_step(mp, n_games, mid, seed, partial_obs=False, max_units=0):
+def _masked_multi_step(mp, n_games, seed, partial_obs=False, max_units=0):
     _torch()
     from microrts_amd import DeviceVecEnv
 
     S = 2 * n_games
     env = DeviceVecEnv(S, 0, 2000, [mp] * S, seed=seed, partial_obs=partial_obs, max_units=max_units)
     assert env.fused_multi_step, "the bench's shape must run multi-step launches"
-    rep = _MaskedReplica(mp, _picks(n_games, mid), seed, partial_obs)
+    rep = _MaskedReplica(mp, _picks(n_games), seed, partial_obs)
     env.reset()
     env.random_policy(SEED, 0)
     env.rollout_fused(SEED, 1, BURNIN)  # the first launch is a single step, then multi-step launches
@@ -105,13 +117,13 @@ def _masked_multi_step(mp, n_games, mid, seed, partial_obs=False, max_units=0):
 def test_full_size_c3_multi_step():
     """BASELINE configs[2] (c3) as bench.py times it: 4096 self-play games on basesWorkers16x16, the
     fused masked policy, delta masks, K steps per k_env launch."""
-    _masked_multi_step("maps/16x16/basesWorkers16x16.xml", 4096, 1234, seed=5)
+    _masked_multi_step("maps/16x16/basesWorkers16x16.xml", 4096, seed=5)
 
 
 def test_full_size_c5_multi_step():
     """BASELINE configs[4] (c5) per GPU: 2048 partially observable self-play games on
     BWDistantResources32x32, max_units 256, multi-step launches with incremental PO views."""
-    _masked_multi_step("maps/BWDistantResources32x32.xml", 2048, 777, seed=7, partial_obs=True, max_units=256)
+    _masked_multi_step("maps/BWDistantResources32x32.xml", 2048, seed=7, partial_obs=True, max_units=256)
 
 
 def test_full_size_c2_multi_step():
@@ -126,7 +138,7 @@ def test_full_size_c2_multi_step():
     env = DeviceVecEnv(2 * E, 0, 2000, [mp] * (2 * E), seed=8)
     assert env.multi_step_capable
     S, H, W, C, K = env.dims
-    picks = _picks(E, 500)
+    picks = _picks(E)
     ref = oracle_py.OracleVecClient(len(picks), 0, 2000, [mp] * len(picks), seed=8)
     env.reset()
     ref.reset()
