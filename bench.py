@@ -89,7 +89,19 @@ def parse():
                          "prints the line with with_gather = {error} and all ranks exit 0 (a hung collective must "
                          "not cost the headline line)")
     ap.add_argument("--no-compare", action="store_true", help="skip the other policy form's comparison window")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--utt", type=int, choices=[1, 2], default=1,
+                    help="UnitTypeTable version: 1 VERSION_ORIGINAL (the traces', SURVEY.md §8(d)), 2 VERSION_ORIGINAL_"
+                         "FINETUNED (SURVEY.md §8(d)'s secondary sweep); CANCEL_BOTH either way")
+    ap.add_argument("--no-full-contract", action="store_true",
+                    help="skip the full_contract window (full mask rewrite + separate policy launch, one launch per step)")
+    ap.add_argument("--gather-window", choices=["records", "tensor"], default="records",
+                    help="with_gather: records = all-gather of the compact game records (default); tensor = the "
+                         "per-step all-gather of the uint8 / int16 observation tensor")
+    ap.add_argument("--records-steps", type=int, default=0,
+                    help="steps per launch of the records window (0 = the K steps in one launch)")
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the all-cores CPU baseline (default: every CPU this process may use, capped by "
+                         "the cgroup's CPU quota)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per step-kernel launch from a rocprofv3 --pmc pass (profiles/), for roofline.traffic")
     a = ap.parse_args()
@@ -109,6 +121,9 @@ def parse():
         a.launch = "native" if a.policy in ("fused", "uniform", "uniform-split") else "graph"
     if a.launch == "native" and a.policy not in ("fused", "uniform", "uniform-split"):
         ap.error("--launch native needs --policy fused or uniform")
+    if a.launch == "graph" and a.gather_obs:
+        # a torch.cuda.graph capture of torch.distributed collectives (why it aborted)
+        ap.error("--launch graph cannot capture the --gather-obs collectives; use --launch eager")
     return a
 
 
@@ -160,8 +175,49 @@ class _FenceFreeEvent:
         return ms.value
 
 
+def lib_sha256():
+    """SHA-256 of the libmrts.so this process runs (the counter files name the library they describe)."""
+    import hashlib
+
+    from microrts_amd import _lib
+
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def cgroup_cpus():
+    """CPUs' worth of time the cgroup grants this process (cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                return float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def all_cores():
+    """SURVEY.md §8(d)'s "all cores": the CPUs this process may run on (affinity), capped by the
+    cgroup's CPU quota when one is set (more threads than that only time-share the same cores)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    q = cgroup_cpus()
+    return max(1, min(usable, int(q))) if q else usable
+
+
 def host_info():
-    """The host the CPU baseline ran on: logical CPUs (nproc), the CPUs this process may use, the model."""
+    """The host the CPU baseline ran on: logical CPUs (nproc), the CPUs this process may use, the
+    cgroup's CPU quota, the model."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -175,26 +231,28 @@ def host_info():
         usable = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         usable = os.cpu_count()
-    return {"nproc": os.cpu_count(), "usable_cpus": usable, "cpu_model": model}
+    return {"nproc": os.cpu_count(), "usable_cpus": usable, "cgroup_cpu_quota": cgroup_cpus(), "cpu_model": model}
 
 
-def cpu_baseline(map_path, threads, burnin, uniform=False, po=False, runs=5):
+def cpu_baseline(map_path, threads, burnin, uniform=False, po=False, runs=5, utt=1):
     """The CPU oracle (C++ restatement of the Java engine; the JVM is not available) running the
     same workload: VecClient self-play + getMasks + the same Philox policy (or c2's uniform rows),
-    partially observable views for c5, std::thread shards over games.  Median of `runs` runs
-    (SURVEY.md §8(d)); a bounded sample (a few seconds of CPU time per run)."""
+    partially observable views for c5, std::thread shards over games — on all cores (`threads`,
+    all_cores()) and on one thread, the sequential loop of JNIGridnetVecClient.gameStep
+    (SURVEY.md §8(d)).  Median of `runs` runs; a bounded sample (a few seconds per run)."""
     import statistics
 
     from tests import oracle_py
 
     L = oracle_py.load()
-    games_per_thread, steps = (8 if po else 48), 300
+    games_per_thread, steps = 48, (100 if po else 300)
     games = games_per_thread * threads
-    flags = (1 if uniform else 0) | (2 if po else 0)
+    flags = (1 if uniform else 0) | (2 if po else 0) | (utt << 2)
     rates = [games * steps / L.oref_bench3(map_path.encode(), games, steps, threads, SEED, burnin, flags) for _ in range(runs)]
     ones = [games_per_thread * steps / L.oref_bench3(map_path.encode(), games_per_thread, steps, 1, SEED, burnin, flags)
             for _ in range(3)]
-    what = "uniform rows, no masks" if uniform else "masks + masked policy" + (", partially observable views" if po else "")
+    what = ("uniform rows, no masks" if uniform else "masks + masked policy" + (", partially observable views" if po else "")) + \
+        (f", UTT version {utt}" if utt != 1 else "")
     return {
         "value": statistics.median(rates),
         "unit": "env-steps/s",
@@ -318,6 +376,117 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
     }
 
 
+def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
+    """SURVEY.md §8e's second curve with the compact observation exchange: the same K
+    steps (multi-step launches of a.records_steps steps each, 0 = one launch), and after each launch an
+    in-place RCCL all-gather of every step's game records (the unit lists GameState.getVectorObservation
+    reads) on the handle's own stream, overlapping the next launch; barrier + synchronize bracket and
+    max over ranks as the headline.  The receiver's render of every rank's observations (uint8) is
+    timed separately per step (render_ms_per_step)."""
+    rx = mdist.RecordExchange(env, units_per_record=64, steps_per_launch=a.records_steps)
+
+    def run(first, n):
+        if mode["fused"]:
+            return rx.rollout_fused(SEED, first + 1, n)
+        return rx.rollout_uniform(SEED, first, n)
+
+    run(base, 3)  # untimed: the first collectives set up the communicator's channels
+    rx.buffer(a.steps)
+    torch.cuda.synchronize(env.device)
+    dist.barrier()
+    torch.cuda.synchronize(env.device)
+    t0 = time.perf_counter()
+    off = run(base + 3, a.steps)
+    torch.cuda.synchronize(env.device)
+    dist.barrier()
+    t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
+    # the receiving side: every rank's observations of one step back as uint8 planes
+    S = env.dims[0]
+    out8 = torch.zeros((world * S,) + tuple(env.obs.shape[1:]), dtype=torch.uint8, device=env.device)
+    n_r = min(5, a.steps)
+    e0, e1 = _FenceFreeEvent(), _FenceFreeEvent()
+    cur = torch.cuda.current_stream(env.device)
+    rx.render(off, 0, out8)
+    e0.record(cur)
+    for j in range(n_r):
+        rx.render(off, j, out8)
+    e1.record(cur)
+    torch.cuda.synchronize(env.device)
+    render_ms = e0.elapsed_time(e1) / n_r
+    rec_bytes = (S // 2) * rx.words * 4
+    return {
+        "value": total_games * a.steps / t,
+        "ms_per_step": 1e3 * t / a.steps,
+        "collective": "in-place RCCL all-gather (ring over xGMI) of each launch's compact game records: per game and step "
+                      f"{rx.words} words = live units (<= 64) x (cell, hp, resources, type, owner, action), the inputs of "
+                      "GameState.getVectorObservation; on the handle's own stream, overlapping the next launch",
+        "payload_bytes_per_rank_per_step": rec_bytes,
+        "observation_bytes_per_rank_per_step": {"uint8": env.obs.numel(), "int32": 4 * env.obs.numel()},
+        "render_ms_per_step": render_ms,
+        "render": f"mrts_render_records_dev: all {world} ranks' observations of one step rebuilt as uint8 "
+                  f"[{world * S}, {env.dims[3]}, {env.dims[1]}, {env.dims[2]}] (not in value: a consumer may read the "
+                  "records directly)",
+        "steps_per_launch": a.records_steps or "all",
+        "launch": "multi-step launches (each game's state in LDS), every step's records written by the step kernel",
+    }
+
+
+def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, dist, DeviceVecEnv):
+    """VERDICT r3 #3a — SURVEY.md §8(d)'s byte contract, as the Java client moves it: every mask byte
+    rewritten each step (JNIGridnetClientSelfPlay.java:196-209, mask_delta off), the policy as its own
+    launch reading the full masks and writing every action row, one step launch per step (a per-step
+    consumer), on a second handle with the headline's shard.  -> the JSON block."""
+    import numpy as np
+
+    from microrts_amd import UnitTypeTable
+
+    env = DeviceVecEnv(sh["n_slots"], 0, 2000, [os.path.join(ROOT, a.map)] * sh["n_slots"], device=local, seed=SEED,
+                       partial_obs=a.po, max_units=a.max_units, slot_id_base=sh["slot_id_base"], mask_delta=False,
+                       source_bits=False, utt=UnitTypeTable(a.utt, 1))
+    S, H, W, C, K = env.dims
+    env.reset()
+    for k in range(a.burnin):
+        env.random_policy(SEED, k)
+        env.step()
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream(env.device)
+    cap.wait_stream(torch.cuda.current_stream(env.device))
+    with torch.cuda.graph(graph, stream=cap):  # kernels only: no collective in this graph
+        for k in range(a.steps):
+            env.random_policy(SEED, a.burnin + k)
+            env.step()
+    torch.cuda.synchronize(env.device)
+    graph.replay()  # warm
+    torch.cuda.synchronize(env.device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(env.device)
+    t0 = time.perf_counter()
+    graph.replay()
+    torch.cuda.synchronize(env.device)
+    if world > 1:
+        dist.barrier()
+    t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
+    assert not env.error_flags().any()
+    units = float(np.mean([env.dump_state(s)[4] for s in range(0, min(S, 64), 2)]))
+    HW = H * W
+    survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * units + 2 * HW + 16))
+    env.close()
+    step_s = t / a.steps
+    return {
+        "value": total_games * a.steps / t,
+        "ms_per_step": 1e3 * step_s,
+        "mask_mode": "full (every mask byte rewritten every step)",
+        "policy": "separate masked-uniform policy launch per step (reads every mask byte, writes every action row)",
+        "launch": "hipGraph replay of K x (policy launch + step launch)",
+        "survey_8d_bytes_per_step": survey,
+        "survey_8d_GBps": survey / step_s / 1e9,
+        "survey_8d_frac": survey / step_s / 1e9 / HBM_PEAK_GBS,
+        "note": "SURVEY.md §8(d): B = A + O + M + S per env-step (all action rows read, int32 observation, uint8 masks, "
+                "live state); time = the whole step (policy + step kernels) from the wall clock",
+    }
+
+
 def main_c1(a, json_fd):
     """BASELINE config c1: one JNIBotClient env (bot-only JNIGridnetVecClient, :157-177 / JNIBotClient
     :108-135), RandomBiasedAI vs RandomBiasedAI — plumbing; the CPU oracle's rate is the reference
@@ -402,13 +571,15 @@ def main():
     use_pg = dist.is_initialized()
     rccl_world = dist.get_world_size() if use_pg else 1
     assert rccl_world == world, f"process group has {rccl_world} ranks, --gpus {a.gpus}"
-    from microrts_amd import DeviceVecEnv
+    from microrts_amd import DeviceVecEnv, UnitTypeTable
     from microrts_amd import dist as mdist
 
     E = a.envs
+    utt = UnitTypeTable(a.utt, 1)
+    utt_name = {1: "VERSION_ORIGINAL", 2: "VERSION_ORIGINAL_FINETUNED"}[a.utt] + ", CANCEL_BOTH"
     sh = mdist.shard(rank, E)
     env = DeviceVecEnv(sh["n_slots"], 0, 2000, [os.path.join(ROOT, a.map)] * sh["n_slots"], device=local, seed=SEED,
-                       partial_obs=a.po, max_units=a.max_units,
+                       partial_obs=a.po, max_units=a.max_units, utt=utt,
                        slot_id_base=sh["slot_id_base"], mask_delta=a.mask_mode == "delta",
                        source_bits=a.mask_mode == "delta")
     S, H, W, C, K = env.dims
@@ -500,19 +671,13 @@ def main():
     native = native_path
     if a.launch == "graph":
         try:
-            if gather_buf is not None:  # the capture starts with no collective in flight
-                gather_buf.wait()
-                torch.cuda.synchronize(env.device)
-                gather_buf.fired = [False, False]
+            assert gather_buf is None  # parse(): no torch.distributed collective is ever captured
             graph = torch.cuda.CUDAGraph()
             cap = torch.cuda.Stream(env.device)
             cap.wait_stream(torch.cuda.current_stream(env.device))
-            # thread_local: the process group's watchdog thread may query events during the capture
-            with torch.cuda.graph(graph, stream=cap, capture_error_mode="thread_local"):
+            with torch.cuda.graph(graph, stream=cap):
                 for k in range(a.steps):
                     one_step(base + k)
-                if gather_buf is not None:
-                    gather_buf.wait()  # the comm stream joins the capture: the last exchange is in the graph
             torch.cuda.synchronize(env.device)
         except Exception as ex:  # capture unsupported here: time eagerly instead
             print(f"bench: hipGraph capture failed ({ex!r}); eager launches", file=sys.stderr)
@@ -644,12 +809,18 @@ def main():
     traffic, traffic_src = a.pmc_traffic, "--pmc-traffic (bytes per launch)" if a.pmc_traffic is not None else None
     # per-config counters of the same command (tools/profile_config.sh + tools/profile_summary.py)
     pj = None
+    pmc_note = None
     pl = os.path.join(ROOT, "profiles", f"pmc_{a.config}.json")
     if os.path.exists(pl):
         pj = json.load(open(pl))
         if not (pj.get("envs_per_gpu") == E and a.map in (pj.get("workload") or "")
+                and pj.get("utt", "VERSION_ORIGINAL, CANCEL_BOTH") == utt_name
                 and pj.get("mask_mode") == ("off" if uniform else a.mask_mode) and launch_ms is not None):
             pj = None  # another workload or launch form: its counters do not describe this line
+        elif pj.get("libmrts_sha256") != lib_sha256():
+            pmc_note = (f"profiles/pmc_{a.config}.json was taken with another libmrts.so "
+                        f"({(pj.get('libmrts_sha256') or 'no hash')[:12]}); its counters are not used")
+            pj = None  # stale counters must not describe this library's kernel
     if traffic is None and pj is not None and pj.get("traffic_bytes_per_step"):
         per_step = pj["traffic_bytes_per_step"]
         traffic = per_step * steps_per_launch
@@ -657,43 +828,56 @@ def main():
                        f"{per_step / 1e6:.1f} MB per step x {steps_per_launch} steps per launch)")
     issue = None
     if pj is not None and pj.get("issue"):
-        # the issue roofline: VALU instructions per game-step x game-steps/s against the chip's VALU issue
-        # ceiling — 1024 SIMDs x one wave64 VALU instruction per quad-cycle each (SQ_ACTIVE_INST_VALU
-        # measured ~1 quad-cycle per instruction) at the clock GRBM_GUI_ACTIVE gives for the launch
+        # The issue roofline: VALU instructions per game-step (SQ_INSTS_VALU, this library's
+        # PMC pass) x game-steps/s against the SIMDs' VALU issue ceiling for THIS kernel's instruction mix:
+        # 1024 SIMDs x clock / c_mix, c_mix = the cycles per wave64 VALU instruction that the issue probe
+        # (tools/probes/valu_issue_probe.hip) measures per opcode class at the kernel's waves per SIMD with
+        # full EXEC, weighted by the kernel's static VALU opcode mix (tools/issue_roofline.py ->
+        # profiles/issue_ceiling_<cfg>.json).  The guide's flat 2 cycles per instruction is reported beside it.
         iq = pj["issue"]
         per = iq["per_game_step"]
         clk = iq.get("clock_ghz_grbm") or 2.4
         rate = E / (kern_ms * 1e-3)  # game-steps per second of kernel time
         valu = per["SQ_INSTS_VALU"] * rate
-        ceiling = 1024 * clk * 1e9 / 4
+        icp = os.path.join(ROOT, "profiles", f"issue_ceiling_{a.config}.json")
+        ic = json.load(open(icp)) if os.path.exists(icp) else None
+        c_mix = ic["c_mix_cycles"] if ic else 2.0
+        ceiling = 1024 * clk * 1e9 / c_mix
         issue = {
-            "bound": "valu_issue",
+            "achieved": valu / 1e9,
+            "peak": ceiling / 1e9,
+            "unit": "G wave64 VALU instructions/s",
+            "frac": valu / ceiling,
+            "c_mix_cycles_per_valu": c_mix,
+            "cycles_per_valu_achieved": 1024 * clk * 1e9 / valu,
+            "frac_vs_guide_2_cycles": valu / (1024 * clk * 1e9 / 2),
             "valu_insts_per_game_step": per["SQ_INSTS_VALU"],
             "salu_insts_per_game_step": per.get("SQ_INSTS_SALU"),
             "lds_insts_per_game_step": per.get("SQ_INSTS_LDS"),
-            "achieved": valu / 1e9,
-            "peak": ceiling / 1e9,
-            "unit": "G wave-VALU-instructions/s",
-            "frac": valu / ceiling,
-            "valu_busy_frac": iq.get("valu_busy_frac"),
             "valu_lane_utilization": iq.get("valu_lane_utilization"),
+            "valu_busy_frac": iq.get("valu_busy_frac"),
             "dual_issue_quad_cycles_per_game_step": per.get("SQ_ACTIVE_INST_VALU2"),
             "clock_ghz": clk,
-            "source": f"profiles/pmc_{a.config}.json ({pj['tag']}: SQ PMC pass of the same command)",
+            "games_per_simd": iq.get("games_per_simd"),
+            "source": f"profiles/pmc_{a.config}.json ({pj['tag']}: SQ PMC pass of the same command, same libmrts.so) + "
+                      + (f"profiles/issue_ceiling_{a.config}.json (probe {ic['probe']}, static mix of {ic['static_valu_instructions']} "
+                         "VALU opcodes)" if ic else "no issue_ceiling file: the guide's 2 cycles"),
         }
-    # what the counters show bounds the kernel: VALU issue when the SIMDs' vector issue is saturated
-    # over the waves' lifetimes (c3: four games per SIMD), else the per-game dependent chain (c2 / c5:
-    # one / two games per SIMD leave the issue half idle); HBM only without counters
-    if issue is not None and (issue.get("valu_busy_frac") or 0) >= 0.9:
-        bound, bound_note = "valu_issue", ("SIMD vector issue busy {:.0%} of the waves' lifetimes (roofline.issue); the "
-                                           "HBM figures are the step contract's bytes".format(issue["valu_busy_frac"]))
+    hbm_frac = achieved / HBM_PEAK_GBS
+    # what the numbers show bounds the kernel: VALU issue when the SIMDs issue this mix near its measured
+    # ceiling (c3: four games per SIMD), else the per-game dependent chain (c2 / c5: one / two games per
+    # SIMD leave issue slots idle); HBM only without counters
+    if issue is not None and issue["frac"] >= 0.6 and issue["frac"] > hbm_frac:
+        bound, bound_note = "valu_issue", ("VALU issue at {:.2f} of this kernel's probe-measured ceiling ({:.2f} cycles per "
+                                           "instruction for its mix; achieved {:.2f}), HBM at {:.2f} of peak (step-contract "
+                                           "bytes, roofline.frac)".format(issue["frac"], issue["c_mix_cycles_per_valu"],
+                                                                          issue["cycles_per_valu_achieved"], hbm_frac))
     elif issue is not None:
-        bound, bound_note = "latency", ("per-game dependent chain: SIMD vector issue busy only {:.0%} of the waves' "
-                                        "lifetimes with {:.0f} game(s) per SIMD (roofline.issue); the HBM figures are the "
-                                        "step contract's bytes".format(issue.get("valu_busy_frac") or 0,
-                                                                       (pj or {}).get("issue", {}).get("games_per_simd", 0)))
+        bound, bound_note = "latency", ("per-game dependent chain: VALU issue at {:.2f} of the probe-measured ceiling with "
+                                        "{:.0f} game(s) per SIMD (roofline.issue); HBM at {:.2f} of peak (step-contract "
+                                        "bytes)".format(issue["frac"], issue.get("games_per_simd") or 0, hbm_frac))
     else:
-        bound, bound_note = "hbm", "HBM step-contract bytes (no counter file for this workload)"
+        bound, bound_note = "hbm", "HBM step-contract bytes (no counter file of this library for this workload)"
     total_games = E * world
     value = total_games * a.steps / t
     out = {
@@ -711,23 +895,24 @@ def main():
         "dtype": "int32",
         "data": ("synthetic (unmasked uniform random rows for every cell, Philox seed 0x5EEDC0DE)" if uniform
                  else "synthetic (masked uniform random policy, Philox seed 0x5EEDC0DE)"),
-        "parity": "bit-exact vs the C++ oracle (trace-pinned: all 280 reference traces replay exactly; Java itself "
-                  "cannot run in this image) — tests/test_gpu_parity.py, tests/test_kats.py; value over the K timed "
-                  "steps above",
+        "parity": "bit-exact: the reference's 280 recorded games (data/traces, 17,085 entries) replay through these HIP "
+                  "kernels with every PhysicalGameState equal to the trace's (tests/test_gpu_traces.py); every output vs the "
+                  "trace-pinned C++ oracle (tests/test_gpu_parity.py, test_headline_parity.py at this config's full size, "
+                  "test_kats.py); Java itself cannot run in this image",
         "config": {
             "workload": f"{a.config}: {a.map} self-play, {E} games/GPU ({2 * E} player slots), "
                         + ("obs every step, no masks (SURVEY §8(d) c2)" if uniform else "masks+obs every step")
                         + (", partial observability" if a.po else "")
-                        + (f", max_units {a.max_units} (capacity errors checked)" if a.max_units else ""),
+                        + (f", max_units {a.max_units} (capacity errors checked)" if a.max_units else "")
+                        + (f", UTT version {a.utt}" if a.utt != 1 else ""),
             "envs_per_gpu": E,
-            "utt": "VERSION_ORIGINAL, CANCEL_BOTH",
+            "utt": utt_name,
             "reward_functions": "[WinLossRewardFunction] (with one reward function Java's self-play reset throws, "
                                 "JNIGridnetClientSelfPlay.java:235-238; here the one slot is zeroed — DESIGN.md §8)",
             "max_steps": 2000,
             "burnin_steps": a.burnin,
             "mask_mode": "off" if uniform else a.mask_mode,
-            "launch": ("hipGraph replay of the K timed steps and their RCCL exchanges" if graph is not None and gather_buf is not None
-                       else f"one {'mrts_rollout_uniform_dev' if uniform else 'mrts_rollout_fused_dev'} call: ONE k_env launch runs the K steps of every game (multi-step "
+            "launch": (f"one {'mrts_rollout_uniform_dev' if uniform else 'mrts_rollout_fused_dev'} call: ONE k_env launch runs the K steps of every game (multi-step "
                        "launch, each game's state kept in LDS between its steps; every step's observation, masks, "
                        "rewards, dones and next action rows written to HBM)" if multi
                        else "one mrts_rollout_uniform_dev call (K fused policy+step launches from C++)" if native and uni_fused
@@ -763,7 +948,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_source": traffic_src,
+            "traffic_source": traffic_src if pmc_note is None else pmc_note,
             "kernel": "k_env<MODE_STEP>" + (" + fused policy rows" if fused else " + fused uniform rows" if uni_fused else ""),
             "alg_bytes_per_launch": contract * steps_per_launch,
             "alg_bytes_per_step": contract,
@@ -826,12 +1011,13 @@ def main():
         out["other_policy_form"] = {"policy": "uniform-split" if mode["uni_fused"] else "uniform",
                                     "value": total_games * a.steps / t2, "ms_per_step": 1e3 * t2 / a.steps}
         assert not env.error_flags().any()
+    if not a.no_full_contract and not uniform and gather_buf is None:
+        out["full_contract"] = full_contract_window(a, sh, local, base, E * world, world, mdist, torch, dist, DeviceVecEnv)
     if gather_buf is None and not a.no_gather_window:
-        # SURVEY.md §8e's second curve: the same step with the north-star observation exchange every
-        # step (RCCL all-gather of the int16 observation tensor over xGMI, written by the step kernel
-        # under full observability, on a comm stream overlapping the next step).  A per-step consumer
-        # cannot use multi-step launches, so this window runs one step launch per step, captured with
-        # its collectives in one hipGraph.
+        # SURVEY.md §8e's second curve: the same steps with the north-star observation exchange — by
+        # default the compact game records of every step, all-gathered once per launch (records_window,
+        # DESIGN.md §7); --gather-window tensor: the per-step all-gather of the observation tensor itself
+        # (one step launch per step, libmrts's own capture of the steps and their collectives).
         if not use_pg:
             out["with_gather"] = {"error": f"no process group: {pg_error}"}
         else:
@@ -844,16 +1030,24 @@ def main():
                 sys.stderr.flush()
                 os._exit(0)
 
+            records_ok = (a.gather_window == "records" and dist.get_backend() != "gloo" and not a.po and native
+                          and (mode["fused"] or mode["uni_fused"]))
             try:
-                out["with_gather"] = run_with_deadline(
-                    lambda: gather_window(env, a, xg, one_step, base + 3 * a.steps + 20, E * world, world, mdist, torch,
-                                          dist, mode), a.gather_timeout, give_up)
+                if records_ok:
+                    out["with_gather"] = run_with_deadline(
+                        lambda: records_window(env, a, mode, base + 3 * a.steps + 20, E * world, world, mdist, torch, dist),
+                        a.gather_timeout, give_up)
+                else:
+                    out["with_gather"] = run_with_deadline(
+                        lambda: gather_window(env, a, xg, one_step, base + 3 * a.steps + 20, E * world, world, mdist, torch,
+                                              dist, mode), a.gather_timeout, give_up)
             except Exception as ex:  # the headline line must survive a failed exchange window
                 print(f"bench: exchange window failed: {ex!r}", file=sys.stderr)
                 out["with_gather"] = {"error": repr(ex)}
             assert not env.error_flags().any()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads, a.burnin, uniform, po=a.po)
+        out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads or all_cores(), a.burnin, uniform, po=a.po,
+                                           utt=a.utt)
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

@@ -53,7 +53,8 @@ enum {
     MRTS_ERR_PRODUCE_TYPE = 1u << 2,  /* decoded produce type out of range: Java throws (UnitAction.java:697) */
     MRTS_ERR_OLDER_CONFLICT = 1u << 3,/* issue() older-conflict branch: Java prints (GameState.java:298-317) */
     MRTS_ERR_NEG_RESOURCES = 1u << 4, /* produce skipped at execution: Java prints (UnitAction.java:457-461) */
-    MRTS_ERR_MOVE_COLLISION = 1u << 5 /* internal invariant (one unit per cell) violated */
+    MRTS_ERR_MOVE_COLLISION = 1u << 5,/* internal invariant (one unit per cell) violated */
+    MRTS_ERR_RECORD = 1u << 6         /* more live units than an observation record holds (mrts_set_records) */
 };
 
 typedef struct {
@@ -206,6 +207,37 @@ int mrts_set_exchange_bytes(mrts_env* env, int32_t bytes_per_value);
 int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
                                       double* d_reward, uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps,
                                       int16_t* d_send0, int16_t* d_send1, int16_t* d_recv, void* stream);
+/* Compact observation exchange (the payload of BASELINE configs[3]'s all-gather).  The
+ * observation GameState.getVectorObservation returns (rts/GameState.java:922-968) is a pure function of
+ * the unit list (position, hp, resources, owner, type, the assignment's action type) and the map's
+ * terrain, so the exchange all-gathers that: one record per game and step = 1 + units_per_record
+ * 32-bit words (live units in list order; layout in microrts_amd/csrc/mrts_internal.h recWords), and
+ * the receiver rebuilds any rank's observations with mrts_render_records_dev.  c3: ~0.26 KB per game
+ * instead of 3 KB of uint8 planes for its two slots.
+ * mrts_set_records: units per record (0 = off) and steps per launch of a records rollout (0 = up to
+ * MRTS_MAX_ITER); self-play handles with full observability on maps of <= 256 cells whose every
+ * observation value fits a byte, else -ENOTSUP.  A game with more live units than a record holds sets
+ * MRTS_ERR_RECORD.
+ * mrts_rollout_{fused,uniform}_records_dev: mrts_rollout_{fused,uniform}_dev's steps (multi-step
+ * launches where possible), each launch's records written at this rank's place of its chunk of d_recv
+ * and all-gathered in place on the handle's RCCL communicator (mrts_exchange_init) while the next launch
+ * runs; all collectives are complete when `stream` reaches the end of the call.  d_recv (16-byte aligned)
+ * holds n_steps * nranks * n_games * (1 + units_per_record) words; step_offsets (may be NULL) receives,
+ * per step, int64 [2]: the word offset in d_recv of rank 0's records of that step and the stride between
+ * consecutive ranks' records of it.
+ * mrts_render_records_dev: records of n_ranks x n_games games (rank r's game g at d_rec + r * rank_stride
+ * + g * (1 + units_per_record) words; the terrain of game g from this handle's map of game g) into
+ * d_out [n_ranks][2 * n_games][C][H][W] as uint8 (out_bytes 1) or int32 (out_bytes 4, 16-byte aligned). */
+int mrts_set_records(mrts_env* env, int32_t units_per_record, int32_t steps_per_launch);
+int mrts_rollout_fused_records_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                   double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed,
+                                   uint32_t first_next_step, int32_t n_steps, uint32_t* d_recv, int64_t* step_offsets,
+                                   void* stream);
+int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                     double* d_reward, uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps,
+                                     uint32_t* d_recv, int64_t* step_offsets, void* stream);
+int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,
+                            int32_t out_bytes, void* stream);
 /* Graph form of a handle's calls (no Java counterpart): everything this handle enqueues on `stream`
  * between mrts_capture_begin and mrts_capture_end (stream capture, thread-local mode; the exchange
  * stream of an exchange rollout is joined inside the call) is instantiated as one graph, which

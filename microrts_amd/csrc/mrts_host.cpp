@@ -43,6 +43,8 @@ hipError_t prepareLds(size_t bytes);
 hipError_t launchCopyGames(int32_t* dst, const int32_t* src, const int32_t* pairs, int n, int n_dst, int n_src,
                            int CAP, int HW, hipStream_t stream);
 hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, float* out, hipStream_t stream);
+hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
+                               int64_t rank_stride, void* out, int out_bytes, hipStream_t stream);
 }  // namespace mrts
 
 static thread_local std::string g_err;
@@ -490,7 +492,10 @@ struct mrts_env {
     // native observation exchange (mrts_exchange_init): an RCCL communicator over this handle's ranks,
     // its own communication stream, and per send buffer the step-ready / collective-done events
     ncclComm_t exComm = nullptr;
-    int exRanks = 0;
+    int exRanks = 0, exRank = 0;
+    // compact observation records (mrts_set_records): units per record (0 = off), steps per launch of a
+    // records rollout (0 = as many as a launch can run)
+    int recUnits = 0, recSteps = 0;
     hipStream_t exStream = nullptr;
     hipEvent_t exReady[2] = {nullptr, nullptr}, exDone[2] = {nullptr, nullptr};
     // mrts_capture_begin / _end / mrts_replay: the calls enqueued in between, as one instantiated graph
@@ -924,13 +929,24 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
 }
 
 namespace {
+// records rollout (mrts_rollout_*_records_dev): the launch writes its steps' records into `chunk`, the
+// part of the receive buffer its all-gather fills, at this rank's place ([rank][n_iter][games][words])
+struct RecPlan {
+    uint32_t* chunk;
+    int rank;
+};
+void planRecords(const mrts_env* env, KDyn& D, const RecPlan* rec) {
+    if (!rec) return;
+    D.rec_units = env->recUnits;
+    D.rec_out = rec->chunk + (size_t)rec->rank * D.n_iter * env->nGames * recWords(env->recUnits);
+}
 // n_iter consecutive fused steps (next_step, next_step + 1, ...) as ONE launch when the handle runs a
 // specialised full-observability self-play kernel and is in the steady fused state (the previous
 // launch was a fused step on these buffers: delta masks and policy rows, forwarded action words);
 // else one step.  Returns the number of steps enqueued.
 int stepFused(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
               uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t next_step, int32_t n_iter, void* stream,
-              hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+              hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, const RecPlan* rec = nullptr) {
     if (!d_actions || !d_masks) throw Fail{-EINVAL, "actions and masks are required"};
     if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
     HIPCHK(hipSetDevice(env->device));
@@ -953,6 +969,7 @@ int stepFused(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32
     D.fwd_read = env->fusedActions == d_actions ? 1 : 0;  // games check H_FWD == this stamp - 1
     const bool steady = D.pol_delta && D.fwd_read && D.mask_delta && envIterable(env->hstatic);
     D.n_iter = (steady && n_iter > 1) ? n_iter : 1;
+    planRecords(env, D, rec);
     HIPCHK(env->launch(0, D, pickStream(env, stream), e0, e1));
     env->fusedActions = d_actions;
     if (env->lastPolicyActions == d_actions) env->polValid = false;  // the standalone policy's delta base is stale
@@ -1131,7 +1148,7 @@ namespace {
 // are drawn in the kernel, so no steady state is needed), else one.  Returns the steps enqueued.
 int stepUniform(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs, double* d_reward, uint8_t* d_done,
                 uint8_t* d_masks, int32_t mask_player, uint64_t seed, uint32_t step, int32_t n_iter, void* stream,
-                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+                hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr, const RecPlan* rec = nullptr) {
     if (!env || !d_actions) throw Fail{-EINVAL, "null argument"};
     if ((uintptr_t)d_actions & 3) throw Fail{-EINVAL, "misaligned buffer"};
     if (env->forwardModel) throw Fail{-EINVAL, "a forward-model handle advances through mrts_playout*"};
@@ -1154,6 +1171,7 @@ int stepUniform(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int
     // masks in a loop need the delta row sets of the previous write (kept in LDS between iterations)
     const bool loopable = envIterable(env->hstatic) && (!d_masks || D.mask_delta);
     D.n_iter = (loopable && n_iter > 1) ? n_iter : 1;
+    planRecords(env, D, rec);
     if (d_masks || env->fusedActions == d_actions) env->fusedActions = nullptr;
     if (env->lastPolicyActions == d_actions) env->polValid = false;
     HIPCHK(env->launch(0, D, pickStream(env, stream), e0, e1));
@@ -1274,8 +1292,115 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t*
     env->obs16 = saved;
     env->obs8 = nullptr;
 }
+// The compact-record exchange (mrts_rollout_*_records_dev): launches of up to recSteps steps write every
+// step's game records into the receive buffer at this rank's place of the launch's chunk; after each
+// launch, an in-place all-gather of that chunk on the exchange stream (it overlaps the next launch,
+// which writes the next chunk).  step(k, n, plan) enqueues up to n steps from step k and returns how
+// many it enqueued.
+template <class StepFn>
+void recordsLoop(mrts_env* env, int32_t n_steps, uint32_t* d_recv, int64_t* offsets, void* stream, StepFn step) {
+    if (!env->exComm) throw Fail{-EINVAL, "mrts_exchange_init first"};
+    if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
+    if (!d_recv || ((uintptr_t)d_recv & 15)) throw Fail{-EINVAL, "the receive buffer must be non-null and 16-byte aligned"};
+    if (!env->obsImg) throw Fail{-ENOTSUP, "records: an observation value no longer fits a byte"};
+    HIPCHK(hipSetDevice(env->device));
+    hipStream_t s = pickStream(env, stream);
+    const size_t per = (size_t)env->nGames * recWords(env->recUnits);  // words per rank and step
+    size_t base = 0;                                                   // words of d_recv filled so far
+    bool any = false;
+    for (int32_t k = 0; k < n_steps;) {
+        const int32_t cap = env->multiStep ? (env->recSteps > 0 ? env->recSteps : MRTS_MAX_ITER) : 1;
+        const RecPlan rp{d_recv + base, env->exRank};
+        const int32_t n = step(k, std::min<int32_t>(n_steps - k, cap), &rp);
+        HIPCHK(hipEventRecord(env->exReady[0], s));
+        HIPCHK(hipStreamWaitEvent(env->exStream, env->exReady[0], 0));
+        const size_t words = (size_t)n * per;
+        ncclChk(g_rccl.allGather(d_recv + base + (size_t)env->exRank * words, d_recv + base, words * 4, ncclUint8, env->exComm,
+                                 env->exStream),
+                "ncclAllGather");
+        if (offsets)
+            for (int32_t j = 0; j < n; j++) {
+                offsets[2 * (size_t)(k + j)] = (int64_t)(base + (size_t)j * per);
+                offsets[2 * (size_t)(k + j) + 1] = (int64_t)words;
+            }
+        base += (size_t)env->exRanks * words;
+        k += n;
+        any = true;
+    }
+    if (any) {  // the caller's stream covers every collective of the call
+        HIPCHK(hipEventRecord(env->exDone[0], env->exStream));
+        HIPCHK(hipStreamWaitEvent(s, env->exDone[0], 0));
+    }
+}
 }  // namespace
 extern "C" {
+
+int mrts_set_records(mrts_env* env, int32_t units_per_record, int32_t steps_per_launch) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    if (units_per_record == 0) {
+        env->recUnits = 0;
+        return 0;
+    }
+    if (units_per_record < 1 || units_per_record > 0xFFFF || steps_per_launch < 0)
+        return fail(Fail{-EINVAL, "units per record 1..65535, steps per launch >= 0"});
+    if (env->partialObs || env->HW > 256 || (env->HW & 3) || env->utt.ntypes > 7 || !env->obsImg || env->nSpGames != env->nGames)
+        return fail(Fail{-ENOTSUP, "records: self-play handles, full observability, maps of <= 256 cells (a multiple of 4), "
+                                   "<= 7 unit types, every observation value < 256"});
+    env->recUnits = units_per_record;
+    env->recSteps = steps_per_launch;
+    return 0;
+}
+
+int mrts_rollout_fused_records_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                   double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed,
+                                   uint32_t first_next_step, int32_t n_steps, uint32_t* d_recv, int64_t* step_offsets,
+                                   void* stream) {
+    if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
+    try {
+        RolloutEvents ev(env, stream);
+        recordsLoop(env, n_steps, d_recv, step_offsets, stream, [&](int32_t k, int32_t n, const RecPlan* rp) {
+            return stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
+                             first_next_step + (uint32_t)k, n, stream, nullptr, nullptr, rp);
+        });
+        ev.done();
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
+                                     double* d_reward, uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps,
+                                     uint32_t* d_recv, int64_t* step_offsets, void* stream) {
+    if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
+    try {
+        RolloutEvents ev(env, stream);
+        recordsLoop(env, n_steps, d_recv, step_offsets, stream, [&](int32_t k, int32_t n, const RecPlan* rp) {
+            return stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, n,
+                               stream, nullptr, nullptr, rp);
+        });
+        ev.done();
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,
+                            int32_t out_bytes, void* stream) {
+    try {
+        if (!env || !d_rec || !d_out || n_ranks < 1 || rank_stride < 0) throw Fail{-EINVAL, "bad argument"};
+        if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
+        if (out_bytes != 1 && out_bytes != 4) throw Fail{-EINVAL, "out_bytes: 1 (uint8) or 4 (int32)"};
+        if (((uintptr_t)d_out & (out_bytes == 4 ? 15 : 3)) || ((uintptr_t)d_rec & 3)) throw Fail{-EINVAL, "misaligned buffer"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(launchRenderRecords(env->hstatic, env->d_static, d_rec, env->recUnits, n_ranks, rank_stride, d_out, out_bytes,
+                                   pickStream(env, stream)));
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
 
 int mrts_capture_begin(mrts_env* env, void* stream) {
     try {
@@ -1338,6 +1463,7 @@ int mrts_exchange_init(mrts_env* env, const char* rccl_path, int32_t nranks, int
         std::memcpy(&id, unique_id, sizeof(id));
         ncclChk(g_rccl.commInitRank(&env->exComm, nranks, id, rank), "ncclCommInitRank");
         env->exRanks = nranks;
+        env->exRank = rank;
         HIPCHK(hipStreamCreateWithFlags(&env->exStream, hipStreamNonBlocking));
         for (int b = 0; b < 2; b++) {
             HIPCHK(hipEventCreateWithFlags(&env->exReady[b], hipEventDisableTiming));

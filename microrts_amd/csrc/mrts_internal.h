@@ -186,7 +186,16 @@ struct KDyn {
     const int32_t* trace_until;
     int32_t* trace_out;
     int32_t trace_generic;
+    // compact observation records (mrts_rollout_*_records_dev): after each step's observation write, game
+    // g of iteration it writes its record at rec_out + (it * n_sp_games + g) * (1 + rec_units) words
+    // (recWord in mrts_kernels.hip); null = off
+    uint32_t* rec_out;
+    int32_t rec_units;
 };
+// compact observation record of one game (full observability, maps of <= 256 cells, every plane value
+// < 256): word 0 = live units n (<= rec_units) | overflow << 31, then one word per live unit in list
+// order: cell | hp << 8 | resources << 16 | (type + 1) << 24 | (player + 1) << 27 | action type << 29
+constexpr int recWords(int units) { return 1 + units; }
 constexpr int BAL_COST = 16;
 constexpr int PRIO_KEYS = 8 * 8 * 2 * 16 * 4;  // XCC x SE x SH x CU x SIMD (HW_ID / XCC_ID fields)
 // PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);

@@ -112,7 +112,7 @@ DEV int prodCategory(uint32_t typeFlags) {  // the reward functions' name tests 
 enum { GK_PASSIVE = 0, GK_RANDOM_BIASED = 1 };                    // AI kinds (bits 4-7 ai1, 8-11 ai2)
 enum : uint32_t {
     E_CAPACITY = 1u << 0, E_ADDUNIT = 1u << 1, E_PRODUCE_TYPE = 1u << 2, E_OLDER = 1u << 3,
-    E_NEG_RES = 1u << 4, E_COLLISION = 1u << 5
+    E_NEG_RES = 1u << 4, E_COLLISION = 1u << 5, E_RECORD = 1u << 6
 };
 // MODE_TRACE per-game result word (KDyn.trace_out)
 enum : uint32_t { TR_ISSUED = 1u, TR_GAMEOVER = 2u, TR_NO_UNIT = 4u };
@@ -2790,6 +2790,34 @@ struct Game {
             }
         }
     }
+    // The compact observation record of this game (KDyn.rec_out, mrts_internal.h recWords): the live
+    // units in list order, one word each — every field GameState.getVectorObservation reads
+    // (rts/GameState.java:922-968: hp, resources, owner, type, the assignment's action type; the
+    // terrain plane is the map's).  Both players' observations follow from it (the owner plane is
+    // ((owner + p) % 2) + 1), so one record per game replaces 2 x 6 x HW observation values on the
+    // wire of the exchange (k_render_records rebuilds them).  More live units than the record holds
+    // set E_RECORD (the exchange then reports an error).
+    DEV void writeRecord(int it) {
+        const int RU = D.rec_units;
+        uint32_t* r = D.rec_out + ((size_t)it * D.n_sp_games + g) * (size_t)recWords(RU);
+        int n = 0;
+        for (int s0 = 0; s0 < nu; s0 += 64) {
+            const int s = s0 + lid();
+            const uint32_t cu = s < nu ? uc[s] : UC_DEAD;
+            const bool live = !(cu & UC_DEAD);
+            const uint64_t m = ballot(live);
+            const int idx = n + lanes_below(m);
+            if (live && idx < RU) {
+                const uint32_t a = ua[s];
+                const uint32_t act = (a & UA_PRESENT) ? (uint32_t)ua_type(a) : 0u;
+                r[1 + idx] = (uint32_t)(uy(cu) * W + ux(cu)) | (((uint32_t)hp[s] & 0xFFu) << 8) | (((uint32_t)res[s] & 0xFFu) << 16) |
+                             ((uint32_t)(utyp(cu) + 1) << 24) | ((uint32_t)(uplay(cu) + 1) << 27) | (act << 29);
+            }
+            n += __popcll(m);
+        }
+        if (lid() == 0) r[0] = (uint32_t)(n < RU ? n : RU) | (n > RU ? 0x80000000u : 0u);
+        if (n > RU) addErr(E_RECORD);
+    }
     // helper-wave launch: the observation's cells for the helper wave to render (lane = cell, HW <= 64),
     // player 0's view: word 0 = hp | resources << 16, word 1 = owner | type << 4 | action << 8 | wall << 12
     DEV void packObs(uint32_t* buf) const {
@@ -4934,6 +4962,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
 #endif
         }
     }
+    if (MODE == MODE_STEP && MRTS_UNLIKELY(D.rec_out != nullptr) && external) G.writeRecord(it);
     if (HELP && !FPO) __syncthreads();  // A_{it+1}: step it's cells packed; the helper's rows of step it + 1 ready
     if (HELP && FPO) {
         if (poHelpFlags == 0u && G.lid() == 0) poHelpHdr[(it & 1) * 4 + 2] = 0u;
@@ -5342,6 +5371,77 @@ hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t st
 // the dst game keeps its own random streams (Sampler.generator / GameState.r / UnitAction.r are
 // JVM-global, not part of a GameState), its kind (playout policies), and its mask row sets (they
 // describe the dst handle's mask buffer).  One block of 256 threads per pair.
+// Receiver side of the compact observation exchange: the records of n_ranks x n_games games (rank r's
+// game g at rec + r * rank_stride + g * recWords(units) words) back into both player slots'
+// observation planes — GameState.getVectorObservation (rts/GameState.java:922-968), the owner plane
+// per viewing player (:947-949), the terrain plane from the local handle's map of game g (every rank
+// holds the same maps per game index).  out = [n_ranks][2 * n_games][C][HW] as uint8 (out_bytes 1)
+// or int32 (4).  One wave per game: the units paint a byte image in LDS, then each lane stores 4 cells
+// per plane.  HW <= 256, HW % 4 == 0 (the host checks).
+__global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict__ PS, const uint32_t* __restrict__ rec,
+                                                       int units, int64_t rank_stride, void* __restrict__ out, int out_bytes) {
+    __shared__ uint32_t imgw[5 * 256 / 4];
+    uint8_t* img = (uint8_t*)imgw;
+    const KStatic& P = *PS;
+    const int g = (int)blockIdx.x, r = (int)blockIdx.y, l = (int)threadIdx.x, HW = P.HW, C = P.C, G = P.n_games;
+    const uint32_t* rc = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units);
+    for (int i = l; i < 5 * HW / 4; i += 64) imgw[i] = 0u;
+    const uint32_t hdr = rc[0];
+    __syncthreads();
+    const int n = (int)(hdr & 0xFFFFu);
+    for (int i = l; i < n; i += 64) {
+        const uint32_t w = rc[1 + i];
+        const int c = (int)(w & 0xFFu);
+        img[c] = (uint8_t)(w >> 8);
+        img[HW + c] = (uint8_t)(w >> 16);
+        img[2 * HW + c] = (uint8_t)((w >> 27) & 3u);
+        img[3 * HW + c] = (uint8_t)((w >> 24) & 7u);
+        img[4 * HW + c] = (uint8_t)(w >> 29);
+    }
+    __syncthreads();
+    const uint32_t* terr = (const uint32_t*)(P.tmpl + P.tmpl_off[g] + T_TERR);
+    const size_t slot0 = (size_t)r * 2 * G + 2 * (size_t)g;
+    for (int c4 = 4 * l; c4 < HW; c4 += 256) {
+        uint32_t pw[6];
+#pragma unroll
+        for (int q = 0; q < 5; q++) pw[q] = imgw[(q * HW + c4) >> 2];
+        const uint32_t t = terr[c4 >> 2];  // walls: non-zero terrain bytes
+        uint32_t tw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) tw |= (((t >> (8 * j)) & 0xFFu) ? 1u : 0u) << (8 * j);
+        pw[5] = tw;
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                uint32_t w = pw[q];
+                if (i == 1 && q == 2) {  // the other player's owners: 1 <-> 2, 0 stays
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t b = (w >> (8 * j)) & 0xFFu;
+                        x |= (b ? 3u - b : 0u) << (8 * j);
+                    }
+                    w = x;
+                }
+                const size_t off = ((slot0 + i) * C + q) * (size_t)HW + c4;
+                if (out_bytes == 1) {
+                    *(uint32_t*)((uint8_t*)out + off) = w;
+                } else {
+                    st4<true>((int32_t*)out + off, (int)(w & 0xFFu), (int)((w >> 8) & 0xFFu), (int)((w >> 16) & 0xFFu),
+                              (int)(w >> 24));
+                }
+            }
+        }
+    }
+}
+hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
+                               int64_t rank_stride, void* out, int out_bytes, hipStream_t stream) {
+    hipLaunchKernelGGL(k_render_records, dim3((unsigned)hs.n_games, (unsigned)n_ranks), dim3(64), 0, stream, ds, rec, units,
+                       rank_stride, out, out_bytes);
+    return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_copy_games(int32_t* __restrict__ dst, const int32_t* __restrict__ src,
                                                     const int32_t* __restrict__ pairs, int n_dst, int n_src,
                                                     int words, int maskLo, int maskHi) {

@@ -215,3 +215,52 @@ class NativeExchange:
 
     def replay(self):
         self.env.replay()
+
+
+class RecordExchange:
+    """The compact observation exchange (mrts_rollout_*_records_dev): every step's game
+    records — the unit lists GameState.getVectorObservation reads (rts/GameState.java:922-968), ~20x
+    fewer bytes than the observation planes — all-gathered over the handle's own RCCL communicator,
+    one in-place all-gather per launch, overlapping the next launch; env.render_records rebuilds any
+    rank's observations.  Every rank of `group` must construct it (ncclCommInitRank is collective)."""
+
+    def __init__(self, env, units_per_record=64, steps_per_launch=0, group=None):
+        import ctypes
+
+        from microrts_amd import _lib
+
+        self.env = env
+        self.world, self.rank = dist.get_world_size(group), dist.get_rank(group)
+        L, h = env._h.L, env._h.h
+        self.words = env.set_records(units_per_record, steps_per_launch)
+        path = rccl_library_path().encode()
+        uid = (ctypes.c_char * 128)()
+        ok = L.mrts_rccl_unique_id(path, uid) == 0
+        flag = torch.tensor([1 if ok else 0], device=env.device if dist.get_backend(group) != "gloo" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+        if not bool(flag.item()):
+            why = L.mrts_last_error().decode() if not ok else "another rank"
+            raise RuntimeError(f"RCCL could not be bound on every rank: {why}")
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=0, group=group)
+        uid = (ctypes.c_char * 128).from_buffer_copy(box[0])
+        _lib.check(L.mrts_exchange_init(h, path, self.world, self.rank, uid))
+        self.recv = None
+
+    def buffer(self, n_steps):
+        if self.recv is None or self.recv.numel() < n_steps * self.world * (self.env.dims[0] // 2) * self.words:
+            self.recv = self.env.records_buffer(n_steps, self.world)
+        return self.recv
+
+    def rollout_fused(self, seed, first_next_step, n_steps):
+        """env.rollout_fused(...) with every step's records all-gathered into self.recv; returns the
+        per-step (offset, rank stride) table."""
+        return self.env.rollout_fused_records(seed, first_next_step, n_steps, self.buffer(n_steps))
+
+    def rollout_uniform(self, seed, first_step, n_steps):
+        return self.env.rollout_uniform_records(seed, first_step, n_steps, self.buffer(n_steps))
+
+    def render(self, offsets, step, out):
+        """All ranks' observations of step `step` of the last rollout into out [world * slots, C, H, W]."""
+        off, stride = offsets[step]
+        return self.env.render_records(self.recv, int(off), int(stride), self.world, out)

@@ -567,6 +567,56 @@ class DeviceVecEnv:
                                                          self._p(send[1]), self._p(recv), self._s(stream)))
         self._obs_written()
 
+    def set_records(self, units_per_record=64, steps_per_launch=0):
+        """Enable the compact observation records (mrts_set_records): units per game record (0 = off) and
+        steps per launch of a records rollout (0 = as many as a launch runs).  Returns words per record."""
+        _lib.check(self._h.L.mrts_set_records(self._h.h, int(units_per_record), int(steps_per_launch)))
+        self.record_units = int(units_per_record)
+        return 1 + self.record_units
+
+    def records_buffer(self, n_steps, world=1):
+        """A receive buffer for n_steps of a records rollout over `world` ranks (uint32 words)."""
+        return self.torch.zeros(n_steps * world * (self._h.S // 2) * (1 + self.record_units), dtype=self.torch.int32,
+                                device=self.device)
+
+    def rollout_fused_records(self, seed, first_next_step, n_steps, recv, stream=None):
+        """rollout_fused whose every step's game records are all-gathered into recv
+        (mrts_rollout_fused_records_dev; microrts_amd.dist.RecordExchange sets it up).  Returns the
+        per-step (word offset of rank 0's records, rank stride) as int64 [n_steps, 2]."""
+        h = self._h
+        if self._policy_out is not None and self._policy_out is self.actions and self.actions._version != self._policy_version:
+            _lib.check(h.L.mrts_policy_invalidate(h.h))
+        self._obs_guard()
+        a, pl, o, r, d, m = self._bufs()
+        off = np.zeros((max(n_steps, 1), 2), dtype=np.int64)
+        _lib.check(h.L.mrts_rollout_fused_records_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, first_next_step, n_steps,
+                                                      self._p(recv), off.ctypes.data_as(ctypes.c_void_p), self._s(stream)))
+        self._obs_written()
+        self._policy_out, self._policy_version = self.actions, self.actions._version
+        return off[:n_steps]
+
+    def rollout_uniform_records(self, seed, first_step, n_steps, recv, stream=None):
+        """rollout_uniform (fused form) whose every step's game records are all-gathered into recv
+        (mrts_rollout_uniform_records_dev).  Returns the per-step offsets as rollout_fused_records."""
+        h = self._h
+        self._obs_guard()
+        a, pl, o, r, d, _ = self._bufs()
+        off = np.zeros((max(n_steps, 1), 2), dtype=np.int64)
+        _lib.check(h.L.mrts_rollout_uniform_records_dev(h.h, a, pl, o, r, d, seed, first_step, n_steps, self._p(recv),
+                                                        off.ctypes.data_as(ctypes.c_void_p), self._s(stream)))
+        self._obs_written()
+        return off[:n_steps]
+
+    def render_records(self, recv, offset, rank_stride, n_ranks, out, stream=None):
+        """The observations of n_ranks x games records (rank r's at recv[offset + r * rank_stride:]) into
+        out [n_ranks * slots, C, H, W] (uint8 or int32) — mrts_render_records_dev."""
+        h = self._h
+        ob = out.element_size()
+        assert ob in (1, 4) and out.is_contiguous() and out.numel() == n_ranks * self.obs.numel()
+        ptr = ctypes.c_void_p(recv.data_ptr() + 4 * int(offset))
+        _lib.check(h.L.mrts_render_records_dev(h.h, ptr, int(n_ranks), int(rank_stride), self._p(out), ob, self._s(stream)))
+        return out
+
     def step_rows(self, rows, stream=None):
         """gameStep with Java rows: int32 [slots][n_rows][8] on this device (any order, duplicates ok)."""
         h = self._h

@@ -945,9 +945,10 @@ double oref_bench3(const char* map_path, int n_games, int steps, int threads, ui
 double oref_bench2(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin, int uniform) {
     return oref_bench3(map_path, n_games, steps, threads, seed, burnin, uniform ? 1 : 0);
 }
-// flags bit 0: uniform rows (c2); bit 1: partially observable views (c5, PartiallyObservableGameState)
+// flags bit 0: uniform rows (c2); bit 1: partially observable views (c5, PartiallyObservableGameState);
+// bits 2-3: the UnitTypeTable version (0 = 1, VERSION_ORIGINAL; 2 = VERSION_ORIGINAL_FINETUNED)
 double oref_bench3(const char* map_path, int n_games, int steps, int threads, uint64_t seed, int burnin, int flags) {
-    const int uniform = flags & 1, po = (flags >> 1) & 1;
+    const int uniform = flags & 1, po = (flags >> 1) & 1, uttv = ((flags >> 2) & 3) ? ((flags >> 2) & 3) : 1;
     std::mutex mu;
     std::condition_variable cv;
     int arrived = 0;
@@ -957,7 +958,7 @@ double oref_bench3(const char* map_path, int n_games, int steps, int threads, ui
     for (int t = 0; t < threads; t++) {
         per[(size_t)t] = n_games / threads + (t < n_games % threads ? 1 : 0);
         std::vector<const char*> paths((size_t)per[(size_t)t] * 2, map_path);
-        hs[(size_t)t] = oref_create(per[(size_t)t] * 2, 0, nullptr, 2000, po, 1, 1, paths.data(), seed + (uint64_t)t * 1000003ULL, nullptr);
+        hs[(size_t)t] = oref_create(per[(size_t)t] * 2, 0, nullptr, 2000, po, uttv, 1, paths.data(), seed + (uint64_t)t * 1000003ULL, nullptr);
         oref_reset(hs[(size_t)t], nullptr, nullptr, nullptr, nullptr);
     }
     auto worker = [&](int t) {

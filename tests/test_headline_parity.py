@@ -422,3 +422,70 @@ def test_exchange_needs_an_observation_buffer():
                                                SEED, 1, 2, p(send[0]), p(send[1]), p(recv), st)
     assert r == -22
     B.close()
+
+
+@pytest.mark.parametrize("mp,uniform,spl", [("maps/16x16/basesWorkers16x16.xml", False, 0),
+                                            ("maps/16x16/basesWorkers16x16.xml", False, 7),
+                                            ("maps/8x8/basesWorkers8x8.xml", True, 0)])
+def test_record_exchange_one_rank(mp, uniform, spl):
+    """the compact observation exchange (mrts_rollout_*_records_dev) on a one-rank RCCL
+    communicator.  Every step's records, all-gathered and rendered back on the receiving side
+    (mrts_render_records_dev, int32 and uint8), equal the sender's own int32 observation of that step —
+    taken from a twin handle stepped one launch per step — while the records rollout runs its steps as
+    multi-step launches (spl = steps per launch, 0 = one launch); every other output equals the twin's."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n_sp = 64
+    A = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=23, with_masks=not uniform)
+    B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=23, with_masks=not uniform)
+    A.set_multi_step(False)
+    for e in (A, B):
+        e.reset()
+        if not uniform:
+            e.random_policy(SEED, 0)
+    _exchange_env(B)
+    words = B.set_records(64, spl)
+    S = n_sp
+    k = 0
+    for n in (1, 40, 25):
+        want = []
+        for j in range(n):
+            if uniform:
+                A.rollout_uniform(SEED, k + j, 1)
+            else:
+                A.rollout_fused(SEED, k + j + 1, 1)
+            A.synchronize()
+            want.append(A.obs.clone())
+        recv = B.records_buffer(n)
+        off = B.rollout_uniform_records(SEED, k, n, recv) if uniform else B.rollout_fused_records(SEED, k + 1, n, recv)
+        k += n
+        B.synchronize()
+        assert off.shape == (n, 2) and (off[:, 1] % ((S // 2) * words) == 0).all()
+        for j in range(n):
+            got = torch.zeros_like(B.obs)
+            B.render_records(recv, off[j, 0], off[j, 1], 1, got)
+            g8 = torch.zeros(tuple(B.obs.shape), dtype=torch.uint8, device=B.device)
+            B.render_records(recv, off[j, 0], off[j, 1], 1, g8)
+            B.synchronize()
+            assert torch.equal(got, want[j]), f"step {k - n + j}: rendered int32 observation"
+            assert torch.equal(g8.to(torch.int32), want[j]), f"step {k - n + j}: rendered uint8 observation"
+        for name in ("obs", "reward", "done", "actions") + (() if uniform else ("masks",)):
+            assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
+        for s in range(0, n_sp, 2):
+            assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
+    for e in (A, B):
+        assert not e.error_flags().any()
+    # a record too small for the games' unit lists is an error, not a silent truncation
+    assert B.set_records(2, 0) == 3
+    recv = B.records_buffer(2)
+    if uniform:
+        B.rollout_uniform_records(SEED, k, 2, recv)
+    else:
+        B.rollout_fused_records(SEED, k + 1, 2, recv)
+    B.synchronize()
+    assert (B.error_flags() & (1 << 6)).any(), "MRTS_ERR_RECORD"
+    P = DeviceVecEnv(8, 0, 300, ["maps/BWDistantResources32x32.xml"] * 8, seed=1, partial_obs=True, max_units=256)
+    assert P._h.L.mrts_set_records(P._h.h, 64, 0) != 0  # partially observable: refused
+    for e in (A, B, P):
+        e.close()

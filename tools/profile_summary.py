@@ -84,9 +84,13 @@ def main():
     launch_us = dur(r) / 1e3
     singles = [dur(x) / 1e3 for x in k_env_launches(trace)[-K:]]
     out = {"tag": a.tag, "config": cfg, "workload": bench["config"]["workload"], "mask_mode": bench["config"]["mask_mode"],
-           "envs_per_gpu": games, "steps_per_launch": K, "kernel": "k_env<MODE_STEP> multi-step",
+           "envs_per_gpu": games, "utt": bench["config"].get("utt"), "steps_per_launch": K,
+           "kernel": "k_env<MODE_STEP> multi-step",
            "trace_launch_us": launch_us, "trace_us_per_step": launch_us / K, "bench_event_us_per_step": bench["step_kernel_ms"] * 1e3,
-           "single_step_launch_us": statistics.mean(singles)}
+           "single_step_launch_us": statistics.mean(singles),
+           # the library the counters were taken with (tools/profile_config.sh); bench.py refuses a mismatch
+           "libmrts_sha256": open(os.path.join(a.src, "libmrts.sha256")).read().strip()
+           if os.path.exists(os.path.join(a.src, "libmrts.sha256")) else None}
     lines = [f"# Profile {a.tag} — {cfg}", "", "bench.py line (profiled flags):", "", "```json", json.dumps(bench, indent=1), "```", "",
              "## rocprofv3 --kernel-trace --stats (every launch of the command)", "", "```",
              open(os.path.join(a.src, "stats", "run_kernel_stats.csv")).read().strip(), "```", "",
