@@ -413,6 +413,18 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     e1.record(cur)
     torch.cuda.synchronize(env.device)
     render_ms = e0.elapsed_time(e1) / n_r
+    # the render of an 8-rank step on this one GPU (every "rank" reads this rank's records: rank stride 0) —
+    # what each rank of c4 writes per step if it materialises every rank's observations
+    out8r = torch.zeros((8 * S,) + tuple(env.obs.shape[1:]), dtype=torch.uint8, device=env.device)
+    o0, _ = off[0]
+    env.render_records(rx.recv, int(o0), 0, 8, out8r)
+    e0.record(cur)
+    for j in range(n_r):
+        env.render_records(rx.recv, int(off[j][0]), 0, 8, out8r)
+    e1.record(cur)
+    torch.cuda.synchronize(env.device)
+    render8_ms = e0.elapsed_time(e1) / n_r
+    del out8r
     rec_bytes = (S // 2) * rx.words * 4
     return {
         "value": total_games * a.steps / t,
@@ -423,6 +435,8 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
         "payload_bytes_per_rank_per_step": rec_bytes,
         "observation_bytes_per_rank_per_step": {"uint8": env.obs.numel(), "int32": 4 * env.obs.numel()},
         "render_ms_per_step": render_ms,
+        "render_ms_per_step_8_ranks": render8_ms,
+        "render_GBps_8_ranks": 8 * env.obs.numel() / (render8_ms * 1e-3) / 1e9,
         "render": f"mrts_render_records_dev: all {world} ranks' observations of one step rebuilt as uint8 "
                   f"[{world * S}, {env.dims[3]}, {env.dims[1]}, {env.dims[2]}] (not in value: a consumer may read the "
                   "records directly)",

@@ -12,7 +12,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG/$CFG
 mkdir -p "$OUT"
-BARGS="--config $CFG --steps 100 --warmup 10 --burnin 1000 --no-cpu-baseline --no-compare --no-gather-window $*"
+BARGS="--config $CFG --steps 100 --warmup 10 --burnin 1000 --no-cpu-baseline --no-compare --no-gather-window --no-full-contract $*"
 SQ="SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 # the counters describe THIS library: bench.py ignores a pmc_<cfg>.json whose hash differs
 sha256sum microrts_amd/libmrts.so | cut -d' ' -f1 > "$OUT/libmrts.sha256"
