@@ -424,21 +424,24 @@ def test_exchange_needs_an_observation_buffer():
     B.close()
 
 
-@pytest.mark.parametrize("mp,uniform,spl", [("maps/16x16/basesWorkers16x16.xml", False, 0),
-                                            ("maps/16x16/basesWorkers16x16.xml", False, 7),
-                                            ("maps/8x8/basesWorkers8x8.xml", True, 0)])
-def test_record_exchange_one_rank(mp, uniform, spl):
+@pytest.mark.parametrize("mp,uniform,spl,max_steps", [("maps/16x16/basesWorkers16x16.xml", False, 0, 300),
+                                                      ("maps/16x16/basesWorkers16x16.xml", False, 7, 300),
+                                                      ("maps/16x16/basesWorkers16x16.xml", False, 0, 13),
+                                                      ("maps/8x8/basesWorkers8x8.xml", True, 0, 300),
+                                                      ("maps/8x8/basesWorkers8x8.xml", True, 0, 11)])
+def test_record_exchange_one_rank(mp, uniform, spl, max_steps):
     """the compact observation exchange (mrts_rollout_*_records_dev) on a one-rank RCCL
     communicator.  Every step's records, all-gathered and rendered back on the receiving side
     (mrts_render_records_dev, int32 and uint8), equal the sender's own int32 observation of that step —
     taken from a twin handle stepped one launch per step — while the records rollout runs its steps as
-    multi-step launches (spl = steps per launch, 0 = one launch); every other output equals the twin's."""
+    multi-step launches (spl = steps per launch, 0 = one launch); every other output equals the twin's.
+    A small max_steps puts auto-resets inside the launches (the record then holds the reset state)."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
 
     n_sp = 64
-    A = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=23, with_masks=not uniform)
-    B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=23, with_masks=not uniform)
+    A = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform)
+    B = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform)
     A.set_multi_step(False)
     for e in (A, B):
         e.reset()
