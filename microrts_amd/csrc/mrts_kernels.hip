@@ -441,9 +441,28 @@ DEV void unpackFwd(uint32_t w, int32_t a[7]) {
     a[6] = (int32_t)((w >> 19) & 127u) - 1;
 }
 
+// The kernel's KDyn argument as a pointer into the constant (kernarg) address space.  The multi-step
+// loop makes it opaque once per iteration (freshLane), so the compiler re-reads a field with a scalar
+// load (SMEM) where the step uses it, instead of loading every field at kernel entry and keeping it
+// live across the loop: that spilled ~240 SGPRs into VGPR lanes, and every reload was a v_readlane —
+// a VALU instruction in a VALU-issue-bound kernel (MRTS_DYN_LAUNDER = 0: the old form).
+#ifndef MRTS_DYN_LAUNDER
+#define MRTS_DYN_LAUNDER 1
+#endif
+typedef const __attribute__((address_space(4))) KDyn* KDynPtr;
+// k_env's KDyn argument: its third kernel argument, after the two pointers, at byte 16 of the kernarg
+// segment.  The offset is laundered (not the address: an address escaping into asm makes the compiler
+// copy the whole argument to scratch memory first).
+static_assert(alignof(KDyn) <= 8, "k_env(int32_t*, const KStatic*, KDyn): KDyn at kernarg byte 16");
+DEV KDynPtr kdynArg(bool launder) {
+    int z = 0;
+    if (launder) asm volatile("" : "+s"(z));
+    return (KDynPtr)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() + 16 + z);
+}
 struct Game {
+#define D (*Dp)
     const KStatic& P;
-    const KDyn& D;  // the kernel argument itself (kernarg memory): fields load on demand
+    KDynPtr Dp;  // the kernel argument itself (kernarg memory): fields load on demand
     const DevUtt& U;
     int g, H, W, HW, CAP;
     int K, NT, R;  // mask slots per cell, unit types, attack window (2 * max range + 1): table values or constants
@@ -505,6 +524,10 @@ struct Game {
     }
     DEV void freshLane() {
         if (iter) asm volatile("" : "=v"(lidv) : "0"((int)threadIdx.x));
+        // multi-step kernels: the kernel argument's address made opaque again each step, so the fields
+        // and addresses derived from it are re-read (SMEM) in the phase that uses them rather than held
+        // across the step in spilled SGPRs (each reload a v_readlane)
+        if (iter && MRTS_DYN_LAUNDER) Dp = kdynArg(true);
     }
     // the helper wave of a HELP launch (threads 64..127) runs Game methods as lanes 0..63
     DEV void helperLane() { asm volatile("" : "=v"(lidv) : "0"((int)threadIdx.x - 64)); }
@@ -537,9 +560,9 @@ struct Game {
 
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
     // array offset then folds to an immediate), else the kernel arguments
-    DEV Game(const KStatic& p, const KDyn& d, int32_t* stb, int stw, uint8_t* smem, int h, int w, int hw, int cap, bool partial,
+    DEV Game(const KStatic& p, const KDyn& d /* k_env's argument D; other fields read through kdynArg */, int32_t* stb, int stw, uint8_t* smem, int h, int w, int hw, int cap, bool partial,
              int k, int nt, int r, bool iterating = false, int game = -1)
-        : P(p), D(d), U(*(const DevUtt*)smem), g(game >= 0 ? game : (int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
+        : P(p), Dp(kdynArg(false)), U(*(const DevUtt*)smem), g(game >= 0 ? game : (int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
           po(partial), iter(iterating), stBase(stb), stWords(stw) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
@@ -4343,6 +4366,7 @@ struct Game {
         }
         wsync();
     }
+#undef D
 };
 
 // PassiveAI.getAction = fillWithNones(gs, p, 10) (ai/PassiveAI.java:41-45): nothing to park, the
