@@ -402,7 +402,8 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
     # the receiving side: every rank's observations of one step back as uint8 planes
     S = env.dims[0]
-    out8 = torch.zeros((world * S,) + tuple(env.obs.shape[1:]), dtype=torch.uint8, device=env.device)
+    b8 = torch.int8 if a.po else torch.uint8  # partially observable: a dead unit in a view can show hp <= 0
+    out8 = torch.zeros((world * S,) + tuple(env.obs.shape[1:]), dtype=b8, device=env.device)
     n_r = min(5, a.steps)
     e0, e1 = _FenceFreeEvent(), _FenceFreeEvent()
     cur = torch.cuda.current_stream(env.device)
@@ -415,7 +416,7 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     render_ms = e0.elapsed_time(e1) / n_r
     # the render of an 8-rank step on this one GPU (every "rank" reads this rank's records: rank stride 0) —
     # what each rank of c4 writes per step if it materialises every rank's observations
-    out8r = torch.zeros((8 * S,) + tuple(env.obs.shape[1:]), dtype=torch.uint8, device=env.device)
+    out8r = torch.zeros((8 * S,) + tuple(env.obs.shape[1:]), dtype=b8, device=env.device)
     o0, _ = off[0]
     env.render_records(rx.recv, int(o0), 0, 8, out8r)
     e0.record(cur)
@@ -430,14 +431,17 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
         "value": total_games * a.steps / t,
         "ms_per_step": 1e3 * t / a.steps,
         "collective": "in-place RCCL all-gather (ring over xGMI) of each launch's compact game records: per game and step "
-                      f"{rx.words} words = live units (<= 64) x (cell, hp, resources, type, owner, action), the inputs of "
-                      "GameState.getVectorObservation; on the handle's own stream, overlapping the next launch",
+                      + (f"{rx.words} words = the units of either view (<= 64) x 2 words (cell, hp, resources, type, owner, "
+                         "snapshot membership and seen action per view), the inputs of "
+                         "PartiallyObservableGameState.getVectorObservation" if a.po else
+                         f"{rx.words} words = live units (<= 64) x (cell, hp, resources, type, owner, action), the inputs of "
+                         "GameState.getVectorObservation") + "; on the handle's own stream, overlapping the next launch",
         "payload_bytes_per_rank_per_step": rec_bytes,
         "observation_bytes_per_rank_per_step": {"uint8": env.obs.numel(), "int32": 4 * env.obs.numel()},
         "render_ms_per_step": render_ms,
         "render_ms_per_step_8_ranks": render8_ms,
         "render_GBps_8_ranks": 8 * env.obs.numel() / (render8_ms * 1e-3) / 1e9,
-        "render": f"mrts_render_records_dev: all {world} ranks' observations of one step rebuilt as uint8 "
+        "render": f"mrts_render_records_dev: all {world} ranks' observations of one step rebuilt as {'int8' if a.po else 'uint8'} "
                   f"[{world * S}, {env.dims[3]}, {env.dims[1]}, {env.dims[2]}] (not in value: a consumer may read the "
                   "records directly)",
         "steps_per_launch": a.records_steps or "all",
@@ -1044,7 +1048,7 @@ def main():
                 sys.stderr.flush()
                 os._exit(0)
 
-            records_ok = (a.gather_window == "records" and dist.get_backend() != "gloo" and not a.po and native
+            records_ok = (a.gather_window == "records" and dist.get_backend() != "gloo" and native
                           and (mode["fused"] or mode["uni_fused"]))
             try:
                 if records_ok:

@@ -213,21 +213,28 @@ int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const i
  * terrain, so the exchange all-gathers that: one record per game and step = 1 + units_per_record
  * 32-bit words (live units in list order; layout in microrts_amd/csrc/mrts_internal.h recWords), and
  * the receiver rebuilds any rank's observations with mrts_render_records_dev.  c3: ~0.26 KB per game
- * instead of 3 KB of uint8 planes for its two slots.
+ * instead of 3 KB of uint8 planes for its two slots.  Partially observable handles
+ * (PartiallyObservableGameState.getVectorObservation, rts/PartiallyObservableGameState.java:82-154):
+ * 1 + 2 * units_per_record words — the units of either view's snapshot with the snapshot's membership
+ * and seen action per view; the receiver paints the sight disks from the unit-type table.  c5: ~0.5 KB
+ * per game instead of 16 KB of byte planes.
  * mrts_set_records: units per record (0 = off) and steps per launch of a records rollout (0 = up to
- * MRTS_MAX_ITER); self-play handles with full observability on maps of <= 256 cells whose every
- * observation value fits a byte, else -ENOTSUP.  A game with more live units than a record holds sets
- * MRTS_ERR_RECORD.
+ * MRTS_MAX_ITER); self-play handles on maps whose cell count is a multiple of 4 — full observability:
+ * <= 256 cells, every observation value fits a byte; partial observability: <= 15 unit types — else
+ * -ENOTSUP.  A game with more units than a record holds (or, partially observable, an hp outside int8 /
+ * resources outside uint8) sets MRTS_ERR_RECORD.
+ * mrts_record_words: 32-bit words per game record as set (0 = records off).
  * mrts_rollout_{fused,uniform}_records_dev: mrts_rollout_{fused,uniform}_dev's steps (multi-step
  * launches where possible), each launch's records written at this rank's place of its chunk of d_recv
  * and all-gathered in place on the handle's RCCL communicator (mrts_exchange_init) while the next launch
  * runs; all collectives are complete when `stream` reaches the end of the call.  d_recv (16-byte aligned)
- * holds n_steps * nranks * n_games * (1 + units_per_record) words; step_offsets (may be NULL) receives,
+ * holds n_steps * nranks * n_games * mrts_record_words words; step_offsets (may be NULL) receives,
  * per step, int64 [2]: the word offset in d_recv of rank 0's records of that step and the stride between
  * consecutive ranks' records of it.
  * mrts_render_records_dev: records of n_ranks x n_games games (rank r's game g at d_rec + r * rank_stride
- * + g * (1 + units_per_record) words; the terrain of game g from this handle's map of game g) into
- * d_out [n_ranks][2 * n_games][C][H][W] as uint8 (out_bytes 1) or int32 (out_bytes 4, 16-byte aligned). */
+ * + g * mrts_record_words words; the terrain of game g from this handle's map of game g) into
+ * d_out [n_ranks][2 * n_games][C][H][W] as uint8 (out_bytes 1; int8 for partially observable handles,
+ * whose dead units' hp may be negative) or int32 (out_bytes 4, 16-byte aligned). */
 int mrts_set_records(mrts_env* env, int32_t units_per_record, int32_t steps_per_launch);
 int mrts_rollout_fused_records_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
                                    double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed,
@@ -236,6 +243,7 @@ int mrts_rollout_fused_records_dev(mrts_env* env, int32_t* d_actions, const int3
 int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
                                      double* d_reward, uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps,
                                      uint32_t* d_recv, int64_t* step_offsets, void* stream);
+int32_t mrts_record_words(const mrts_env* env);
 int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,
                             int32_t out_bytes, void* stream);
 /* Graph form of a handle's calls (no Java counterpart): everything this handle enqueues on `stream`

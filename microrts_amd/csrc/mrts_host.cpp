@@ -938,7 +938,7 @@ struct RecPlan {
 void planRecords(const mrts_env* env, KDyn& D, const RecPlan* rec) {
     if (!rec) return;
     D.rec_units = env->recUnits;
-    D.rec_out = rec->chunk + (size_t)rec->rank * D.n_iter * env->nGames * recWords(env->recUnits);
+    D.rec_out = rec->chunk + (size_t)rec->rank * D.n_iter * env->nGames * recWords(env->recUnits, env->partialObs);
 }
 // n_iter consecutive fused steps (next_step, next_step + 1, ...) as ONE launch when the handle runs a
 // specialised full-observability self-play kernel and is in the steady fused state (the previous
@@ -1302,10 +1302,11 @@ void recordsLoop(mrts_env* env, int32_t n_steps, uint32_t* d_recv, int64_t* offs
     if (!env->exComm) throw Fail{-EINVAL, "mrts_exchange_init first"};
     if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
     if (!d_recv || ((uintptr_t)d_recv & 15)) throw Fail{-EINVAL, "the receive buffer must be non-null and 16-byte aligned"};
-    if (!env->obsImg) throw Fail{-ENOTSUP, "records: an observation value no longer fits a byte"};
+    // (partially observable records carry hp as int8: the kernel flags a value outside the record's range)
+    if (!env->obsImg && !env->partialObs) throw Fail{-ENOTSUP, "records: an observation value no longer fits a byte"};
     HIPCHK(hipSetDevice(env->device));
     hipStream_t s = pickStream(env, stream);
-    const size_t per = (size_t)env->nGames * recWords(env->recUnits);  // words per rank and step
+    const size_t per = (size_t)env->nGames * recWords(env->recUnits, env->partialObs);  // words per rank and step
     size_t base = 0;                                                   // words of d_recv filled so far
     bool any = false;
     for (int32_t k = 0; k < n_steps;) {
@@ -1343,9 +1344,15 @@ int mrts_set_records(mrts_env* env, int32_t units_per_record, int32_t steps_per_
     }
     if (units_per_record < 1 || units_per_record > 0xFFFF || steps_per_launch < 0)
         return fail(Fail{-EINVAL, "units per record 1..65535, steps per launch >= 0"});
-    if (env->partialObs || env->HW > 256 || (env->HW & 3) || env->utt.ntypes > 7 || !env->obsImg || env->nSpGames != env->nGames)
-        return fail(Fail{-ENOTSUP, "records: self-play handles, full observability, maps of <= 256 cells (a multiple of 4), "
-                                   "<= 7 unit types, every observation value < 256"});
+    if (env->nSpGames != env->nGames || (env->HW & 3))
+        return fail(Fail{-ENOTSUP, "records: self-play handles, maps whose cell count is a multiple of 4"});
+    if (!env->partialObs && (env->HW > 256 || env->utt.ntypes > 7 || !env->obsImg))
+        return fail(Fail{-ENOTSUP, "records (full observability): maps of <= 256 cells, <= 7 unit types, every observation "
+                                   "value < 256"});
+    if (env->partialObs && (env->HW > 65536 || env->utt.ntypes > 15 || env->hstatic.C != 8 ||
+                            4 * (size_t)(2 * env->HW + 4 * env->H * ((env->W + 31) / 32)) > 64 * 1024))
+        return fail(Fail{-ENOTSUP, "records (partial observability): <= 15 unit types, the receiver's render state in 64 KB "
+                                   "of LDS (maps of <= ~7,900 cells)"});
     env->recUnits = units_per_record;
     env->recSteps = steps_per_launch;
     return 0;
@@ -1384,6 +1391,11 @@ int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const in
     } catch (const Fail& f) {
         return fail(f);
     }
+}
+
+int32_t mrts_record_words(const mrts_env* env) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    return env->recUnits ? recWords(env->recUnits, env->partialObs) : 0;
 }
 
 int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,

@@ -187,15 +187,21 @@ struct KDyn {
     int32_t* trace_out;
     int32_t trace_generic;
     // compact observation records (mrts_rollout_*_records_dev): after each step's observation write, game
-    // g of iteration it writes its record at rec_out + (it * n_sp_games + g) * (1 + rec_units) words
-    // (recWord in mrts_kernels.hip); null = off
+    // g of iteration it writes its record at rec_out + (it * n_sp_games + g) * recWords(rec_units, po)
+    // words (writeRecord in mrts_kernels.hip); null = off
     uint32_t* rec_out;
     int32_t rec_units;
 };
-// compact observation record of one game (full observability, maps of <= 256 cells, every plane value
-// < 256): word 0 = live units n (<= rec_units) | overflow << 31, then one word per live unit in list
-// order: cell | hp << 8 | resources << 16 | (type + 1) << 24 | (player + 1) << 27 | action type << 29
-constexpr int recWords(int units) { return 1 + units; }
+// compact observation record of one game, word 0 = units n (<= rec_units) | overflow << 31, then per unit
+// in list order:
+// * full observability (maps of <= 256 cells, every plane value < 256), the live units, one word each:
+//   cell | hp << 8 | resources << 16 | (type + 1) << 24 | (player + 1) << 27 | action type << 29;
+// * partial observability, the units either player's view holds (dead ones included: a view keeps the
+//   units of its snapshot), two words each: cell | (hp as int8) << 16 | resources << 24, and
+//   (type + 1) | (player + 1) << 4 | snapshot byte << 8 (bit p: in view p; bits 2+3p..4+3p: the action
+//   type + 1 view p saw, 0 = none) — hp of a dead unit may be negative, a value outside int8 / uint8
+//   sets the overflow bit
+constexpr int recWords(int units, bool po) { return 1 + (po ? 2 : 1) * units; }
 constexpr int BAL_COST = 16;
 constexpr int PRIO_KEYS = 8 * 8 * 2 * 16 * 4;  // XCC x SE x SH x CU x SIMD (HW_ID / XCC_ID fields)
 // PO render record per game (int32 words): [0] views rendered by the last observation write (bit p);

@@ -459,6 +459,33 @@ DEV KDynPtr kdynArg(bool launder) {
     if (launder) asm volatile("" : "+s"(z));
     return (KDynPtr)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() + 16 + z);
 }
+// One sight disk (dx^2 + dy^2 <= sr^2) ORed into per-row bitmaps of a W-wide map ((W + 31) / 32 words a
+// row): one atomicOr per covered row word.  dlo / dhi: the unit-type table's half-widths for sr <= 15
+// (host-computed, DevUtt::diskLo/Hi); a larger sight takes the integer square root per row.
+DEV void paintDiskRows(uint32_t* rows, int H, int W, int x, int y, int sr, uint32_t dlo, uint32_t dhi) {
+    const int WPR = (W + 31) >> 5;
+    for (int dy = -sr; dy <= sr; dy++) {
+        const int yy = y + dy;
+        if (yy < 0 || yy >= H) continue;
+        const int ady = dy < 0 ? -dy : dy;
+        int w;
+        if (sr <= 15) {
+            w = (int)(((ady < 8 ? dlo : dhi) >> (4 * (ady & 7))) & 0xFu);
+        } else {
+            const int lim = sr * sr - dy * dy;
+            w = (int)__builtin_sqrtf((float)lim);
+            while (w * w > lim) w--;
+            while ((w + 1) * (w + 1) <= lim) w++;
+        }
+        const int x0 = max(0, x - w), x1 = min(W - 1, x + w);
+        for (int k = x0 >> 5; k <= (x1 >> 5); k++) {
+            const int lo = max(x0, 32 * k) - 32 * k, hi = min(x1, 32 * k + 31) - 32 * k;
+            const uint32_t b = (hi - lo == 31) ? 0xFFFFFFFFu : (((1u << (hi - lo + 1)) - 1u) << lo);
+            atomicOr(&rows[yy * WPR + k], b);
+        }
+    }
+}
+
 struct Game {
 #define D (*Dp)
     const KStatic& P;
@@ -2010,29 +2037,8 @@ struct Game {
     // Sight disks (dx^2 + dy^2 <= sightRadius^2 of the seeing unit's type) painted into per-row bitmaps:
     // lane = seeing unit, one atomicOr per covered row word; a cell is seen iff its bit is set.
     DEV void paintDisk(uint32_t* rows, uint32_t u) const {
-        const int WPR = (W + 31) >> 5;
-        const int t = utyp(u), sr = U.sight[t], x = ux(u), y = uy(u);
-        const uint32_t dlo = U.diskLo[t], dhi = U.diskHi[t];
-        for (int dy = -sr; dy <= sr; dy++) {
-            const int yy = y + dy;
-            if (yy < 0 || yy >= H) continue;
-            const int ady = dy < 0 ? -dy : dy;
-            int w;
-            if (sr <= 15) {  // the table's half-width (host-computed, DevUtt::diskLo/Hi)
-                w = (int)(((ady < 8 ? dlo : dhi) >> (4 * (ady & 7))) & 0xFu);
-            } else {
-                const int lim = sr * sr - dy * dy;
-                w = (int)__builtin_sqrtf((float)lim);
-                while (w * w > lim) w--;
-                while ((w + 1) * (w + 1) <= lim) w++;
-            }
-            const int x0 = max(0, x - w), x1 = min(W - 1, x + w);
-            for (int k = x0 >> 5; k <= (x1 >> 5); k++) {
-                const int lo = max(x0, 32 * k) - 32 * k, hi = min(x1, 32 * k + 31) - 32 * k;
-                const uint32_t b = (hi - lo == 31) ? 0xFFFFFFFFu : (((1u << (hi - lo + 1)) - 1u) << lo);
-                atomicOr(&rows[yy * WPR + k], b);
-            }
-        }
+        const int t = utyp(u);
+        paintDiskRows(rows, H, W, ux(u), uy(u), U.sight[t], U.diskLo[t], U.diskHi[t]);
     }
     // paintDisk for every lane with `act` at once, maps with W <= 32 (one row word) and sight <= 15:
     // a uniform loop over dy up to the table's largest sight, one predicated atomicOr per row
@@ -2820,9 +2826,37 @@ struct Game {
     // ((owner + p) % 2) + 1), so one record per game replaces 2 x 6 x HW observation values on the
     // wire of the exchange (k_render_records rebuilds them).  More live units than the record holds
     // set E_RECORD (the exchange then reports an error).
+    // Partially observable (po): the record holds what PartiallyObservableGameState.getVectorObservation
+    // reads for both views (rts/PartiallyObservableGameState.java:82-154, as writeObsPO renders it) — every
+    // unit of either view's snapshot in list order with its live fields (a dead one stays until the
+    // compaction) and the snapshot byte (membership and seen action per view); walls and sight disks
+    // follow on the receiving side from the map and the unit-type table.
     DEV void writeRecord(int it) {
         const int RU = D.rec_units;
-        uint32_t* r = D.rec_out + ((size_t)it * D.n_sp_games + g) * (size_t)recWords(RU);
+        uint32_t* r = D.rec_out + ((size_t)it * D.n_sp_games + g) * (size_t)recWords(RU, po);
+        if (po) {
+            int n = 0;
+            bool bad = false;
+            for (int s0 = 0; s0 < nu; s0 += 64) {
+                const int s = s0 + lid();
+                const uint32_t sb = s < nu ? (uint32_t)snap[s] : 0u;
+                const bool inv = (sb & 3u) != 0;
+                const uint64_t m = ballot(inv);
+                const int idx = n + lanes_below(m);
+                if (inv && idx < RU) {
+                    const uint32_t cu = uc[s];
+                    const int h = hp[s], rs = res[s];
+                    bad |= h < -128 || h > 127 || rs < 0 || rs > 255;
+                    r[1 + 2 * idx] = (uint32_t)(uy(cu) * W + ux(cu)) | (((uint32_t)h & 0xFFu) << 16) | ((uint32_t)rs << 24);
+                    r[2 + 2 * idx] = (uint32_t)(utyp(cu) + 1) | ((uint32_t)(uplay(cu) + 1) << 4) | ((sb & 0xFFu) << 8);
+                }
+                n += __popcll(m);
+            }
+            const bool over = n > RU || ballot(bad) != 0;
+            if (lid() == 0) r[0] = (uint32_t)(n < RU ? n : RU) | (over ? 0x80000000u : 0u);
+            if (over) addErr(E_RECORD);
+            return;
+        }
         int n = 0;
         for (int s0 = 0; s0 < nu; s0 += 64) {
             const int s = s0 + lid();
@@ -5408,7 +5442,7 @@ __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict
     uint8_t* img = (uint8_t*)imgw;
     const KStatic& P = *PS;
     const int g = (int)blockIdx.x, r = (int)blockIdx.y, l = (int)threadIdx.x, HW = P.HW, C = P.C, G = P.n_games;
-    const uint32_t* rc = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units);
+    const uint32_t* rc = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units, false);
     for (int i = l; i < 5 * HW / 4; i += 64) imgw[i] = 0u;
     const uint32_t hdr = rc[0];
     __syncthreads();
@@ -5459,10 +5493,84 @@ __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict
         }
     }
 }
+// The same for partially observable handles (PartiallyObservableGameState.getVectorObservation,
+// rts/PartiallyObservableGameState.java:82-154, as Game::writeObsPO renders it): per view p, the last
+// unit of p's snapshot on each cell (list order) gives planes 0-4 — its live hp, resources, owner
+// relative to p, type, and the action type p's snapshot saw — plane 5 the map's walls, planes 6 / 7
+// whether a sight disk of one of the view's units owned by p / by the other player covers the cell.
+// out = [n_ranks][2 * n_games][8][HW] as int8 (out_bytes 1: a dead unit's hp can be negative) or int32.
+// One block of 256 threads per game and rank; LDS: the per-view cell owners (2 x HW words) and sight
+// rows (2 views x 2 x H x (W + 31) / 32 words).  HW % 4 == 0 (the host checks).
+__global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __restrict__ PS, const uint32_t* __restrict__ rec,
+                                                           int units, int64_t rank_stride, void* __restrict__ out, int out_bytes) {
+    extern __shared__ __align__(16) uint32_t lds[];
+    const KStatic& P = *PS;
+    const int g = (int)blockIdx.x, r = (int)blockIdx.y, t = (int)threadIdx.x;
+    const int H = P.H, W = P.W, HW = P.HW, C = P.C, G = P.n_games, NR = H * ((W + 31) >> 5);
+    uint32_t* const sc = lds;             // [view][cell]: index + 1 of the view's last unit on the cell, 0 = none
+    uint32_t* const rows = lds + 2 * HW;  // [view][own, other][NR]
+    const uint32_t* rc = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units, true);
+    for (int i = t; i < 2 * HW + 4 * NR; i += 256) lds[i] = 0u;
+    const int n = (int)(rc[0] & 0xFFFFu);
+    __syncthreads();
+    for (int i = t; i < n; i += 256) {
+        const uint32_t w0 = rc[1 + 2 * i], w1 = rc[2 + 2 * i];
+        const int c = (int)(w0 & 0xFFFFu), ty = (int)(w1 & 15u) - 1, pl = (int)((w1 >> 4) & 3u) - 1;
+        const uint32_t sb = (w1 >> 8) & 0xFFu;
+        const int x = c % W, y = c / W;
+        for (int p = 0; p < 2; p++) {
+            if (!((sb >> p) & 1u)) continue;
+            atomicMax(&sc[p * HW + c], (uint32_t)(i + 1));
+            if (pl >= 0)
+                paintDiskRows(rows + (2 * p + (pl == p ? 0 : 1)) * NR, H, W, x, y, P.utt.sight[ty], P.utt.diskLo[ty],
+                              P.utt.diskHi[ty]);
+        }
+    }
+    __syncthreads();
+    const uint32_t* terr = (const uint32_t*)(P.tmpl + P.tmpl_off[g] + T_TERR);
+    const int WPR = (W + 31) >> 5;
+    for (int c4 = 4 * t; c4 < HW; c4 += 4 * 256) {
+        const uint32_t tw = terr[c4 >> 2];  // walls: non-zero terrain bytes
+        for (int p = 0; p < 2; p++) {
+            int v[8][4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int c = c4 + j, x = c % W, y = c / W;
+                const uint32_t s = sc[p * HW + c];
+                const uint32_t w0 = s ? rc[2 * s - 1] : 0u, w1 = s ? rc[2 * s] : 0u;
+                const int pl = (int)((w1 >> 4) & 3u) - 1, ca = (int)((w1 >> (10 + 3 * p)) & 7u);
+                v[0][j] = s ? (int)(int8_t)(uint8_t)(w0 >> 16) : 0;
+                v[1][j] = s ? (int)(w0 >> 24) : 0;
+                v[2][j] = (s && pl >= 0) ? ((pl + p) % 2) + 1 : 0;
+                v[3][j] = s ? (int)(w1 & 15u) : 0;
+                v[4][j] = (s && ca) ? ca - 1 : 0;
+                v[5][j] = ((tw >> (8 * j)) & 0xFFu) ? 1 : 0;
+                v[6][j] = (int)((rows[(2 * p) * NR + y * WPR + (x >> 5)] >> (x & 31)) & 1u);
+                v[7][j] = (int)((rows[(2 * p + 1) * NR + y * WPR + (x >> 5)] >> (x & 31)) & 1u);
+            }
+            const size_t slot = (size_t)r * 2 * G + 2 * (size_t)g + p;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const size_t off = (slot * C + q) * (size_t)HW + c4;
+                if (out_bytes == 1)
+                    *(uint32_t*)((uint8_t*)out + off) = (uint32_t)(v[q][0] & 0xFF) | ((uint32_t)(v[q][1] & 0xFF) << 8) |
+                                                         ((uint32_t)(v[q][2] & 0xFF) << 16) | ((uint32_t)(v[q][3] & 0xFF) << 24);
+                else
+                    st4<true>((int32_t*)out + off, v[q][0], v[q][1], v[q][2], v[q][3]);
+            }
+        }
+    }
+}
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
                                int64_t rank_stride, void* out, int out_bytes, hipStream_t stream) {
-    hipLaunchKernelGGL(k_render_records, dim3((unsigned)hs.n_games, (unsigned)n_ranks), dim3(64), 0, stream, ds, rec, units,
-                       rank_stride, out, out_bytes);
+    if (hs.partial_obs) {
+        const size_t lds = 4 * (size_t)(2 * hs.HW + 4 * hs.H * ((hs.W + 31) / 32));
+        hipLaunchKernelGGL(k_render_records_po, dim3((unsigned)hs.n_games, (unsigned)n_ranks), dim3(256), lds, stream, ds, rec,
+                           units, rank_stride, out, out_bytes);
+    } else {
+        hipLaunchKernelGGL(k_render_records, dim3((unsigned)hs.n_games, (unsigned)n_ranks), dim3(64), 0, stream, ds, rec, units,
+                           rank_stride, out, out_bytes);
+    }
     return hipGetLastError();
 }
 

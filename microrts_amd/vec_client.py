@@ -572,11 +572,12 @@ class DeviceVecEnv:
         steps per launch of a records rollout (0 = as many as a launch runs).  Returns words per record."""
         _lib.check(self._h.L.mrts_set_records(self._h.h, int(units_per_record), int(steps_per_launch)))
         self.record_units = int(units_per_record)
-        return 1 + self.record_units
+        self.record_words = int(self._h.L.mrts_record_words(self._h.h))
+        return self.record_words
 
     def records_buffer(self, n_steps, world=1):
         """A receive buffer for n_steps of a records rollout over `world` ranks (uint32 words)."""
-        return self.torch.zeros(n_steps * world * (self._h.S // 2) * (1 + self.record_units), dtype=self.torch.int32,
+        return self.torch.zeros(n_steps * world * (self._h.S // 2) * self.record_words, dtype=self.torch.int32,
                                 device=self.device)
 
     def rollout_fused_records(self, seed, first_next_step, n_steps, recv, stream=None):
@@ -609,7 +610,8 @@ class DeviceVecEnv:
 
     def render_records(self, recv, offset, rank_stride, n_ranks, out, stream=None):
         """The observations of n_ranks x games records (rank r's at recv[offset + r * rank_stride:]) into
-        out [n_ranks * slots, C, H, W] (uint8 or int32) — mrts_render_records_dev."""
+        out [n_ranks * slots, C, H, W] (uint8 or int32; int8 or int32 for a partially observable handle) —
+        mrts_render_records_dev."""
         h = self._h
         ob = out.element_size()
         assert ob in (1, 4) and out.is_contiguous() and out.numel() == n_ranks * self.obs.numel()

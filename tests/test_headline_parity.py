@@ -424,24 +424,34 @@ def test_exchange_needs_an_observation_buffer():
     B.close()
 
 
-@pytest.mark.parametrize("mp,uniform,spl,max_steps", [("maps/16x16/basesWorkers16x16.xml", False, 0, 300),
-                                                      ("maps/16x16/basesWorkers16x16.xml", False, 7, 300),
-                                                      ("maps/16x16/basesWorkers16x16.xml", False, 0, 13),
-                                                      ("maps/8x8/basesWorkers8x8.xml", True, 0, 300),
-                                                      ("maps/8x8/basesWorkers8x8.xml", True, 0, 11)])
-def test_record_exchange_one_rank(mp, uniform, spl, max_steps):
-    """the compact observation exchange (mrts_rollout_*_records_dev) on a one-rank RCCL
-    communicator.  Every step's records, all-gathered and rendered back on the receiving side
-    (mrts_render_records_dev, int32 and uint8), equal the sender's own int32 observation of that step —
-    taken from a twin handle stepped one launch per step — while the records rollout runs its steps as
-    multi-step launches (spl = steps per launch, 0 = one launch); every other output equals the twin's.
-    A small max_steps puts auto-resets inside the launches (the record then holds the reset state)."""
+@pytest.mark.parametrize("mp,uniform,spl,max_steps,po", [("maps/16x16/basesWorkers16x16.xml", False, 0, 300, False),
+                                                         ("maps/16x16/basesWorkers16x16.xml", False, 7, 300, False),
+                                                         ("maps/16x16/basesWorkers16x16.xml", False, 0, 13, False),
+                                                         ("maps/8x8/basesWorkers8x8.xml", True, 0, 300, False),
+                                                         ("maps/8x8/basesWorkers8x8.xml", True, 0, 11, False),
+                                                         ("maps/BWDistantResources32x32.xml", False, 0, 300, True),
+                                                         ("maps/BWDistantResources32x32.xml", False, 9, 17, True),
+                                                         ("maps/16x16/basesWorkers16x16.xml", False, 0, 300, True),
+                                                         ("maps/8x8/basesWorkers8x8.xml", True, 0, 300, True),
+                                                         ("maps/8x8/basesWorkers8x8.xml", False, 0, 400, "dead")])
+def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
+    """the compact observation exchange (mrts_rollout_*_records_dev) on a one-rank
+    RCCL communicator.  Every step's records, all-gathered and rendered back on the receiving side
+    (mrts_render_records_dev, int32 and uint8 / int8), equal the sender's own int32 observation of that
+    step — taken from a twin handle stepped one launch per step — while the records rollout runs its steps
+    as multi-step launches (spl = steps per launch, 0 = one launch); every other output equals the twin's.
+    A small max_steps puts auto-resets inside the launches (the record then holds the reset state).
+    po: partially observable handles (two record words per unit of either view; the receiver paints the
+    sight disks) — the 32x32 map runs c5's helper-wave kernel in the records rollout; po = "dead": 266
+    masked random steps on 8x8, long enough that a view shows units that died in the step (their hp <= 0,
+    kept by the view's snapshot until the compaction), and the test checks that one did."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
 
     n_sp = 64
-    A = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform)
-    B = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform)
+    kw = dict(partial_obs=True, max_units=256) if po else {}
+    A = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform, **kw)
+    B = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform, **kw)
     A.set_multi_step(False)
     for e in (A, B):
         e.reset()
@@ -451,7 +461,8 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps):
     words = B.set_records(64, spl)
     S = n_sp
     k = 0
-    for n in (1, 40, 25):
+    dead_seen = False
+    for n in (1, 40, 25) + ((100, 100) if po == "dead" else ()):
         want = []
         for j in range(n):
             if uniform:
@@ -460,6 +471,8 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps):
                 A.rollout_fused(SEED, k + j + 1, 1)
             A.synchronize()
             want.append(A.obs.clone())
+            if po:
+                dead_seen |= bool(((want[-1][:, 0] <= 0) & (want[-1][:, 3] > 0)).any())
         recv = B.records_buffer(n)
         off = B.rollout_uniform_records(SEED, k, n, recv) if uniform else B.rollout_fused_records(SEED, k + 1, n, recv)
         k += n
@@ -468,19 +481,21 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps):
         for j in range(n):
             got = torch.zeros_like(B.obs)
             B.render_records(recv, off[j, 0], off[j, 1], 1, got)
-            g8 = torch.zeros(tuple(B.obs.shape), dtype=torch.uint8, device=B.device)
+            g8 = torch.zeros(tuple(B.obs.shape), dtype=torch.int8 if po else torch.uint8, device=B.device)
             B.render_records(recv, off[j, 0], off[j, 1], 1, g8)
             B.synchronize()
             assert torch.equal(got, want[j]), f"step {k - n + j}: rendered int32 observation"
-            assert torch.equal(g8.to(torch.int32), want[j]), f"step {k - n + j}: rendered uint8 observation"
+            assert torch.equal(g8.to(torch.int32), want[j]), f"step {k - n + j}: rendered byte observation"
         for name in ("obs", "reward", "done", "actions") + (() if uniform else ("masks",)):
             assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
         for s in range(0, n_sp, 2):
             assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
     for e in (A, B):
         assert not e.error_flags().any()
+    if po == "dead":
+        assert dead_seen, "no view showed a unit that died in its step"
     # a record too small for the games' unit lists is an error, not a silent truncation
-    assert B.set_records(2, 0) == 3
+    assert B.set_records(2, 0) == (5 if po else 3)
     recv = B.records_buffer(2)
     if uniform:
         B.rollout_uniform_records(SEED, k, 2, recv)
@@ -488,7 +503,5 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps):
         B.rollout_fused_records(SEED, k + 1, 2, recv)
     B.synchronize()
     assert (B.error_flags() & (1 << 6)).any(), "MRTS_ERR_RECORD"
-    P = DeviceVecEnv(8, 0, 300, ["maps/BWDistantResources32x32.xml"] * 8, seed=1, partial_obs=True, max_units=256)
-    assert P._h.L.mrts_set_records(P._h.h, 64, 0) != 0  # partially observable: refused
-    for e in (A, B, P):
+    for e in (A, B):
         e.close()
