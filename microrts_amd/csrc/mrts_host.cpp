@@ -1350,9 +1350,10 @@ int mrts_set_records(mrts_env* env, int32_t units_per_record, int32_t steps_per_
         return fail(Fail{-ENOTSUP, "records (full observability): maps of <= 256 cells, <= 7 unit types, every observation "
                                    "value < 256"});
     if (env->partialObs && (env->HW > 65536 || env->utt.ntypes > 15 || env->hstatic.C != 8 ||
-                            4 * (size_t)(2 * env->HW + 4 * env->H * ((env->W + 31) / 32)) > 64 * 1024))
-        return fail(Fail{-ENOTSUP, "records (partial observability): <= 15 unit types, the receiver's render state in 64 KB "
-                                   "of LDS (maps of <= ~7,900 cells)"});
+                            4 * (size_t)(2 * env->HW + 4 * env->H * ((env->W + 31) / 32) + recWords(units_per_record, true)) >
+                                64 * 1024))
+        return fail(Fail{-ENOTSUP, "records (partial observability): <= 15 unit types, the receiver's render state and one "
+                                   "record in 64 KB of LDS"});
     env->recUnits = units_per_record;
     env->recSteps = steps_per_launch;
     return 0;

@@ -5446,7 +5446,7 @@ __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict
     for (int i = l; i < 5 * HW / 4; i += 64) imgw[i] = 0u;
     const uint32_t hdr = rc[0];
     __syncthreads();
-    const int n = (int)(hdr & 0xFFFFu);
+    const int n = min((int)(hdr & 0xFFFFu), units);
     for (int i = l; i < n; i += 64) {
         const uint32_t w = rc[1 + i];
         const int c = (int)(w & 0xFFu);
@@ -5499,8 +5499,9 @@ __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict
 // relative to p, type, and the action type p's snapshot saw — plane 5 the map's walls, planes 6 / 7
 // whether a sight disk of one of the view's units owned by p / by the other player covers the cell.
 // out = [n_ranks][2 * n_games][8][HW] as int8 (out_bytes 1: a dead unit's hp can be negative) or int32.
-// One block of 256 threads per game and rank; LDS: the per-view cell owners (2 x HW words) and sight
-// rows (2 views x 2 x H x (W + 31) / 32 words).  HW % 4 == 0 (the host checks).
+// One block of 256 threads per game and rank; LDS: the per-view cell owners (2 x HW words), sight rows
+// (2 views x 2 x H x (W + 31) / 32 words) and the record itself (the per-cell lookups stay on chip).
+// HW % 4 == 0 (the host checks).
 __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __restrict__ PS, const uint32_t* __restrict__ rec,
                                                            int units, int64_t rank_stride, void* __restrict__ out, int out_bytes) {
     extern __shared__ __align__(16) uint32_t lds[];
@@ -5509,9 +5510,11 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
     const int H = P.H, W = P.W, HW = P.HW, C = P.C, G = P.n_games, NR = H * ((W + 31) >> 5);
     uint32_t* const sc = lds;             // [view][cell]: index + 1 of the view's last unit on the cell, 0 = none
     uint32_t* const rows = lds + 2 * HW;  // [view][own, other][NR]
-    const uint32_t* rc = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units, true);
+    uint32_t* const rc = rows + 4 * NR;   // the record (1 + 2 x units words)
+    const uint32_t* rg = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units, true);
+    const int n = min((int)(rg[0] & 0xFFFFu), units);
     for (int i = t; i < 2 * HW + 4 * NR; i += 256) lds[i] = 0u;
-    const int n = (int)(rc[0] & 0xFFFFu);
+    for (int i = t; i < 1 + 2 * n; i += 256) rc[i] = rg[i];
     __syncthreads();
     for (int i = t; i < n; i += 256) {
         const uint32_t w0 = rc[1 + 2 * i], w1 = rc[2 + 2 * i];
@@ -5564,7 +5567,7 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
                                int64_t rank_stride, void* out, int out_bytes, hipStream_t stream) {
     if (hs.partial_obs) {
-        const size_t lds = 4 * (size_t)(2 * hs.HW + 4 * hs.H * ((hs.W + 31) / 32));
+        const size_t lds = 4 * (size_t)(2 * hs.HW + 4 * hs.H * ((hs.W + 31) / 32) + recWords(units, true));
         hipLaunchKernelGGL(k_render_records_po, dim3((unsigned)hs.n_games, (unsigned)n_ranks), dim3(256), lds, stream, ds, rec,
                            units, rank_stride, out, out_bytes);
     } else {
