@@ -491,7 +491,22 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
     survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * units + 2 * HW + 16))
     env.close()
     step_s = t / a.steps
-    return {
+    # the HBM bytes this leg really moves (the policy launch reads every mask byte the step launch wrote,
+    # and the step re-reads every action row): PMC passes of the same leg, same library
+    # (tools/profile_full_contract.sh + tools/full_contract_pmc.py summarize)
+    traffic = None
+    pf = os.path.join(ROOT, "profiles", f"pmc_full_contract_{a.config}.json")
+    if os.path.exists(pf) and a.utt == 1 and world == 1:
+        pj = json.load(open(pf))
+        if pj.get("libmrts_sha256") != lib_sha256():
+            traffic = {"note": f"{os.path.relpath(pf, ROOT)} was taken with another libmrts.so; not used"}
+        elif pj.get("games") == sh["n_slots"] // 2:
+            tb = pj["traffic_bytes_per_step"]
+            traffic = {"bytes_per_step": tb, "GBps": tb / step_s / 1e9, "frac": tb / step_s / 1e9 / HBM_PEAK_GBS,
+                       "kernel_GBps": tb / (pj["kernel_us_per_step"] * 1e-6) / 1e9,
+                       "source": f"{os.path.relpath(pf, ROOT)} ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE of the leg's "
+                                 "policy + step launches, separate --pmc passes, same libmrts.so)"}
+    out = {
         "value": total_games * a.steps / t,
         "ms_per_step": 1e3 * step_s,
         "mask_mode": "full (every mask byte rewritten every step)",
@@ -503,6 +518,9 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
         "note": "SURVEY.md §8(d): B = A + O + M + S per env-step (all action rows read, int32 observation, uint8 masks, "
                 "live state); time = the whole step (policy + step kernels) from the wall clock",
     }
+    if traffic is not None:
+        out["traffic"] = traffic
+    return out
 
 
 def main_c1(a, json_fd):

@@ -5450,6 +5450,7 @@ __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict
     for (int i = l; i < n; i += 64) {
         const uint32_t w = rc[1 + i];
         const int c = (int)(w & 0xFFu);
+        if (c >= HW) continue;  // (a foreign buffer: no LDS write out of range)
         img[c] = (uint8_t)(w >> 8);
         img[HW + c] = (uint8_t)(w >> 16);
         img[2 * HW + c] = (uint8_t)((w >> 27) & 3u);
@@ -5519,7 +5520,7 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
     for (int i = t; i < n; i += 256) {
         const uint32_t w0 = rc[1 + 2 * i], w1 = rc[2 + 2 * i];
         const int c = (int)(w0 & 0xFFFFu), ty = (int)(w1 & 15u) - 1, pl = (int)((w1 >> 4) & 3u) - 1;
-        const uint32_t sb = (w1 >> 8) & 0xFFu;
+        const uint32_t sb = (c < HW && ty >= 0 && ty < MAX_TYPES) ? (w1 >> 8) & 0xFFu : 0u;  // (a foreign buffer: no LDS write out of range)
         const int x = c % W, y = c / W;
         for (int p = 0; p < 2; p++) {
             if (!((sb >> p) & 1u)) continue;
