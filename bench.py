@@ -334,12 +334,14 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
         torch.cuda.synchronize(env.device)
         nx.replay()  # warm replay (the first replay carries one-off costs)
         torch.cuda.synchronize(env.device)
-        dist.barrier()
+        if world > 1:  # (one rank: nothing to wait for; the headline window does the same)
+            dist.barrier()
         torch.cuda.synchronize(env.device)
         t0 = time.perf_counter()
         nx.replay()
         torch.cuda.synchronize(env.device)
-        dist.barrier()
+        if world > 1:  # (one rank: nothing to wait for; the headline window does the same)
+            dist.barrier()
         t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
         how = ("native: mrts_rollout_*_exchange_dev enqueues each step launch and its ncclAllGather on the handle's own "
                "RCCL communicator, captured once as a graph by libmrts (mrts_capture_begin / _end) and replayed")
@@ -351,14 +353,16 @@ def gather_window(env, a, xg, one_step, base, total_games, world, mdist, torch, 
                 one_step(base + k)
             gb.wait()
             torch.cuda.synchronize(env.device)
-            dist.barrier()
+            if world > 1:  # (one rank: nothing to wait for; the headline window does the same)
+                dist.barrier()
             torch.cuda.synchronize(env.device)
             t0 = time.perf_counter()
             for k in range(a.steps):
                 one_step(base + 3 + k)
             gb.wait()  # the last step's exchange belongs to the window
             torch.cuda.synchronize(env.device)
-            dist.barrier()
+            if world > 1:  # (one rank: nothing to wait for; the headline window does the same)
+                dist.barrier()
             t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
         finally:
             xg["buf"] = None
@@ -393,12 +397,14 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     run(base, 3)  # untimed: the first collectives set up the communicator's channels
     rx.buffer(a.steps)
     torch.cuda.synchronize(env.device)
-    dist.barrier()
+    if world > 1:  # (one rank: nothing to wait for; the headline window does the same)
+        dist.barrier()
     torch.cuda.synchronize(env.device)
     t0 = time.perf_counter()
     off = run(base + 3, a.steps)
     torch.cuda.synchronize(env.device)
-    dist.barrier()
+    if world > 1:  # (one rank: nothing to wait for; the headline window does the same)
+        dist.barrier()
     t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
     # the receiving side: every rank's observations of one step back as uint8 planes
     S = env.dims[0]

@@ -5525,7 +5525,11 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
         for (int p = 0; p < 2; p++) {
             if (!((sb >> p) & 1u)) continue;
             atomicMax(&sc[p * HW + c], (uint32_t)(i + 1));
+#ifdef MRTS_RENDER_NOPAINT  // diagnostic build: the render without its sight disks
+            if (false)
+#else
             if (pl >= 0)
+#endif
                 paintDiskRows(rows + (2 * p + (pl == p ? 0 : 1)) * NR, H, W, x, y, P.utt.sight[ty], P.utt.diskLo[ty],
                               P.utt.diskHi[ty]);
         }
