@@ -2839,13 +2839,13 @@ struct Game {
             bool bad = false;
             for (int s0 = 0; s0 < nu; s0 += 64) {
                 const int s = s0 + lid();
-                const uint32_t sb = s < nu ? (uint32_t)snap[s] : 0u;
+                const bool in = s < nu;  // every LDS read of the lane in one round (no dependent second round)
+                const uint32_t sb = in ? (uint32_t)snap[s] : 0u, cu = in ? uc[s] : 0u;
+                const int h = in ? hp[s] : 0, rs = in ? res[s] : 0;
                 const bool inv = (sb & 3u) != 0;
                 const uint64_t m = ballot(inv);
                 const int idx = n + lanes_below(m);
                 if (inv && idx < RU) {
-                    const uint32_t cu = uc[s];
-                    const int h = hp[s], rs = res[s];
                     bad |= h < -128 || h > 127 || rs < 0 || rs > 255;
                     r[1 + 2 * idx] = (uint32_t)(uy(cu) * W + ux(cu)) | (((uint32_t)h & 0xFFu) << 16) | ((uint32_t)rs << 24);
                     r[2 + 2 * idx] = (uint32_t)(utyp(cu) + 1) | ((uint32_t)(uplay(cu) + 1) << 4) | ((sb & 0xFFu) << 8);
@@ -2860,15 +2860,16 @@ struct Game {
         int n = 0;
         for (int s0 = 0; s0 < nu; s0 += 64) {
             const int s = s0 + lid();
-            const uint32_t cu = s < nu ? uc[s] : UC_DEAD;
+            const bool in = s < nu;  // every LDS read of the lane in one round (no dependent second round)
+            const uint32_t cu = in ? uc[s] : UC_DEAD, a = in ? ua[s] : 0u;
+            const uint32_t hr = in ? ((uint32_t)hp[s] & 0xFFu) | (((uint32_t)res[s] & 0xFFu) << 8) : 0u;
             const bool live = !(cu & UC_DEAD);
             const uint64_t m = ballot(live);
             const int idx = n + lanes_below(m);
             if (live && idx < RU) {
-                const uint32_t a = ua[s];
                 const uint32_t act = (a & UA_PRESENT) ? (uint32_t)ua_type(a) : 0u;
-                r[1 + idx] = (uint32_t)(uy(cu) * W + ux(cu)) | (((uint32_t)hp[s] & 0xFFu) << 8) | (((uint32_t)res[s] & 0xFFu) << 16) |
-                             ((uint32_t)(utyp(cu) + 1) << 24) | ((uint32_t)(uplay(cu) + 1) << 27) | (act << 29);
+                r[1 + idx] = (uint32_t)(uy(cu) * W + ux(cu)) | (hr << 8) | ((uint32_t)(utyp(cu) + 1) << 24) |
+                             ((uint32_t)(uplay(cu) + 1) << 27) | (act << 29);
             }
             n += __popcll(m);
         }
@@ -5517,7 +5518,9 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
     for (int i = t; i < 2 * HW + 4 * NR; i += 256) lds[i] = 0u;
     for (int i = t; i < 1 + 2 * n; i += 256) rc[i] = rg[i];
     __syncthreads();
-    for (int i = t; i < n; i += 256) {
+    const int SM = P.utt.maxSight;
+    const bool rowPaint = W <= 32 && SM <= 15;  // one word per sight row, table half-widths
+    for (int i = t; i < n; i += 256) {  // the views' last unit per cell; and the sight disks (general maps)
         const uint32_t w0 = rc[1 + 2 * i], w1 = rc[2 + 2 * i];
         const int c = (int)(w0 & 0xFFFFu), ty = (int)(w1 & 15u) - 1, pl = (int)((w1 >> 4) & 3u) - 1;
         const uint32_t sb = (c < HW && ty >= 0 && ty < MAX_TYPES) ? (w1 >> 8) & 0xFFu : 0u;  // (a foreign buffer: no LDS write out of range)
@@ -5528,12 +5531,33 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
 #ifdef MRTS_RENDER_NOPAINT  // diagnostic build: the render without its sight disks
             if (false)
 #else
-            if (pl >= 0)
+            if (pl >= 0 && !rowPaint)
 #endif
                 paintDiskRows(rows + (2 * p + (pl == p ? 0 : 1)) * NR, H, W, x, y, P.utt.sight[ty], P.utt.diskLo[ty],
                               P.utt.diskHi[ty]);
         }
     }
+#ifndef MRTS_RENDER_NOPAINT
+    if (rowPaint) {
+        // every (unit, row offset) pair on its own thread: 8 units x 32 row offsets per pass (2 SM + 1 <= 31),
+        // one atomicOr per view the unit is in — not one thread looping over a unit's rows
+        const int dy = (t & 31) - SM;
+        for (int i = t >> 5; i < n; i += 8) {
+            const uint32_t w0 = rc[1 + 2 * i], w1 = rc[2 + 2 * i];
+            const int c = (int)(w0 & 0xFFFFu), ty = (int)(w1 & 15u) - 1, pl = (int)((w1 >> 4) & 3u) - 1;
+            const uint32_t sb = (c < HW && ty >= 0 && ty < MAX_TYPES && pl >= 0) ? (w1 >> 8) & 3u : 0u;
+            const int ady = dy < 0 ? -dy : dy, sr = sb ? P.utt.sight[ty] : -1;
+            const int x = c % W, yy = c / W + dy;
+            if (ady <= sr && yy >= 0 && yy < H) {
+                const uint32_t half = ((ady < 8 ? P.utt.diskLo[ty] : P.utt.diskHi[ty]) >> (4 * (ady & 7))) & 0xFu;
+                const int x0 = max(0, x - (int)half), x1 = min(W - 1, x + (int)half);
+                const uint32_t b = ((2u << (x1 - x0)) - 1u) << x0;  // columns x0..x1 (x1 - x0 = 31: 2u << 31 wraps to 0)
+                if (sb & 1u) atomicOr(&rows[(pl == 0 ? 0 : 1) * NR + yy], b);
+                if (sb & 2u) atomicOr(&rows[(2 + (pl == 1 ? 0 : 1)) * NR + yy], b);
+            }
+        }
+    }
+#endif
     __syncthreads();
     const uint32_t* terr = (const uint32_t*)(P.tmpl + P.tmpl_off[g] + T_TERR);
     const int WPR = (W + 31) >> 5;
