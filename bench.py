@@ -175,14 +175,12 @@ class _FenceFreeEvent:
         return ms.value
 
 
-def lib_sha256():
-    """SHA-256 of the libmrts.so this process runs (the counter files name the library they describe)."""
-    import hashlib
-
+def code_sha256():
+    """SHA-256 of the gfx950 code object of the libmrts.so this process runs: the counter files name the
+    kernels' machine code they describe (microrts_amd._lib.device_code_sha256)."""
     from microrts_amd import _lib
 
-    with open(_lib.LIB_PATH, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()
+    return _lib.device_code_sha256()
 
 
 def cgroup_cpus():
@@ -498,20 +496,20 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
     env.close()
     step_s = t / a.steps
     # the HBM bytes this leg really moves (the policy launch reads every mask byte the step launch wrote,
-    # and the step re-reads every action row): PMC passes of the same leg, same library
+    # and the step re-reads every action row): PMC passes of the same leg, same kernel code
     # (tools/profile_full_contract.sh + tools/full_contract_pmc.py summarize)
     traffic = None
     pf = os.path.join(ROOT, "profiles", f"pmc_full_contract_{a.config}.json")
     if os.path.exists(pf) and a.utt == 1 and world == 1:
         pj = json.load(open(pf))
-        if pj.get("libmrts_sha256") != lib_sha256():
-            traffic = {"note": f"{os.path.relpath(pf, ROOT)} was taken with another libmrts.so; not used"}
+        if pj.get("gfx950_code_sha256") != code_sha256():
+            traffic = {"note": f"{os.path.relpath(pf, ROOT)} was taken with other kernel code; not used"}
         elif pj.get("games") == sh["n_slots"] // 2:
             tb = pj["traffic_bytes_per_step"]
             traffic = {"bytes_per_step": tb, "GBps": tb / step_s / 1e9, "frac": tb / step_s / 1e9 / HBM_PEAK_GBS,
                        "kernel_GBps": tb / (pj["kernel_us_per_step"] * 1e-6) / 1e9,
                        "source": f"{os.path.relpath(pf, ROOT)} ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE of the leg's "
-                                 "policy + step launches, separate --pmc passes, same libmrts.so)"}
+                                 "policy + step launches, separate --pmc passes, same gfx950 code object)"}
     out = {
         "value": total_games * a.steps / t,
         "ms_per_step": 1e3 * step_s,
@@ -859,9 +857,9 @@ def main():
                 and pj.get("utt", "VERSION_ORIGINAL, CANCEL_BOTH") == utt_name
                 and pj.get("mask_mode") == ("off" if uniform else a.mask_mode) and launch_ms is not None):
             pj = None  # another workload or launch form: its counters do not describe this line
-        elif pj.get("libmrts_sha256") != lib_sha256():
-            pmc_note = (f"profiles/pmc_{a.config}.json was taken with another libmrts.so "
-                        f"({(pj.get('libmrts_sha256') or 'no hash')[:12]}); its counters are not used")
+        elif pj.get("gfx950_code_sha256") != code_sha256():
+            pmc_note = (f"profiles/pmc_{a.config}.json was taken with other kernel code "
+                        f"({(pj.get('gfx950_code_sha256') or 'no hash')[:12]}); its counters are not used")
             pj = None  # stale counters must not describe this library's kernel
     if traffic is None and pj is not None and pj.get("traffic_bytes_per_step"):
         per_step = pj["traffic_bytes_per_step"]
@@ -901,7 +899,7 @@ def main():
             "dual_issue_quad_cycles_per_game_step": per.get("SQ_ACTIVE_INST_VALU2"),
             "clock_ghz": clk,
             "games_per_simd": iq.get("games_per_simd"),
-            "source": f"profiles/pmc_{a.config}.json ({pj['tag']}: SQ PMC pass of the same command, same libmrts.so) + "
+            "source": f"profiles/pmc_{a.config}.json ({pj['tag']}: SQ PMC pass of the same command, same gfx950 code object) + "
                       + (f"profiles/issue_ceiling_{a.config}.json (probe {ic['probe']}, static mix of {ic['static_valu_instructions']} "
                          "VALU opcodes)" if ic else "no issue_ceiling file: the guide's 2 cycles"),
         }

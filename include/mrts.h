@@ -186,6 +186,11 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
  * with dlopen / dlsym, so libmrts has no link-time dependency on RCCL. */
 int mrts_rccl_unique_id(const char* rccl_path, void* out);
 int mrts_exchange_init(mrts_env* env, const char* rccl_path, int32_t nranks, int32_t rank, const void* unique_id);
+/* Test transport (no RCCL, one GPU): the exchange calls behave as on rank `rank` of `nranks`, and each
+ * all-gather copies this rank's bytes into every rank's place — as if the nranks - 1 peers had produced
+ * the same data — so the multi-rank layout (rank offsets, strides, chunk bases, the render of every
+ * rank) is checkable where RCCL cannot place two ranks on one device. */
+int mrts_exchange_init_loopback(mrts_env* env, int32_t nranks, int32_t rank);
 /* n_steps fused steps (mrts_rollout_fused_dev's, but one launch per step: every step's observation is
  * exchanged) each followed by an all-gather of that step's observation as int16 [n_slots][C][H][W]
  * (the step kernel writes it into d_send0 / d_send1 alternately, mrts_set_obs16's transport) from every

@@ -17,11 +17,40 @@ ERR_BITS = {
     1 << 4: "NEG_RESOURCES", 1 << 5: "MOVE_COLLISION",
 }
 
+def device_code_sha256(path=None):
+    """SHA-256 of the gfx950 code object inside libmrts.so (the .hip_fatbin offload bundle's amdgcn entry):
+    the kernels' machine code.  Counter files (profiles/pmc_*.json) name the code they describe with it,
+    so a host-only change to the library keeps them valid and any kernel change voids them."""
+    import hashlib
+    import struct
+
+    data = open(path or LIB_PATH, "rb").read()
+    shoff = struct.unpack_from("<Q", data, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stroff = secs[shstrndx][4]
+    for name, _, _, _, off, size in secs:
+        if data[stroff + name:data.index(b"\0", stroff + name)] != b".hip_fatbin":
+            continue
+        b = data[off:off + size]
+        if not b.startswith(b"__CLANG_OFFLOAD_BUNDLE__"):
+            break
+        n, p = struct.unpack_from("<Q", b, 24)[0], 32
+        for _ in range(n):
+            eoff, esize, tl = struct.unpack_from("<QQQ", b, p)
+            p += 24
+            triple = b[p:p + tl].decode()
+            p += tl
+            if "amdgcn" in triple:
+                return hashlib.sha256(b[eoff:eoff + esize]).hexdigest()
+    raise RuntimeError(f"{path or LIB_PATH}: no amdgcn code object in .hip_fatbin")
+
+
 # every symbol include/mrts.h declares
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_step_rows", "mrts_get_masks_i32",
     "mrts_get_masks_host", "mrts_get_masks_i32_host",
-    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_step_fused_dev", "mrts_rollout_fused_dev", "mrts_set_rollout_events", "mrts_rccl_unique_id", "mrts_exchange_init", "mrts_rollout_fused_exchange_dev", "mrts_rollout_uniform_exchange_dev", "mrts_set_exchange_bytes", "mrts_set_records", "mrts_record_words", "mrts_rollout_fused_records_dev", "mrts_rollout_uniform_records_dev", "mrts_render_records_dev", "mrts_capture_begin", "mrts_capture_end", "mrts_replay", "mrts_set_multi_step", "mrts_multi_step_capable", "mrts_set_obs16", "mrts_policy_uniform_dev", "mrts_step_uniform_dev", "mrts_rollout_uniform_dev", "mrts_policy_invalidate", "mrts_set_obs_delta", "mrts_obs_invalidate", "mrts_set_source_output", "mrts_copy_games", "mrts_copy_games_dev", "mrts_playout", "mrts_playout_dev", "mrts_trace_step",
+    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_step_fused_dev", "mrts_rollout_fused_dev", "mrts_set_rollout_events", "mrts_rccl_unique_id", "mrts_exchange_init", "mrts_exchange_init_loopback", "mrts_rollout_fused_exchange_dev", "mrts_rollout_uniform_exchange_dev", "mrts_set_exchange_bytes", "mrts_set_records", "mrts_record_words", "mrts_rollout_fused_records_dev", "mrts_rollout_uniform_records_dev", "mrts_render_records_dev", "mrts_capture_begin", "mrts_capture_end", "mrts_replay", "mrts_set_multi_step", "mrts_multi_step_capable", "mrts_set_obs16", "mrts_policy_uniform_dev", "mrts_step_uniform_dev", "mrts_rollout_uniform_dev", "mrts_policy_invalidate", "mrts_set_obs_delta", "mrts_obs_invalidate", "mrts_set_source_output", "mrts_copy_games", "mrts_copy_games_dev", "mrts_playout", "mrts_playout_dev", "mrts_trace_step",
     "mrts_evaluate", "mrts_evaluate_dev", "mrts_utt_json", "mrts_get_state_json",
     "mrts_set_state_json", "mrts_checkpoint_size", "mrts_checkpoint", "mrts_restore", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
@@ -109,6 +138,7 @@ def load(path=LIB_PATH):
     C = ctypes.c_char_p
     L.mrts_rccl_unique_id.argtypes = [C, P]
     L.mrts_exchange_init.argtypes = [P, C, I32, I32, P]
+    L.mrts_exchange_init_loopback.argtypes = [P, I32, I32]
     L.mrts_rollout_fused_exchange_dev.argtypes = [P, P, P, P, P, P, P, I32, U64, U32, I32, P, P, P, P]
     L.mrts_rollout_uniform_exchange_dev.argtypes = [P, P, P, P, P, P, U64, U32, I32, P, P, P, P]
     L.mrts_set_exchange_bytes.argtypes = [P, I32]

@@ -493,6 +493,7 @@ struct mrts_env {
     // its own communication stream, and per send buffer the step-ready / collective-done events
     ncclComm_t exComm = nullptr;
     int exRanks = 0, exRank = 0;
+    bool exLoop = false;  // mrts_exchange_init_loopback: the test transport (no RCCL), see exAllGather
     // compact observation records (mrts_set_records): units per record (0 = off), steps per launch of a
     // records rollout (0 = as many as a launch can run)
     int recUnits = 0, recSteps = 0;
@@ -1245,12 +1246,27 @@ void loadRccl(const char* path) {
 void ncclChk(ncclResult_t r, const char* what) {
     if (r != ncclSuccess) throw Fail{-EIO, std::string(what) + ": " + g_rccl.errorString(r)};
 }
+bool exInited(const mrts_env* env) { return env->exComm != nullptr || env->exLoop; }
+// The all-gather of `bytes` per rank from send into recv ([ranks][bytes]) on the exchange stream.  The
+// loopback test transport (mrts_exchange_init_loopback) stands in for ranks - 1 peers that produced the
+// same bytes as this rank: send is copied to every rank's place — so a wrong rank offset, stride or
+// chunk base shows up on one GPU as a mismatch in some rank's place.
+void exAllGather(mrts_env* env, const void* send, void* recv, size_t bytes) {
+    if (env->exLoop) {
+        for (int r = 0; r < env->exRanks; r++) {
+            uint8_t* dst = (uint8_t*)recv + (size_t)r * bytes;
+            if (dst != send) HIPCHK(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, env->exStream));
+        }
+        return;
+    }
+    ncclChk(g_rccl.allGather(send, recv, bytes, ncclUint8, env->exComm, env->exStream), "ncclAllGather");
+}
 // per step: wait until the collective that last read send buffer k % 2 is done, run the step (it
 // writes its int16 observation there), then all-gather it into recv on the exchange stream
 template <class StepFn>
 void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t* d_send0, int16_t* d_send1, int16_t* d_recv,
                   void* stream, StepFn step) {
-    if (!env->exComm) throw Fail{-EINVAL, "mrts_exchange_init first"};
+    if (!exInited(env)) throw Fail{-EINVAL, "mrts_exchange_init first"};
     // the step kernel writes the transport as part of its observation write (prepObs)
     if (!d_obs) throw Fail{-EINVAL, "the exchange needs an observation buffer (d_obs)"};
     if (env->exBytes == 1 && !env->obsImg) throw Fail{-ENOTSUP, "uint8 exchange: an observation value no longer fits a byte"};
@@ -1277,7 +1293,7 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t*
             step(k);
             HIPCHK(hipEventRecord(env->exReady[b], s));
             HIPCHK(hipStreamWaitEvent(env->exStream, env->exReady[b], 0));
-            ncclChk(g_rccl.allGather(send[b], d_recv, bytes, ncclUint8, env->exComm, env->exStream), "ncclAllGather");
+            exAllGather(env, send[b], d_recv, bytes);
             HIPCHK(hipEventRecord(env->exDone[b], env->exStream));
             pending[b] = true;
             env->exPending[b] = true;
@@ -1299,7 +1315,7 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t*
 // many it enqueued.
 template <class StepFn>
 void recordsLoop(mrts_env* env, int32_t n_steps, uint32_t* d_recv, int64_t* offsets, void* stream, StepFn step) {
-    if (!env->exComm) throw Fail{-EINVAL, "mrts_exchange_init first"};
+    if (!exInited(env)) throw Fail{-EINVAL, "mrts_exchange_init first"};
     if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
     if (!d_recv || ((uintptr_t)d_recv & 15)) throw Fail{-EINVAL, "the receive buffer must be non-null and 16-byte aligned"};
     // (partially observable records carry hp as int8: the kernel flags a value outside the record's range)
@@ -1316,9 +1332,7 @@ void recordsLoop(mrts_env* env, int32_t n_steps, uint32_t* d_recv, int64_t* offs
         HIPCHK(hipEventRecord(env->exReady[0], s));
         HIPCHK(hipStreamWaitEvent(env->exStream, env->exReady[0], 0));
         const size_t words = (size_t)n * per;
-        ncclChk(g_rccl.allGather(d_recv + base + (size_t)env->exRank * words, d_recv + base, words * 4, ncclUint8, env->exComm,
-                                 env->exStream),
-                "ncclAllGather");
+        exAllGather(env, d_recv + base + (size_t)env->exRank * words, d_recv + base, words * 4);
         if (offsets)
             for (int32_t j = 0; j < n; j++) {
                 offsets[2 * (size_t)(k + j)] = (int64_t)(base + (size_t)j * per);
@@ -1469,7 +1483,7 @@ int mrts_rccl_unique_id(const char* rccl_path, void* out) {
 int mrts_exchange_init(mrts_env* env, const char* rccl_path, int32_t nranks, int32_t rank, const void* unique_id) {
     try {
         if (!env || !unique_id || nranks < 1 || rank < 0 || rank >= nranks) throw Fail{-EINVAL, "bad exchange arguments"};
-        if (env->exComm) throw Fail{-EINVAL, "the exchange is already initialised"};
+        if (exInited(env)) throw Fail{-EINVAL, "the exchange is already initialised"};
         loadRccl(rccl_path);
         HIPCHK(hipSetDevice(env->device));
         ncclUniqueId id;
@@ -1482,6 +1496,25 @@ int mrts_exchange_init(mrts_env* env, const char* rccl_path, int32_t nranks, int
             HIPCHK(hipEventCreateWithFlags(&env->exReady[b], hipEventDisableTiming));
             HIPCHK(hipEventCreateWithFlags(&env->exDone[b], hipEventDisableTiming));
         }
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_exchange_init_loopback(mrts_env* env, int32_t nranks, int32_t rank) {
+    try {
+        if (!env || nranks < 1 || rank < 0 || rank >= nranks) throw Fail{-EINVAL, "bad exchange arguments"};
+        if (exInited(env)) throw Fail{-EINVAL, "the exchange is already initialised"};
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(hipStreamCreateWithFlags(&env->exStream, hipStreamNonBlocking));
+        for (int b = 0; b < 2; b++) {
+            HIPCHK(hipEventCreateWithFlags(&env->exReady[b], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&env->exDone[b], hipEventDisableTiming));
+        }
+        env->exRanks = nranks;
+        env->exRank = rank;
+        env->exLoop = true;
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1863,10 +1896,8 @@ void mrts_destroy(mrts_env* env) {
     (void)hipHostFree(env->h_reward);
     (void)hipHostFree(env->h_done);
     if (env->stream) (void)hipStreamDestroy(env->stream);
-    if (env->exComm) {
-        (void)hipStreamSynchronize(env->exStream);
-        (void)g_rccl.commDestroy(env->exComm);
-    }
+    if (env->exStream) (void)hipStreamSynchronize(env->exStream);
+    if (env->exComm) (void)g_rccl.commDestroy(env->exComm);
     if (env->exStream) (void)hipStreamDestroy(env->exStream);
     if (env->capExec) (void)hipGraphExecDestroy(env->capExec);
     if (env->capGraph) (void)hipGraphDestroy(env->capGraph);

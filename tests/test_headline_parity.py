@@ -505,3 +505,69 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
     assert (B.error_flags() & (1 << 6)).any(), "MRTS_ERR_RECORD"
     for e in (A, B):
         e.close()
+
+
+@pytest.mark.parametrize("mp,po,spl,world,rank", [("maps/16x16/basesWorkers16x16.xml", False, 0, 8, 3),
+                                                  ("maps/16x16/basesWorkers16x16.xml", False, 7, 8, 7),
+                                                  ("maps/BWDistantResources32x32.xml", True, 9, 4, 1)])
+def test_record_exchange_loopback_ranks(mp, po, spl, world, rank):
+    """The records exchange's multi-rank layout on one GPU (mrts_exchange_init_loopback: rank `rank` of
+    `world`, every all-gather copies this rank's records into every rank's place, as if the peers had
+    produced the same games).  Every step's chunk: this rank's records sit at offset + rank x stride and
+    every rank's place holds the same words; rendering all `world` ranks gives `world` copies of the
+    twin's int32 observation of that step — a wrong rank offset, stride or chunk base fails here, where
+    RCCL cannot put two ranks on one device.  The tensor exchange's [ranks][...] receive buffer too."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n_sp = 64
+    kw = dict(partial_obs=True, max_units=256) if po else {}
+    A = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=29, **kw)
+    B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=29, **kw)
+    A.set_multi_step(False)
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+    L, h = B._h.L, B._h.h
+    assert L.mrts_exchange_init_loopback(h, world, world) != 0  # rank out of range
+    assert L.mrts_exchange_init_loopback(h, world, rank) == 0
+    assert L.mrts_exchange_init_loopback(h, world, rank) != 0  # already initialised
+    words = B.set_records(64, spl)
+    G = n_sp // 2
+    k = 0
+    for n in (1, 40, 25):
+        want = []
+        for j in range(n):
+            A.rollout_fused(SEED, k + j + 1, 1)
+            A.synchronize()
+            want.append(A.obs.clone())
+        recv = B.records_buffer(n, world)
+        recv.fill_(-7)  # every record header the exchange owes must be written (unit words past n are don't-care)
+        off = B.rollout_fused_records(SEED, k + 1, n, recv)
+        k += n
+        B.synchronize()
+        for j in range(n):
+            o, stride = int(off[j, 0]), int(off[j, 1])
+            assert stride >= G * words and (o + (world - 1) * stride + G * words) <= recv.numel()
+            mine = recv[o + rank * stride:o + rank * stride + G * words]
+            assert not bool((mine.view(G, words)[:, 0] == -7).any()), f"step {k - n + j}: a record header never written"
+            for r in range(world):
+                assert torch.equal(recv[o + r * stride:o + r * stride + G * words], mine), f"step {k - n + j}: rank {r}"
+            out = torch.zeros((world * 2 * G,) + tuple(B.obs.shape[1:]), dtype=torch.int32, device=B.device)
+            B.render_records(recv, o, stride, world, out)
+            B.synchronize()
+            for r in range(world):
+                assert torch.equal(out[r * 2 * G:(r + 1) * 2 * G], want[j]), f"step {k - n + j}: rendered rank {r}"
+        assert torch.equal(A.obs, B.obs) and torch.equal(A.masks, B.masks)
+    if not po:  # the per-step tensor exchange: [ranks][slots][C][H][W]
+        send = [torch.zeros(tuple(B.obs.shape), dtype=torch.int16, device=B.device) for _ in range(2)]
+        tr = torch.full((world,) + tuple(B.obs.shape), -7, dtype=torch.int16, device=B.device)
+        A.rollout_fused(SEED, k + 1, 3)
+        B.rollout_fused_exchange(SEED, k + 1, 3, send, tr)
+        A.synchronize()
+        B.synchronize()
+        for r in range(world):
+            assert torch.equal(tr[r], A.obs.to(torch.int16)), f"tensor exchange rank {r}"
+    for e in (A, B):
+        assert not e.error_flags().any()
+        e.close()

@@ -60,7 +60,7 @@ def summarize(a):
     line = json.loads(open(os.path.join(src, "run.json")).read().strip().splitlines()[-1])
     K, cfg = line["steps"], line["config"]
     out = {"tag": a.tag, "config": cfg, "steps": K, "games": line["games"],
-           "libmrts_sha256": open(os.path.join(src, "libmrts.sha256")).read().strip()}
+           "gfx950_code_sha256": open(os.path.join(src, "code.sha256")).read().strip()}
     per = {}
     for c, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
         ds = dispatches(os.path.join(src, sub, "run_counter_collection.csv"))

@@ -15,7 +15,7 @@ mkdir -p "$OUT"
 BARGS="--config $CFG --steps 100 --warmup 10 --burnin 1000 --no-cpu-baseline --no-compare --no-gather-window --no-full-contract $*"
 SQ="SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 # the counters describe THIS library: bench.py ignores a pmc_<cfg>.json whose hash differs
-sha256sum microrts_amd/libmrts.so | cut -d' ' -f1 > "$OUT/libmrts.sha256"
+python -c "from microrts_amd._lib import device_code_sha256; print(device_code_sha256())" > "$OUT/code.sha256" || exit $?
 timeout -k 10 300 python bench.py $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/stats" -o run -- python3 bench.py $BARGS > "$OUT/stats.log" 2>&1 || exit $?
 timeout -k 5 150 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py $BARGS > "$OUT/pmc_fetch.log" 2>&1 || exit $?

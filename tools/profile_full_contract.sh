@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/$TAG/fc_$CFG
 mkdir -p "$OUT"
 A="tools/full_contract_pmc.py run --config $CFG --steps 20"
-sha256sum microrts_amd/libmrts.so | cut -d' ' -f1 > "$OUT/libmrts.sha256"
+python -c "from microrts_amd._lib import device_code_sha256; print(device_code_sha256())" > "$OUT/code.sha256" || exit $?
 timeout -k 10 300 python $A > "$OUT/run.json" 2> "$OUT/run.err" || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/stats" -o run -- python3 $A > "$OUT/stats.log" 2>&1 || exit $?
 timeout -k 5 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $A > "$OUT/pmc_fetch.log" 2>&1 || exit $?

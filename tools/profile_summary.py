@@ -89,8 +89,8 @@ def main():
            "trace_launch_us": launch_us, "trace_us_per_step": launch_us / K, "bench_event_us_per_step": bench["step_kernel_ms"] * 1e3,
            "single_step_launch_us": statistics.mean(singles),
            # the library the counters were taken with (tools/profile_config.sh); bench.py refuses a mismatch
-           "libmrts_sha256": open(os.path.join(a.src, "libmrts.sha256")).read().strip()
-           if os.path.exists(os.path.join(a.src, "libmrts.sha256")) else None}
+           "gfx950_code_sha256": open(os.path.join(a.src, "code.sha256")).read().strip()
+           if os.path.exists(os.path.join(a.src, "code.sha256")) else None}
     lines = [f"# Profile {a.tag} — {cfg}", "", "bench.py line (profiled flags):", "", "```json", json.dumps(bench, indent=1), "```", "",
              "## rocprofv3 --kernel-trace --stats (every launch of the command)", "", "```",
              open(os.path.join(a.src, "stats", "run_kernel_stats.csv")).read().strip(), "```", "",
