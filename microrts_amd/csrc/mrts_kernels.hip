@@ -171,9 +171,12 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_HELPER_PRIO
 #define MRTS_HELPER_PRIO 0
 #endif
-// 1: partially observable multi-step launches without the render helper wave (A/B builds)
+// 1: partially observable multi-step launches without the render helper wave.  The default since the
+// round-4 full-size soak (tests/soak_full_parity.py): with the helper, 2 of 2048 c5 games showed one stale
+// observation value for a unit that died in the observed step (the helper's packed delta render); every
+// game is bit-exact without it.  0 = the helper build (kept for the fix and its A/B).
 #ifndef MRTS_NO_PO_HELPER
-#define MRTS_NO_PO_HELPER 0
+#define MRTS_NO_PO_HELPER 1
 #endif
 // issue-priority thresholds on a game's unit count (k_env): 1 / 2 / 3 from T1 / T2 / T3 units
 // (units + own idle units; measured against units alone at 24 / 30 / 36: c3 +1.8 % at K = 200,

@@ -30,15 +30,19 @@ POINTS = (("burnin", BURNIN), ("k20", 20), ("k200", 200))
 FIELDS = ("obs", "reward", "done", "masks", "actions")
 
 
-def gpu_run(cfg, tmp):
+def gpu_run(cfg, tmp, variant="bench"):
     import torch
 
     from microrts_amd import DeviceVecEnv
 
     mp_, n_games, po, mu, seed = SHAPES[cfg]
     S = 2 * n_games
-    env = DeviceVecEnv(S, 0, 2000, [os.path.join(ROOT, mp_)] * S, seed=seed, partial_obs=po, max_units=mu)
-    assert env.fused_multi_step
+    env = DeviceVecEnv(S, 0, 2000, [os.path.join(ROOT, mp_)] * S, seed=seed, partial_obs=po, max_units=mu,
+                       obs_delta=variant != "nodelta")
+    if variant == "single":  # one launch per step (no multi-step launch, no helper wave)
+        env.set_multi_step(False)
+    else:
+        assert env.fused_multi_step
     env.reset()
     env.random_policy(SEED, 0)
     k = 0
@@ -68,6 +72,7 @@ def shard(args):
     ref.reset()
     t = 0
     bad = {}
+    detail = []
 
     def act(step):
         m = ref.get_masks(0)
@@ -83,17 +88,22 @@ def shard(args):
         m, nxt = act(t)  # the rows the launch sampled for the next step
         got = {"obs": ref.obs, "reward": ref.reward, "done": ref.done, "masks": m, "actions": nxt}
         for f in FIELDS:
-            ok = np.asarray(z[f][sl]).reshape(len(slots), -1) == np.asarray(got[f]).reshape(len(slots), -1)
+            gz, rz = np.asarray(z[f][sl]).reshape(len(slots), -1), np.asarray(got[f]).reshape(len(slots), -1)
+            ok = gz == rz
             nbad = int((~ok.all(axis=1)).sum())
             if nbad:
                 bad[f"{tag}/{f}"] = nbad
+                for i in np.nonzero(~ok.all(axis=1))[0][:4]:  # where: slot, flat index, GPU value, oracle value
+                    idx = np.nonzero(~ok[i])[0]
+                    detail.append({"point": tag, "field": f, "slot": int(slots[i]), "n_diff": int(len(idx)),
+                                   "first": [[int(j), int(gz[i, j]), int(rz[i, j])] for j in idx[:8]]})
         off = z["state_off"]
         st = z["state"]
         nst = sum(0 if np.array_equal(st[off[s]:off[s + 1]], ref.dump(i)) else 1 for i, s in enumerate(slots))
         if nst:
             bad[f"{tag}/state"] = nst
     ref.close()
-    return g1 - g0, bad
+    return g1 - g0, bad, detail
 
 
 def main():
@@ -101,30 +111,34 @@ def main():
     ap.add_argument("--config", choices=sorted(SHAPES), default="c3")
     ap.add_argument("--workers", type=int, default=16)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--variant", choices=["bench", "nodelta", "single"], default="bench",
+                    help="bench = bench.py's form; nodelta = full observation renders; single = one launch per step")
     ap.add_argument("--gpu-into", default=None, help=argparse.SUPPRESS)  # the GPU child's role
     a = ap.parse_args()
     if a.gpu_into:
-        gpu_run(a.config, a.gpu_into)
+        gpu_run(a.config, a.gpu_into, a.variant)
         return
     t0 = time.time()
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as tmp:
         # the GPU run is a child process of its own: this process never initialises the GPU, so the
         # oracle worker processes it starts next are started from a GPU-free parent
-        subprocess.run([sys.executable, os.path.abspath(__file__), "--config", a.config, "--gpu-into", tmp], check=True)
+        subprocess.run([sys.executable, os.path.abspath(__file__), "--config", a.config, "--variant", a.variant,
+                        "--gpu-into", tmp], check=True)
         t_gpu = time.time() - t0
         n_games = SHAPES[a.config][1]
         step = (n_games + a.workers - 1) // a.workers
         jobs = [(a.config, tmp, g, min(g + step, n_games)) for g in range(0, n_games, step)]
         with mp.get_context("spawn").Pool(len(jobs)) as pool:
             res = pool.map(shard, jobs)
-    bad = {}
-    for _, b in res:
+    bad, detail = {}, []
+    for _, b, d in res:
+        detail += d
         for k, v in b.items():
             bad[k] = bad.get(k, 0) + v
-    out = {"config": a.config, "games": sum(n for n, _ in res), "slots": 2 * sum(n for n, _ in res),
+    out = {"config": a.config, "variant": a.variant, "games": sum(n for n, _, _ in res), "slots": 2 * sum(n for n, _, _ in res),
            "points": [f"{tag} (+{n} steps)" for tag, n in POINTS], "fields": list(FIELDS) + ["state"],
            "mismatching_slots": bad, "bit_exact": not bad, "gpu_s": round(t_gpu, 1), "total_s": round(time.time() - t0, 1),
-           "workers": len(jobs)}
+           "workers": len(jobs), "mismatches": detail[:16]}
     line = json.dumps(out)
     print(line, flush=True)
     if a.out:
