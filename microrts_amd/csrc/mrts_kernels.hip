@@ -4800,8 +4800,10 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
     if (G.po) G.clearSnap();
     if (HELP && FPO && poPacked) {  // S_{it-1}: the helper's snapshot of this step (snapFromPack)
         ldsBarrier();
+#ifndef MRTS_PO_HELPER_NOSNAP  // diagnostic build: the game wave takes its own snapshot
         G.takeSnap((const uint8_t*)(poHelpHdr + 8 + 2 * G.H));
         snapTaken = true;
+#endif
     }
     PHASE(0);
 
