@@ -251,6 +251,20 @@ int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const in
 int32_t mrts_record_words(const mrts_env* env);
 int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,
                             int32_t out_bytes, void* stream);
+/* 1 if a record rendered by this handle since the last call had its overflow bit set (its game held more
+ * units than the record, or a value outside the record's range: the rendered observation lacks them —
+ * the sender's handle flagged MRTS_ERR_RECORD), else 0; resets the flag.  Synchronises the device. */
+int mrts_render_status(mrts_env* env);
+/* Every step's Responses from a rollout call (JNIGridnetVecClient.gameStep returns observation, reward
+ * and done on EVERY call, src/tests/JNIGridnetVecClient.java:213-297, src/ai/jni/Responses.java:12-30;
+ * a multi-step launch otherwise leaves only the last step's in d_reward / d_done).  After this call,
+ * every mrts_rollout_{fused,uniform}[_records|_exchange]_dev call also writes the reward / done of its
+ * k-th step ([n_slots][n_rewards], as d_reward / d_done; done[.][0] = 1 when the step auto-reset the
+ * game) at d_rewards / d_dones + k * n_slots * n_rewards, k = 0 .. n_steps - 1 — inside multi-step
+ * launches too.  With a records rollout, step k's observation is its records rendered
+ * (mrts_render_records_dev at step_offsets[k]): the full per-step Responses without one launch per step.
+ * A rollout call of more than max_steps steps returns -EINVAL.  NULL, NULL turns it off. */
+int mrts_set_step_responses(mrts_env* env, double* d_rewards, uint8_t* d_dones, int32_t max_steps);
 /* Graph form of a handle's calls (no Java counterpart): everything this handle enqueues on `stream`
  * between mrts_capture_begin and mrts_capture_end (stream capture, thread-local mode; the exchange
  * stream of an exchange rollout is joined inside the call) is instantiated as one graph, which

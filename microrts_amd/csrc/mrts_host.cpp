@@ -44,7 +44,7 @@ hipError_t launchCopyGames(int32_t* dst, const int32_t* src, const int32_t* pair
                            int CAP, int HW, hipStream_t stream);
 hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, float* out, hipStream_t stream);
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
-                               int64_t rank_stride, void* out, int out_bytes, hipStream_t stream);
+                               int64_t rank_stride, void* out, int out_bytes, int32_t* err, hipStream_t stream);
 }  // namespace mrts
 
 static thread_local std::string g_err;
@@ -486,9 +486,11 @@ struct mrts_env {
     const int32_t* lastObsPtr = nullptr;
     int32_t* d_poPrev = nullptr;
     uint32_t* d_prioTab = nullptr;  // multi-step launches: per-SIMD issue-rank table (KDyn.prio_tab)
+    int32_t* d_renderErr = nullptr; // the record renders' overflow flag (mrts_render_status)
     int32_t* d_bal = nullptr;       // multi-step launches: balanced game placement (KDyn.bal)
     int obsImg = 0;                 // KDyn.obs_img: every observation value fits a byte
-    bool exPending[2] = {false, false};  // exDone[b] was recorded by an earlier exchange call
+    bool exPending[2] = {false, false};  // exDone[b] was recorded by an earlier (eager) exchange call
+    hipStream_t exLastStream = nullptr;  // the stream of the last eager exchange call (already waits for them)
     // native observation exchange (mrts_exchange_init): an RCCL communicator over this handle's ranks,
     // its own communication stream, and per send buffer the step-ready / collective-done events
     ncclComm_t exComm = nullptr;
@@ -526,6 +528,13 @@ struct mrts_env {
     // mrts_set_rollout_events: HIP events the next native rollout records around its launches (one shot)
     hipEvent_t evStart = nullptr, evEnd = nullptr;
     mutable uint32_t launchStamp = 0;       // KDyn.fwd_stamp of the last k_env launch (never 0)
+    // every step's Responses (mrts_set_step_responses): the ring and its capacity in steps; during a rollout
+    // call respK = the call's next step index (each MODE_STEP launch writes its steps there and advances
+    // it), -1 outside rollout calls
+    double* respRew = nullptr;
+    uint8_t* respDone = nullptr;
+    int32_t respMax = 0;
+    mutable int32_t respK = -1;
     int polParity = 0;
     // the kernels store observations and mask chunks as 16-byte vectors
     static void checkAlign(const KDyn& D) {
@@ -598,6 +607,13 @@ struct mrts_env {
         D.prio_tab = D.n_iter > 1 ? d_prioTab : nullptr;
         D.bal = D.n_iter > 1 ? d_bal : nullptr;
         D.obs_img = obsImg;
+        if (mode == 0 /* MODE_STEP */ && respK >= 0 && respRew) {  // the call's Responses ring (RespScope)
+            const size_t stride = (size_t)nSlots * hstatic.n_rewards;
+            D.reward = respRew + (size_t)respK * stride;
+            D.done = respDone + (size_t)respK * stride;
+            D.resp_stride = (int32_t)stride;
+            respK += D.n_iter > 1 ? D.n_iter : 1;
+        }
         return launchEnv(mode, hstatic, d_static, D, s, e0, e1);
     }
     // a state block about to be injected: if any live unit's hp or resources leaves 0..255, the byte
@@ -931,15 +947,17 @@ int mrts_step_dev(mrts_env* env, const int32_t* d_actions, const int32_t* d_play
 
 namespace {
 // records rollout (mrts_rollout_*_records_dev): the launch writes its steps' records into `chunk`, the
-// part of the receive buffer its all-gather fills, at this rank's place ([rank][n_iter][games][words])
+// part of the receive buffer one all-gather fills, at this rank's place ([rank][steps][games][words]):
+// the chunk holds `steps` steps, and this launch's first one is step `first` of them
 struct RecPlan {
     uint32_t* chunk;
     int rank;
+    int steps, first;
 };
 void planRecords(const mrts_env* env, KDyn& D, const RecPlan* rec) {
     if (!rec) return;
     D.rec_units = env->recUnits;
-    D.rec_out = rec->chunk + (size_t)rec->rank * D.n_iter * env->nGames * recWords(env->recUnits, env->partialObs);
+    D.rec_out = rec->chunk + ((size_t)rec->rank * rec->steps + rec->first) * env->nGames * recWords(env->recUnits, env->partialObs);
 }
 // n_iter consecutive fused steps (next_step, next_step + 1, ...) as ONE launch when the handle runs a
 // specialised full-observability self-play kernel and is in the steady fused state (the previous
@@ -1007,6 +1025,39 @@ struct RolloutEvents {
 };
 }  // namespace
 
+namespace {
+// a rollout call's span of the Responses ring (mrts_set_step_responses): the step launches write step k
+// of the call at ring step k (instead of d_reward / d_done: launch() points them at the ring), and
+// finish() copies the last step's entry into the caller's d_reward / d_done, which hold it as before
+struct RespScope {
+    mrts_env* env;
+    double* rew;
+    uint8_t* done;
+    RespScope(mrts_env* e, int32_t n_steps, double* d_reward, uint8_t* d_done) : env(e), rew(d_reward), done(d_done) {
+        if (!env->respRew) return;
+        if (n_steps > env->respMax) throw Fail{-EINVAL, "more steps than the Responses ring holds (mrts_set_step_responses)"};
+        env->respK = 0;
+    }
+    void finish(void* stream) {
+        if (env->respK <= 0 || !env->respRew) return;
+        const size_t n = (size_t)env->nSlots * env->hstatic.n_rewards, o = (size_t)(env->respK - 1) * n;
+        hipStream_t s = (hipStream_t)stream;
+        if (rew) HIPCHK(hipMemcpyAsync(rew, env->respRew + o, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        if (done) HIPCHK(hipMemcpyAsync(done, env->respDone + o, n, hipMemcpyDeviceToDevice, s));
+    }
+    ~RespScope() { env->respK = -1; }
+};
+}  // namespace
+
+int mrts_set_step_responses(mrts_env* env, double* d_rewards, uint8_t* d_dones, int32_t max_steps) {
+    if (!env) return fail(Fail{-EINVAL, "null handle"});
+    if (!d_rewards != !d_dones || (d_rewards && max_steps < 1)) return fail(Fail{-EINVAL, "both rings and max_steps >= 1, or both NULL"});
+    env->respRew = d_rewards;
+    env->respDone = d_dones;
+    env->respMax = d_rewards ? max_steps : 0;
+    return 0;
+}
+
 int mrts_set_rollout_events(mrts_env* env, void* start, void* end) {
     if (!env) return fail(Fail{-EINVAL, "null handle"});
     env->evStart = (hipEvent_t)start;
@@ -1020,6 +1071,7 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
         // the timing events ride on the launches: start with the first, end re-recorded by each (the last wins)
+        RespScope rs(env, n_steps, d_reward, d_done);
         hipEvent_t e0 = env->evStart, e1 = env->evEnd;
         env->evStart = env->evEnd = nullptr;
         if (n_steps == 0) {
@@ -1032,6 +1084,7 @@ int mrts_rollout_fused_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_p
                            first_next_step + (uint32_t)k, n, stream, e0, e1);
             e0 = nullptr;
         }
+        rs.finish(stream);
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1196,6 +1249,7 @@ int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     if (fused) {
         try {
+            RespScope rs(env, n_steps, d_reward, d_done);
             hipEvent_t e0 = env->evStart, e1 = env->evEnd;  // on the launches (see mrts_rollout_fused_dev)
             env->evStart = env->evEnd = nullptr;
             for (int32_t k = 0; k < n_steps;) {
@@ -1204,15 +1258,22 @@ int mrts_rollout_uniform_dev(mrts_env* env, int32_t* d_actions, const int32_t* d
                                  stream, e0, e1);
                 e0 = nullptr;
             }
+            rs.finish(stream);
             return 0;
         } catch (const Fail& f) {
             return fail(f);
         }
     }
-    for (int32_t k = 0; k < n_steps; k++) {
-        int r = mrts_policy_uniform_dev(env, seed, first_step + (uint32_t)k, d_actions, stream);
-        if (!r) r = mrts_step_dev(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, stream);
-        if (r) return r;
+    try {
+        RespScope rs(env, n_steps, d_reward, d_done);
+        for (int32_t k = 0; k < n_steps; k++) {
+            int r = mrts_policy_uniform_dev(env, seed, first_step + (uint32_t)k, d_actions, stream);
+            if (!r) r = mrts_step_dev(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, stream);
+            if (r) return r;
+        }
+        rs.finish(stream);
+    } catch (const Fail& f) {
+        return fail(f);
     }
     return 0;
 }
@@ -1248,14 +1309,28 @@ void ncclChk(ncclResult_t r, const char* what) {
 }
 bool exInited(const mrts_env* env) { return env->exComm != nullptr || env->exLoop; }
 // The all-gather of `bytes` per rank from send into recv ([ranks][bytes]) on the exchange stream.  The
-// loopback test transport (mrts_exchange_init_loopback) stands in for ranks - 1 peers that produced the
-// same bytes as this rank: send is copied to every rank's place — so a wrong rank offset, stride or
-// chunk base shows up on one GPU as a mismatch in some rank's place.
-void exAllGather(mrts_env* env, const void* send, void* recv, size_t bytes) {
+// loopback test transport (mrts_exchange_init_loopback) stands in for ranks - 1 peers whose data differ
+// from this rank's: the bytes are blocks of `rows` rows of `rowBytes` (a step's games, or
+// slots), and peer r's place receives this rank's blocks with the rows rotated by r - rank — peer r's row
+// i is this rank's row (i + r - rank) mod rows — while this rank's own place is left as written.  So a
+// wrong rank offset, stride or chunk base, or a render that reads another rank's place, shows on one GPU
+// as a rotated (wrong) observation, not as a copy of the right one.
+void exAllGather(mrts_env* env, const void* send, void* recv, size_t bytes, size_t rowBytes, size_t rows) {
     if (env->exLoop) {
+        const size_t blk = rowBytes * rows, nblk = blk ? bytes / blk : 0;
+        if (!blk || nblk * blk != bytes) throw Fail{-EINVAL, "loopback exchange: bytes are not whole blocks"};
         for (int r = 0; r < env->exRanks; r++) {
             uint8_t* dst = (uint8_t*)recv + (size_t)r * bytes;
-            if (dst != send) HIPCHK(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, env->exStream));
+            if (dst == send) continue;
+            const size_t d = (size_t)(((r - env->exRank) % (int)rows + (int)rows) % (int)rows);  // rotation in rows
+            const uint8_t* src = (const uint8_t*)send;
+            // dst rows [0, rows - d) <- src rows [d, rows); dst rows [rows - d, rows) <- src rows [0, d), every block
+            if (rows - d)
+                HIPCHK(hipMemcpy2DAsync(dst, blk, src + d * rowBytes, blk, (rows - d) * rowBytes, nblk, hipMemcpyDeviceToDevice,
+                                        env->exStream));
+            if (d)
+                HIPCHK(hipMemcpy2DAsync(dst + (rows - d) * rowBytes, blk, src, blk, d * rowBytes, nblk, hipMemcpyDeviceToDevice,
+                                        env->exStream));
         }
         return;
     }
@@ -1280,10 +1355,15 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t*
     const size_t bytes = (size_t)env->nSlots * env->C * env->HW * (u8 ? 1 : 2);
     bool pending[2] = {false, false};
     int16_t* const saved = env->obs16;
-    // a send buffer an earlier call's collective may still read (that call returned with the
-    // collectives enqueued on `stream` as it was then): wait for it here too, whatever the stream
+    // a send buffer an earlier call's collective may still read: that call ended with its own stream
+    // waiting for its collectives, so only a call on another stream waits for them here.  Not while
+    // capturing: the events were recorded outside the capture, so the graph could not hold
+    // that dependency — whoever replays a captured exchange orders it after the eager calls itself.
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cst));
+    const bool capturing = cst != hipStreamCaptureStatusNone;
     for (int b = 0; b < 2; b++)
-        if (env->exPending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
+        if (env->exPending[b] && !capturing && s != env->exLastStream) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
     try {
         for (int32_t k = 0; k < n_steps; k++) {
             const int b = k & 1;
@@ -1293,13 +1373,14 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t*
             step(k);
             HIPCHK(hipEventRecord(env->exReady[b], s));
             HIPCHK(hipStreamWaitEvent(env->exStream, env->exReady[b], 0));
-            exAllGather(env, send[b], d_recv, bytes);
+            exAllGather(env, send[b], d_recv, bytes, bytes / env->nSlots, env->nSlots);  // (loopback: rotate slots)
             HIPCHK(hipEventRecord(env->exDone[b], env->exStream));
             pending[b] = true;
-            env->exPending[b] = true;
+            if (!capturing) env->exPending[b] = true;  // (a captured record is the graph's, not an eager event)
         }
         for (int b = 0; b < 2; b++)  // the caller's stream covers every collective of the call
             if (pending[b]) HIPCHK(hipStreamWaitEvent(s, env->exDone[b], 0));
+        if (!capturing && n_steps > 0) env->exLastStream = s;
     } catch (...) {
         env->obs16 = saved;
         env->obs8 = nullptr;
@@ -1308,15 +1389,22 @@ void exchangeLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, int16_t*
     env->obs16 = saved;
     env->obs8 = nullptr;
 }
-// The compact-record exchange (mrts_rollout_*_records_dev): launches of up to recSteps steps write every
-// step's game records into the receive buffer at this rank's place of the launch's chunk; after each
-// launch, an in-place all-gather of that chunk on the exchange stream (it overlaps the next launch,
-// which writes the next chunk).  step(k, n, plan) enqueues up to n steps from step k and returns how
-// many it enqueued.
+// The compact-record exchange (mrts_rollout_*_records_dev): every step's game records go into the receive
+// buffer at this rank's place of its chunk; after each chunk, an in-place all-gather of it on the exchange
+// stream (it overlaps the next chunk's launch).  step(k, n, plan) enqueues up to n steps from step k and
+// returns how many it enqueued.  The chunk schedule depends on the call's arguments and the handle's
+// configuration only — never on whether this handle is in the steady fused state: a chunk
+// covers min(steps left, steps per launch) steps on every rank, and a handle that is not steady runs the
+// chunk's first step alone and the rest as a second launch into the same chunk, so every rank issues the
+// same all-gathers with the same sizes and the same step layout.
 template <class StepFn>
-void recordsLoop(mrts_env* env, int32_t n_steps, uint32_t* d_recv, int64_t* offsets, void* stream, StepFn step) {
+void recordsLoop(mrts_env* env, int32_t n_steps, const int32_t* d_obs, uint32_t* d_recv, int64_t* offsets, void* stream,
+                 StepFn step) {
     if (!exInited(env)) throw Fail{-EINVAL, "mrts_exchange_init first"};
     if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
+    // a partially observable record holds the views' snapshot, which the step takes as part of its
+    // observation write (an auto-reset's fresh snapshot too): without d_obs it would be empty
+    if (env->partialObs && !d_obs) throw Fail{-EINVAL, "partially observable records need an observation buffer (d_obs)"};
     if (!d_recv || ((uintptr_t)d_recv & 15)) throw Fail{-EINVAL, "the receive buffer must be non-null and 16-byte aligned"};
     // (partially observable records carry hp as int8: the kernel flags a value outside the record's range)
     if (!env->obsImg && !env->partialObs) throw Fail{-ENOTSUP, "records: an observation value no longer fits a byte"};
@@ -1325,14 +1413,18 @@ void recordsLoop(mrts_env* env, int32_t n_steps, uint32_t* d_recv, int64_t* offs
     const size_t per = (size_t)env->nGames * recWords(env->recUnits, env->partialObs);  // words per rank and step
     size_t base = 0;                                                   // words of d_recv filled so far
     bool any = false;
+    const int32_t cap = env->multiStep ? (env->recSteps > 0 ? env->recSteps : MRTS_MAX_ITER) : 1;
     for (int32_t k = 0; k < n_steps;) {
-        const int32_t cap = env->multiStep ? (env->recSteps > 0 ? env->recSteps : MRTS_MAX_ITER) : 1;
-        const RecPlan rp{d_recv + base, env->exRank};
-        const int32_t n = step(k, std::min<int32_t>(n_steps - k, cap), &rp);
+        const int32_t n = std::min<int32_t>(n_steps - k, cap);  // the chunk's steps, the same on every rank
+        for (int32_t j = 0; j < n;) {
+            const RecPlan rp{d_recv + base, env->exRank, n, j};
+            j += step(k + j, n - j, &rp);
+        }
         HIPCHK(hipEventRecord(env->exReady[0], s));
         HIPCHK(hipStreamWaitEvent(env->exStream, env->exReady[0], 0));
         const size_t words = (size_t)n * per;
-        exAllGather(env, d_recv + base + (size_t)env->exRank * words, d_recv + base, words * 4);
+        exAllGather(env, d_recv + base + (size_t)env->exRank * words, d_recv + base, words * 4,
+                    4 * (size_t)recWords(env->recUnits, env->partialObs), (size_t)env->nGames);  // (loopback: rotate games)
         if (offsets)
             for (int32_t j = 0; j < n; j++) {
                 offsets[2 * (size_t)(k + j)] = (int64_t)(base + (size_t)j * per);
@@ -1379,11 +1471,13 @@ int mrts_rollout_fused_records_dev(mrts_env* env, int32_t* d_actions, const int3
                                    void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
+        RespScope rs(env, n_steps, d_reward, d_done);
         RolloutEvents ev(env, stream);
-        recordsLoop(env, n_steps, d_recv, step_offsets, stream, [&](int32_t k, int32_t n, const RecPlan* rp) {
+        recordsLoop(env, n_steps, d_obs, d_recv, step_offsets, stream, [&](int32_t k, int32_t n, const RecPlan* rp) {
             return stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
                              first_next_step + (uint32_t)k, n, stream, nullptr, nullptr, rp);
         });
+        rs.finish(stream);
         ev.done();
         return 0;
     } catch (const Fail& f) {
@@ -1396,13 +1490,30 @@ int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const in
                                      uint32_t* d_recv, int64_t* step_offsets, void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
+        RespScope rs(env, n_steps, d_reward, d_done);
         RolloutEvents ev(env, stream);
-        recordsLoop(env, n_steps, d_recv, step_offsets, stream, [&](int32_t k, int32_t n, const RecPlan* rp) {
+        recordsLoop(env, n_steps, d_obs, d_recv, step_offsets, stream, [&](int32_t k, int32_t n, const RecPlan* rp) {
             return stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, n,
                                stream, nullptr, nullptr, rp);
         });
+        rs.finish(stream);
         ev.done();
         return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_render_status(mrts_env* env) {
+    try {
+        if (!env) throw Fail{-EINVAL, "null handle"};
+        if (!env->d_renderErr) return 0;
+        HIPCHK(hipSetDevice(env->device));
+        HIPCHK(hipDeviceSynchronize());
+        int32_t v = 0;
+        HIPCHK(hipMemcpy(&v, env->d_renderErr, 4, hipMemcpyDeviceToHost));
+        if (v) HIPCHK(hipMemset(env->d_renderErr, 0, 4));
+        return v ? 1 : 0;
     } catch (const Fail& f) {
         return fail(f);
     }
@@ -1421,8 +1532,12 @@ int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_rank
         if (out_bytes != 1 && out_bytes != 4) throw Fail{-EINVAL, "out_bytes: 1 (uint8) or 4 (int32)"};
         if (((uintptr_t)d_out & (out_bytes == 4 ? 15 : 3)) || ((uintptr_t)d_rec & 3)) throw Fail{-EINVAL, "misaligned buffer"};
         HIPCHK(hipSetDevice(env->device));
+        if (!env->d_renderErr) {
+            HIPCHK(hipMalloc(&env->d_renderErr, 4));
+            HIPCHK(hipMemset(env->d_renderErr, 0, 4));
+        }
         HIPCHK(launchRenderRecords(env->hstatic, env->d_static, d_rec, env->recUnits, n_ranks, rank_stride, d_out, out_bytes,
-                                   pickStream(env, stream)));
+                                   env->d_renderErr, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1527,11 +1642,13 @@ int mrts_rollout_fused_exchange_dev(mrts_env* env, int32_t* d_actions, const int
                                     int16_t* d_recv, void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
+        RespScope rs(env, n_steps, d_reward, d_done);
         RolloutEvents ev(env, stream);
         exchangeLoop(env, n_steps, d_obs, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
             stepFused(env, d_actions, d_players, d_obs, d_reward, d_done, d_masks, mask_player, seed,
                       first_next_step + (uint32_t)k, 1, stream);
         });
+        rs.finish(stream);
         ev.done();
         return 0;
     } catch (const Fail& f) {
@@ -1544,11 +1661,13 @@ int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const i
                                       int16_t* d_send0, int16_t* d_send1, int16_t* d_recv, void* stream) {
     if (!env || n_steps < 0) return fail(Fail{-EINVAL, "bad rollout arguments"});
     try {
+        RespScope rs(env, n_steps, d_reward, d_done);
         RolloutEvents ev(env, stream);
         exchangeLoop(env, n_steps, d_obs, d_send0, d_send1, d_recv, stream, [&](int32_t k) {
             stepUniform(env, d_actions, d_players, d_obs, d_reward, d_done, nullptr, 0, seed, first_step + (uint32_t)k, 1,
                         stream);
         });
+        rs.finish(stream);
         ev.done();
         return 0;
     } catch (const Fail& f) {
@@ -1873,6 +1992,7 @@ void mrts_destroy(mrts_env* env) {
     (void)hipFree(env->d_static);
     (void)hipFree(env->d_poPrev);
     (void)hipFree(env->d_prioTab);
+    (void)hipFree(env->d_renderErr);
     (void)hipFree(env->d_bal);
     (void)hipFree(env->d_state);
     (void)hipFree(env->d_polPrev);

@@ -191,6 +191,10 @@ struct KDyn {
     // words (writeRecord in mrts_kernels.hip); null = off
     uint32_t* rec_out;
     int32_t rec_units;
+    // every step's Responses (mrts_set_step_responses): `reward` / `done` then point at this launch's first
+    // step in the call's ring and iteration it writes its reward / done [n_slots][n_rewards] at
+    // + it * resp_stride (= n_slots * n_rewards); 0 = every iteration writes the same buffers
+    int32_t resp_stride;
 };
 // compact observation record of one game, word 0 = units n (<= rec_units) | overflow << 31, then per unit
 // in list order:

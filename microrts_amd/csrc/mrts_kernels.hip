@@ -171,12 +171,16 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_HELPER_PRIO
 #define MRTS_HELPER_PRIO 0
 #endif
-// 1: partially observable multi-step launches without the render helper wave.  The default since the
-// round-4 full-size soak (tests/soak_full_parity.py): with the helper, 2 of 2048 c5 games showed one stale
-// observation value for a unit that died in the observed step (the helper's packed delta render); every
-// game is bit-exact without it.  0 = the helper build (kept for the fix and its A/B).
+// 1: partially observable multi-step launches without the render helper wave (A/B builds only).  Round 4
+// had made it the default after its full-size soak found 2 of 2048 c5 games with one stale observation value
+// for a unit that died in the observed step; round 5 found the cause (the renders read the dead unit's
+// fields by readlane inside their divergent chunk loop, from a lane that was off there — writeObsPOFast)
+// and the helper is back on.
+#ifndef MRTS_RESP_RING  // the per-step Responses ring (mrts_set_step_responses); 0 = A/B builds without it
+#define MRTS_RESP_RING 1
+#endif
 #ifndef MRTS_NO_PO_HELPER
-#define MRTS_NO_PO_HELPER 1
+#define MRTS_NO_PO_HELPER 0
 #endif
 // issue-priority thresholds on a game's unit count (k_env): 1 / 2 / 3 from T1 / T2 / T3 units
 // (units + own idle units; measured against units alone at 24 / 30 / 36: c3 +1.8 % at K = 200,
@@ -1369,7 +1373,8 @@ struct Game {
                 bool conf = up && ((bits[tpos >> 5] >> (tpos & 31)) & 1u);
                 for (uint64_t mm = ballot(up); mm; mm &= mm - 1) {
                     const int k = __builtin_ctzll(mm);
-                    if (up && k != l && rl(tpos, k) == tpos) conf = true;
+                    const int tk = rl(tpos, k);  // read in uniform flow: lane k itself is off inside the test below
+                    if (up && k != l && tk == tpos) conf = true;
                 }
                 const int sumc = ballot(cand && cost > 0) ? wave_sum(cand ? cost : 0) : 0;
                 if (!ballot(conf) && runP + sumc <= presP) {
@@ -1714,7 +1719,8 @@ struct Game {
             if (act && (ua[s] & UA_PRESENT)) conf = true;
             for (uint64_t mm = ballot(act); mm; mm &= mm - 1) {
                 const int k = __builtin_ctzll(mm);
-                if (act && rl(s, k) == s && rl(rank, k) < rank) conf = true;
+                const int sk = rl(s, k), rk = rl(rank, k);  // uniform flow (no readlane under a lane test)
+                if (act && sk == s && rk < rank) conf = true;
             }
         }
         int ntgt = 0, ncost = 0, pl = 0;
@@ -2515,7 +2521,8 @@ struct Game {
     // ProduceWorkerRewardFunction.java:20-30 (the other two: the same lines of their files); Attack:
     // AttackRewardFunction.java:20-36 (a legal attack always targets a minplayer unit of the pre-cycle
     // pgs).  Constants are float 1.
-    DEV bool writeRewards(int slot0, int nslots, int pl0, int pl1, bool gameover, int winner) {
+    // it: this launch's iteration (the step's place in the Responses ring, KDyn.resp_reward)
+    DEV bool writeRewards(int slot0, int nslots, int pl0, int pl1, bool gameover, int winner, int it = 0) {
         const int R = D.n_rewards;
         int newSq0 = INF, newSq1 = INF;
         if (MRTS_UNLIKELY(D.reward_need & RN_CLOSER)) closerMin(newSq0, newSq1);
@@ -2526,13 +2533,16 @@ struct Game {
                 resLeft |= ballot(o < nu && !(uc[o] & UC_DEAD) && (U.flags[utyp(uc[o])] & N_RESOURCE) && res[o] > 0) != 0;
             }
         const int k0 = (int)(D.reward_kinds4 & 15u);
+        // the Responses ring (mrts_set_step_responses): reward / done point at the call's ring and each
+        // iteration writes its own step there (resp_stride = n_slots * n_rewards; 0 = the plain buffers)
+        const size_t ro = MRTS_RESP_RING ? (size_t)it * (uint32_t)D.resp_stride : 0;
         const bool done0 = k0 == RF_WINLOSS ? gameover : (k0 == RF_RESOURCE_GATHER ? !resLeft : false);
         const int L = lid();
         if (R == 1 && k0 == RF_WINLOSS) {  // WinLoss alone (the common case): a wave-uniform branch, no switch
             if (L < nslots) {
                 const int p = L ? pl1 : pl0;
-                if (D.reward) D.reward[slot0 + L] = gameover ? (winner == p ? 1.0 : -1.0) : 0.0;
-                if (D.done) D.done[slot0 + L] = gameover ? 1 : 0;
+                if (D.reward) D.reward[ro + slot0 + L] = gameover ? (winner == p ? 1.0 : -1.0) : 0.0;
+                if (D.done) D.done[ro + slot0 + L] = gameover ? 1 : 0;
             }
             return done0;
         }
@@ -2561,8 +2571,8 @@ struct Game {
                         r = closerDist(hdr[HX_OLDSQ + p]) - closerDist(p == 0 ? newSq0 : newSq1);
                     break;
             }
-            if (D.reward) D.reward[(size_t)(slot0 + i) * R + j] = r;
-            if (D.done) D.done[(size_t)(slot0 + i) * R + j] = d ? 1 : 0;
+            if (D.reward) D.reward[ro + (size_t)(slot0 + i) * R + j] = r;
+            if (D.done) D.done[ro + (size_t)(slot0 + i) * R + j] = d ? 1 : 0;
         }
         return done0;
     }
@@ -3021,10 +3031,14 @@ struct Game {
             for (int j = 0; j < 4; j++) sl[j] = (cs[j] < CAP && snap_in(osb[j], p)) ? cs[j] : -1;
             for (uint64_t m = deadM; m; m &= m - 1) {  // the view's dead units: a later list position wins
                 const int ds = __builtin_ctzll(m);
-                const uint32_t dcu = uniu((uint32_t)rl((int)cu, ds));
+                // the dead unit's fields from LDS, never by readlane: this loop is divergent (lanes >= n
+                // are off), and the compiler may recompute a lane's cu / hp / snapshot byte inside it for
+                // the active lanes only, so a readlane of an inactive lane returns a stale register
+                // (round 5: the c5 helper's stale-value case)
+                const uint32_t dcu = uc[ds];
                 const int dcell = uy(dcu) * W + ux(dcu);
-                const int dh = rl(hv, ds), dr = rl(rv, ds);
-                const uint32_t dsb = uniu((uint32_t)rl((int)sb, ds));
+                const int dh = hp[ds], dr = res[ds];
+                const uint32_t dsb = snap[ds];
 #pragma unroll
                 for (int j = 0; j < 4; j++)
                     if (dcell == 4 * c4 + j && ds > sl[j]) {
@@ -3223,10 +3237,11 @@ struct Game {
             for (int j = 0; j < 4; j++) sl[j] = (cs[j] < CAP && snap_in(osb[j], v)) ? cs[j] : -1;
             for (uint64_t m = deadAny; m; m &= m - 1) {  // the view's dead units: a later list position wins
                 const int ds = __builtin_ctzll(m);
-                const uint32_t dcu = uniu((uint32_t)rl((int)cu, ds));
+                // from LDS, not by readlane of an inactive lane (writeObsPOFast)
+                const uint32_t dcu = uc[ds];
                 const int dcell = uy(dcu) * W + ux(dcu);
-                const int dh = rl(hv, ds), dr = rl(rv, ds);
-                const uint32_t dsb = uniu((uint32_t)rl((int)sb, ds));
+                const int dh = hp[ds], dr = res[ds];
+                const uint32_t dsb = snap[ds];
                 const bool mine = (deadM >> ds) & 1ull;
 #pragma unroll
                 for (int j = 0; j < 4; j++)
@@ -3523,10 +3538,13 @@ struct Game {
             for (int j = 0; j < 4; j++) sl[j] = (cs[j] < CAP && snap_in(osb[j], v)) ? cs[j] : -1;
             for (uint64_t m = deadAny; m; m &= m - 1) {  // the view's dead units: a later list position wins
                 const int ds = __builtin_ctzll(m);
-                const uint32_t dcu = uniu((uint32_t)rl((int)cu, ds));
+                // from the pack, not by readlane of an inactive lane (writeObsPOFast): the compiler sank
+                // this wave's pack reads (cu, hp | res, snapshot byte) into the divergent item loop, so
+                // lane ds's registers held a stale value whenever lane ds had no item (round 4's soak case)
+                const uint32_t dcu = pk[ds], dkv = pk[64 + ds];
                 const int dcell = uy(dcu) * W + ux(dcu);
-                const int dh = rl(hv, ds), dr = rl(rv, ds);
-                const uint32_t dsb = uniu((uint32_t)rl((int)sb, ds));
+                const int dh = (int)(int16_t)(dkv & 0xFFFFu), dr = (int)(int16_t)(dkv >> 16);
+                const uint32_t dsb = pk[128 + ds] & 0xFFu;
                 const bool mine = (deadM >> ds) & 1ull;
 #pragma unroll
                 for (int j = 0; j < 4; j++)
@@ -4958,9 +4976,10 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
         // reward/done and forcing done[0] (tests/JNIGridnetVecClient.java:214-287)
         const int steps = G.hget(H_STEPS) + 1;
         G.hset(H_STEPS, steps);
-        const bool done0 = G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner);
+        const bool done0 = G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner, it);
         const bool reset = done0 || steps >= D.max_steps;
-        if (reset && D.done && lane_id() < nslots) D.done[(size_t)(slot0 + lane_id()) * D.n_rewards] = 1;
+        if (reset && D.done && lane_id() < nslots)
+            D.done[(MRTS_RESP_RING ? (size_t)it * (uint32_t)D.resp_stride : 0) + (size_t)(slot0 + lane_id()) * D.n_rewards] = 1;
         if (MRTS_UNLIKELY(reset)) {
             G.hset(H_STEPS, 0);  // envSteps[i] = 0 (JNIGridnetVecClient.java:229,264-265,285)
             G.resetFromTemplate();
@@ -5442,8 +5461,11 @@ hipError_t launchWiden(const uint8_t* in, int32_t* out, size_t n, hipStream_t st
 // holds the same maps per game index).  out = [n_ranks][2 * n_games][C][HW] as uint8 (out_bytes 1)
 // or int32 (4).  One wave per game: the units paint a byte image in LDS, then each lane stores 4 cells
 // per plane.  HW <= 256, HW % 4 == 0 (the host checks).
+// A record whose overflow bit is set (its game had more units than the record holds) renders without
+// the missing units: the kernel then sets *err (mrts_render_status reports it).
 __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict__ PS, const uint32_t* __restrict__ rec,
-                                                       int units, int64_t rank_stride, void* __restrict__ out, int out_bytes) {
+                                                       int units, int64_t rank_stride, void* __restrict__ out, int out_bytes,
+                                                       int32_t* __restrict__ err) {
     __shared__ uint32_t imgw[5 * 256 / 4];
     uint8_t* img = (uint8_t*)imgw;
     const KStatic& P = *PS;
@@ -5451,6 +5473,7 @@ __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict
     const uint32_t* rc = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units, false);
     for (int i = l; i < 5 * HW / 4; i += 64) imgw[i] = 0u;
     const uint32_t hdr = rc[0];
+    if (l == 0 && (hdr >> 31)) *err = 1;  // a vector store from one lane (rare)
     __syncthreads();
     const int n = min((int)(hdr & 0xFFFFu), units);
     for (int i = l; i < n; i += 64) {
@@ -5510,7 +5533,8 @@ __global__ __launch_bounds__(64) void k_render_records(const KStatic* __restrict
 // (2 views x 2 x H x (W + 31) / 32 words) and the record itself (the per-cell lookups stay on chip).
 // HW % 4 == 0 (the host checks).
 __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __restrict__ PS, const uint32_t* __restrict__ rec,
-                                                           int units, int64_t rank_stride, void* __restrict__ out, int out_bytes) {
+                                                           int units, int64_t rank_stride, void* __restrict__ out, int out_bytes,
+                                                           int32_t* __restrict__ err) {
     extern __shared__ __align__(16) uint32_t lds[];
     const KStatic& P = *PS;
     const int g = (int)blockIdx.x, r = (int)blockIdx.y, t = (int)threadIdx.x;
@@ -5520,6 +5544,7 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
     uint32_t* const rc = rows + 4 * NR;   // the record (1 + 2 x units words)
     const uint32_t* rg = rec + (size_t)r * (size_t)rank_stride + (size_t)g * recWords(units, true);
     const int n = min((int)(rg[0] & 0xFFFFu), units);
+    if (t == 0 && (rg[0] >> 31)) *err = 1;  // overflow: units or an hp / resource value missing
     for (int i = t; i < 2 * HW + 4 * NR; i += 256) lds[i] = 0u;
     for (int i = t; i < 1 + 2 * n; i += 256) rc[i] = rg[i];
     __syncthreads();
@@ -5599,14 +5624,14 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
     }
 }
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
-                               int64_t rank_stride, void* out, int out_bytes, hipStream_t stream) {
+                               int64_t rank_stride, void* out, int out_bytes, int32_t* err, hipStream_t stream) {
     if (hs.partial_obs) {
         const size_t lds = 4 * (size_t)(2 * hs.HW + 4 * hs.H * ((hs.W + 31) / 32) + recWords(units, true));
         hipLaunchKernelGGL(k_render_records_po, dim3((unsigned)hs.n_games, (unsigned)n_ranks), dim3(256), lds, stream, ds, rec,
-                           units, rank_stride, out, out_bytes);
+                           units, rank_stride, out, out_bytes, err);
     } else {
         hipLaunchKernelGGL(k_render_records, dim3((unsigned)hs.n_games, (unsigned)n_ranks), dim3(64), 0, stream, ds, rec, units,
-                           rank_stride, out, out_bytes);
+                           rank_stride, out, out_bytes, err);
     }
     return hipGetLastError();
 }

@@ -264,3 +264,12 @@ class RecordExchange:
         """All ranks' observations of step `step` of the last rollout into out [world * slots, C, H, W]."""
         off, stride = offsets[step]
         return self.env.render_records(self.recv, int(off), int(stride), self.world, out)
+
+    def check(self):
+        """Raise if a rendered record was truncated (a sender's game held more units than a record, or a
+        value outside its range: mrts_render_status) or one of this rank's games overflowed its record
+        (MRTS_ERR_RECORD).  Synchronises; call it at a point where the learner may wait."""
+        if self.env.render_overflow():
+            raise RuntimeError("a rendered observation record overflowed (units missing): raise units_per_record")
+        if (self.env.error_flags() & (1 << 6)).any():
+            raise RuntimeError("a game of this rank overflowed its observation record (MRTS_ERR_RECORD)")

@@ -387,6 +387,8 @@ class DeviceVecEnv:
         if self.source is not None:
             _lib.check(h.L.mrts_set_source_output(h.h, self._p(self.source)))
         self.mask_player = 0
+        self.partial_obs = bool(partial_obs)
+        self.step_rewards = self.step_dones = None
         self._policy_out, self._policy_version = None, -1
         _lib.check(h.L.mrts_set_obs_delta(h.h, int(bool(obs_delta))))
         self._obs_version = -1
@@ -614,10 +616,36 @@ class DeviceVecEnv:
         mrts_render_records_dev."""
         h = self._h
         ob = out.element_size()
-        assert ob in (1, 4) and out.is_contiguous() and out.numel() == n_ranks * self.obs.numel()
+        T = self.torch
+        # a partially observable view shows a dead unit's hp (<= 0): int8, never uint8 (ADVICE r4)
+        ok = (T.int8, T.int32) if self.partial_obs else (T.uint8, T.int32)
+        assert out.dtype in ok, f"render_records: out must be one of {ok}, not {out.dtype}"
+        assert out.is_contiguous() and out.numel() == n_ranks * self.obs.numel()
         ptr = ctypes.c_void_p(recv.data_ptr() + 4 * int(offset))
         _lib.check(h.L.mrts_render_records_dev(h.h, ptr, int(n_ranks), int(rank_stride), self._p(out), ob, self._s(stream)))
         return out
+
+    def render_overflow(self):
+        """True if a record rendered since the last call had its overflow bit set (units missing from the
+        rendered observation; the sender flagged MRTS_ERR_RECORD) — mrts_render_status, synchronises."""
+        r = self._h.L.mrts_render_status(self._h.h)
+        if r < 0:
+            _lib.check(r)
+        return bool(r)
+
+    def set_step_responses(self, max_steps):
+        """Every step's reward / done from each rollout call of at most max_steps steps
+        (mrts_set_step_responses; Java's gameStep returns them on every call): step k of the next call
+        lands in self.step_rewards[k] / self.step_dones[k] ([slots] or [slots][R], as reward / done).
+        0 turns it off."""
+        h, T = self._h, self.torch
+        if not max_steps:
+            _lib.check(h.L.mrts_set_step_responses(h.h, None, None, 0))
+            self.step_rewards = self.step_dones = None
+            return
+        self.step_rewards = T.zeros((max_steps,) + tuple(self.reward.shape), dtype=T.float64, device=self.device)
+        self.step_dones = T.zeros((max_steps,) + tuple(self.done.shape), dtype=T.uint8, device=self.device)
+        _lib.check(h.L.mrts_set_step_responses(h.h, self._p(self.step_rewards), self._p(self.step_dones), int(max_steps)))
 
     def step_rows(self, rows, stream=None):
         """gameStep with Java rows: int32 [slots][n_rows][8] on this device (any order, duplicates ok)."""

@@ -933,6 +933,37 @@ int oref_trace_dumps(const char* map_path, const char* fixture, int32_t* buf, in
     return n;
 }
 
+// n_steps of the benchmark's rollout on every slot of handle h, in native code (the full-size parity
+// tests run one handle per shard of games on its own Python thread: ctypes drops the GIL here).
+// Step t = step0 + k: uniform = 0 — getMasks(0) (JNIGridnetVecClient.java:307-316), then each slot's
+// masked-uniform row from its own masks (oref_policy, env id slot_base + s, player 0: the GPU's fused
+// policy); uniform = 1 — oref_policy_uniform rows (slot id slot_base + s); then gameStep (:213-297).
+// The last step's responses go to obs / reward / done (each may be null).
+int oref_rollout_policy(void* h, int n_steps, int uniform, int n_types, uint64_t seed, uint32_t slot_base, uint32_t step0,
+                        int32_t* obs, double* reward, uint8_t* done) {
+    try {
+        auto v = (VecClient*)h;
+        const int S = v->nSlots(), HW = v->world->H * v->world->W, K = v->world->K;
+        std::vector<uint8_t> masks(uniform ? 0 : (size_t)S * HW * K);
+        std::vector<int32_t> acts((size_t)S * HW * 7);
+        for (int k = 0; k < n_steps; k++) {
+            const uint32_t t = step0 + (uint32_t)k;
+            if (!uniform) v->masks(0, masks.data());
+            for (int s = 0; s < S; s++) {
+                int32_t* a = acts.data() + (size_t)s * HW * 7;
+                if (uniform) oref_policy_uniform(HW, K, n_types, seed, slot_base + (uint32_t)s, t, a);
+                else oref_policy(masks.data() + (size_t)s * HW * K, HW, K, n_types, seed, slot_base + (uint32_t)s, t, 0, a);
+            }
+            v->step(acts.data(), nullptr);
+        }
+        v->collect(obs, reward, done);
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -22;
+    }
+}
+
 // ------------------------------------------------ CPU baseline: VecClient + random policy,
 // `threads` std::threads each stepping a disjoint shard of games (cores = threads).
 // Returns env-steps executed; *seconds = wall time of the timed region.

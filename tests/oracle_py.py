@@ -73,6 +73,7 @@ def load():
         L.oref_bench_bots.restype = ctypes.c_double
         L.oref_bench_bots.argtypes = [ctypes.c_char_p, I, ctypes.c_int64, I]
         L.oref_policy_uniform.argtypes = [I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, P]
+        L.oref_rollout_policy.argtypes = [P, I, I, I, U64, ctypes.c_uint32, ctypes.c_uint32, P, P, P]
         _lib = L
     return _lib
 
@@ -150,6 +151,13 @@ class OracleVecClient:
         self._chk(self.L.oref_step_rows(self.h, _ptr(r), r.shape[1], _ptr(p), _ptr(self.obs), _ptr(self.reward),
                                         _ptr(self.done)))
         return self.obs.copy(), self.reward.copy(), self.done.copy()
+
+    def rollout_policy(self, n_steps, seed, slot_base, step0, uniform=False, n_types=7):
+        """n_steps gameSteps in native code with the GPU benchmark's own policy streams: the masked-uniform
+        rows of each slot from its own masks (slot id slot_base + s, player 0), or the unmasked uniform
+        rows; obs / reward / done then hold the last step's responses.  Releases the GIL while it runs."""
+        self._chk(self.L.oref_rollout_policy(self.h, n_steps, int(uniform), n_types, seed, slot_base, step0, _ptr(self.obs),
+                                             _ptr(self.reward), _ptr(self.done)))
 
     def get_masks(self, player=0):
         m = np.zeros((self.S, self.H, self.W, self.K), np.uint8)

@@ -459,11 +459,12 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
             e.random_policy(SEED, 0)
     _exchange_env(B)
     words = B.set_records(64, spl)
+    B.set_step_responses(100)  # every step's reward / done
     S = n_sp
     k = 0
     dead_seen = False
     for n in (1, 40, 25) + ((100, 100) if po == "dead" else ()):
-        want = []
+        want, wantR, wantD = [], [], []
         for j in range(n):
             if uniform:
                 A.rollout_uniform(SEED, k + j, 1)
@@ -471,6 +472,8 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
                 A.rollout_fused(SEED, k + j + 1, 1)
             A.synchronize()
             want.append(A.obs.clone())
+            wantR.append(A.reward.clone())
+            wantD.append(A.done.clone())
             if po:
                 dead_seen |= bool(((want[-1][:, 0] <= 0) & (want[-1][:, 3] > 0)).any())
         recv = B.records_buffer(n)
@@ -486,6 +489,8 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
             B.synchronize()
             assert torch.equal(got, want[j]), f"step {k - n + j}: rendered int32 observation"
             assert torch.equal(g8.to(torch.int32), want[j]), f"step {k - n + j}: rendered byte observation"
+            assert torch.equal(B.step_rewards[j], wantR[j]), f"step {k - n + j}: the Responses ring's reward"
+            assert torch.equal(B.step_dones[j], wantD[j]), f"step {k - n + j}: the Responses ring's done"
         for name in ("obs", "reward", "done", "actions") + (() if uniform else ("masks",)):
             assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
         for s in range(0, n_sp, 2):
@@ -507,16 +512,75 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
         e.close()
 
 
+def test_step_responses_every_reward_function():
+    """mrts_set_step_responses with all 8 reward functions (reward / done [slots][8]) and
+    both rollout forms the benchmark shapes run as multi-step launches (c3's masked fused rollout, c2's
+    uniform one): every step's ring entry equals the reward / done a twin returns from one launch per step,
+    across auto-resets (max_steps 60 and gameovers); d_reward / d_done keep the last step's; a call longer
+    than the ring is refused; NULL turns it off."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+    from microrts_amd._lib import REWARD_FUNCTIONS
+
+    rfs = list(REWARD_FUNCTIONS)
+    for mp, uniform in (("maps/16x16/basesWorkers16x16.xml", False), ("maps/8x8/basesWorkers8x8.xml", True)):
+        n_sp = 32
+        A = DeviceVecEnv(n_sp, 0, 60, [mp] * n_sp, seed=31, rfs=rfs, with_masks=not uniform)
+        B = DeviceVecEnv(n_sp, 0, 60, [mp] * n_sp, seed=31, rfs=rfs, with_masks=not uniform)
+        A.set_multi_step(False)
+        for e in (A, B):
+            e.reset()
+            if not uniform:
+                e.random_policy(SEED, 0)
+        B.set_step_responses(150)
+        k = 0
+        saw_done = False
+        for n in (1, 150, 37):
+            wantR, wantD = [], []
+            for j in range(n):
+                if uniform:
+                    A.rollout_uniform(SEED, k + j, 1)
+                else:
+                    A.rollout_fused(SEED, k + j + 1, 1)
+                A.synchronize()
+                wantR.append(A.reward.clone())
+                wantD.append(A.done.clone())
+            if uniform:
+                B.rollout_uniform(SEED, k, n)
+            else:
+                B.rollout_fused(SEED, k + 1, n)
+            k += n
+            B.synchronize()
+            for j in range(n):
+                assert torch.equal(B.step_rewards[j], wantR[j]), f"{mp}: step {k - n + j} reward"
+                assert torch.equal(B.step_dones[j], wantD[j]), f"{mp}: step {k - n + j} done"
+                saw_done |= bool(wantD[j][:, 0].any())
+            for name in ("obs", "reward", "done", "actions"):
+                assert torch.equal(getattr(A, name), getattr(B, name)), f"{mp}: {name} after {k}"
+        assert saw_done, "no auto-reset inside the checked steps"
+        with pytest.raises(RuntimeError):
+            B.rollout_uniform(SEED, k, 151) if uniform else B.rollout_fused(SEED, k + 1, 151)
+        B.set_step_responses(0)
+        for e in (A, B):
+            assert not e.error_flags().any()
+            e.close()
+
+
 @pytest.mark.parametrize("mp,po,spl,world,rank", [("maps/16x16/basesWorkers16x16.xml", False, 0, 8, 3),
                                                   ("maps/16x16/basesWorkers16x16.xml", False, 7, 8, 7),
                                                   ("maps/BWDistantResources32x32.xml", True, 9, 4, 1)])
 def test_record_exchange_loopback_ranks(mp, po, spl, world, rank):
     """The records exchange's multi-rank layout on one GPU (mrts_exchange_init_loopback: rank `rank` of
-    `world`, every all-gather copies this rank's records into every rank's place, as if the peers had
-    produced the same games).  Every step's chunk: this rank's records sit at offset + rank x stride and
-    every rank's place holds the same words; rendering all `world` ranks gives `world` copies of the
-    twin's int32 observation of that step — a wrong rank offset, stride or chunk base fails here, where
-    RCCL cannot put two ranks on one device.  The tensor exchange's [ranks][...] receive buffer too."""
+    `world`; peer r's place receives this rank's records with the games rotated by r - rank, so every
+    rank's data differ — VERDICT r4 #4).  Every step's chunk: this rank's records sit unrotated at
+    offset + rank x stride (the in-place all-gather's send = recv + rank x bytes) and peer r's place holds
+    them rotated by r - rank games; rendering all `world` ranks gives, for rank r, the twin's int32
+    observation with its slots rotated by 2 (r - rank) — a wrong rank offset, stride or chunk base, or a
+    render that reads another rank's place, fails here (shown below by rendering a neighbour's place as
+    this rank's), where RCCL cannot put two ranks on one device.  The tensor exchange's [ranks][...]
+    receive buffer too (rotated by slots).  And the chunk schedule does not depend on whether a handle is
+    in the steady fused state: a twin made unsteady by a get_masks call reports the same
+    per-step offsets."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
 
@@ -524,15 +588,18 @@ def test_record_exchange_loopback_ranks(mp, po, spl, world, rank):
     kw = dict(partial_obs=True, max_units=256) if po else {}
     A = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=29, **kw)
     B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=29, **kw)
+    C = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=29, **kw)  # B's twin, never in the steady state at a call
     A.set_multi_step(False)
-    for e in (A, B):
+    for e in (A, B, C):
         e.reset()
         e.random_policy(SEED, 0)
     L, h = B._h.L, B._h.h
     assert L.mrts_exchange_init_loopback(h, world, world) != 0  # rank out of range
     assert L.mrts_exchange_init_loopback(h, world, rank) == 0
     assert L.mrts_exchange_init_loopback(h, world, rank) != 0  # already initialised
+    assert L.mrts_exchange_init_loopback(C._h.h, world, rank) == 0
     words = B.set_records(64, spl)
+    assert C.set_records(64, spl) == words
     G = n_sp // 2
     k = 0
     for n in (1, 40, 25):
@@ -544,20 +611,35 @@ def test_record_exchange_loopback_ranks(mp, po, spl, world, rank):
         recv = B.records_buffer(n, world)
         recv.fill_(-7)  # every record header the exchange owes must be written (unit words past n are don't-care)
         off = B.rollout_fused_records(SEED, k + 1, n, recv)
+        C.get_masks()  # C leaves the steady fused state: its first launch of the call runs one step alone
+        recvC = C.records_buffer(n, world)
+        recvC.fill_(-7)  # (as recv: unit words past a record's n stay as they were)
+        offC = C.rollout_fused_records(SEED, k + 1, n, recvC)
+        assert np.array_equal(off, offC), "the chunk schedule must not depend on the steady state"
         k += n
         B.synchronize()
+        C.synchronize()
+        assert torch.equal(recv, recvC)
         for j in range(n):
             o, stride = int(off[j, 0]), int(off[j, 1])
             assert stride >= G * words and (o + (world - 1) * stride + G * words) <= recv.numel()
             mine = recv[o + rank * stride:o + rank * stride + G * words]
             assert not bool((mine.view(G, words)[:, 0] == -7).any()), f"step {k - n + j}: a record header never written"
-            for r in range(world):
-                assert torch.equal(recv[o + r * stride:o + r * stride + G * words], mine), f"step {k - n + j}: rank {r}"
+            for r in range(world):  # peer r: this rank's game (g + r - rank) mod G at its game g
+                peer = recv[o + r * stride:o + r * stride + G * words].view(G, words)
+                assert torch.equal(peer, torch.roll(mine.view(G, words), -(r - rank), 0)), f"step {k - n + j}: rank {r}"
             out = torch.zeros((world * 2 * G,) + tuple(B.obs.shape[1:]), dtype=torch.int32, device=B.device)
             B.render_records(recv, o, stride, world, out)
             B.synchronize()
             for r in range(world):
-                assert torch.equal(out[r * 2 * G:(r + 1) * 2 * G], want[j]), f"step {k - n + j}: rendered rank {r}"
+                assert torch.equal(out[r * 2 * G:(r + 1) * 2 * G], torch.roll(want[j], -2 * (r - rank), 0)), \
+                    f"step {k - n + j}: rendered rank {r}"
+            # the check can fail: the neighbour's place rendered as this rank's is not this rank's observation
+            nb = (rank + 1) % world
+            wrong = torch.zeros_like(B.obs)
+            B.render_records(recv, o + nb * stride, stride, 1, wrong)
+            B.synchronize()
+            assert not torch.equal(wrong, want[j]), f"step {k - n + j}: a neighbour's place renders like this rank's"
         assert torch.equal(A.obs, B.obs) and torch.equal(A.masks, B.masks)
     if not po:  # the per-step tensor exchange: [ranks][slots][C][H][W]
         send = [torch.zeros(tuple(B.obs.shape), dtype=torch.int16, device=B.device) for _ in range(2)]
@@ -566,8 +648,8 @@ def test_record_exchange_loopback_ranks(mp, po, spl, world, rank):
         B.rollout_fused_exchange(SEED, k + 1, 3, send, tr)
         A.synchronize()
         B.synchronize()
-        for r in range(world):
-            assert torch.equal(tr[r], A.obs.to(torch.int16)), f"tensor exchange rank {r}"
-    for e in (A, B):
+        for r in range(world):  # peer r: this rank's slot (i + r - rank) mod slots at its slot i
+            assert torch.equal(tr[r], torch.roll(A.obs.to(torch.int16), -(r - rank), 0)), f"tensor exchange rank {r}"
+    for e in (A, B, C):
         assert not e.error_flags().any()
         e.close()
