@@ -386,6 +386,8 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     max over ranks as the headline.  The receiver's render of every rank's observations (uint8) is
     timed separately per step (render_ms_per_step)."""
     rx = mdist.RecordExchange(env, units_per_record=64, steps_per_launch=a.records_steps)
+    # every step's reward / done too (mrts_set_step_responses): with the records, each step's full Responses
+    env.set_step_responses(max(3, a.steps))
 
     def run(first, n):
         if mode["fused"]:
@@ -430,6 +432,7 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     torch.cuda.synchronize(env.device)
     render8_ms = e0.elapsed_time(e1) / n_r
     del out8r
+    env.set_step_responses(0)
     rec_bytes = (S // 2) * rx.words * 4
     return {
         "value": total_games * a.steps / t,
@@ -448,16 +451,23 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
         "render": f"mrts_render_records_dev: all {world} ranks' observations of one step rebuilt as {'int8' if a.po else 'uint8'} "
                   f"[{world * S}, {env.dims[3]}, {env.dims[1]}, {env.dims[2]}] (not in value: a consumer may read the "
                   "records directly)",
+        "responses": "every step's reward / done written to a per-step ring inside the launches (mrts_set_step_responses; "
+                     "rank-local), so with the records each step's full Responses (JNIGridnetVecClient.gameStep) is available",
         "steps_per_launch": a.records_steps or "all",
         "launch": "multi-step launches (each game's state in LDS), every step's records written by the step kernel",
     }
 
 
 def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, dist, DeviceVecEnv):
-    """VERDICT r3 #3a — SURVEY.md §8(d)'s byte contract, as the Java client moves it: every mask byte
-    rewritten each step (JNIGridnetClientSelfPlay.java:196-209, mask_delta off), the policy as its own
+    """VERDICT r3 #3a / r4 #6 — SURVEY.md §8(d)'s byte contract, as the Java client moves it: every mask
+    byte rewritten each step (JNIGridnetClientSelfPlay.java:196-209, mask_delta off), the policy as its own
     launch reading the full masks and writing every action row, one step launch per step (a per-step
-    consumer), on a second handle with the headline's shard.  -> the JSON block."""
+    consumer), on a second handle with the headline's shard.  §8(d) excludes policy generation and reports
+    it separately: the step kernel and the policy kernel are timed apart (fence-free events around each
+    launch of an eager pass), so the §8(d) fraction is given over the step kernel's time (step_only) and
+    over the whole step + policy window (step_plus_policy).  A fused variant (the step kernel samples the
+    next rows itself, masks still fully rewritten, one launch per step) shows what full masks alone cost.
+    -> the JSON block."""
     import numpy as np
 
     from microrts_amd import UnitTypeTable
@@ -470,12 +480,13 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
     for k in range(a.burnin):
         env.random_policy(SEED, k)
         env.step()
+    t_step = a.burnin
     graph = torch.cuda.CUDAGraph()
     cap = torch.cuda.Stream(env.device)
     cap.wait_stream(torch.cuda.current_stream(env.device))
     with torch.cuda.graph(graph, stream=cap):  # kernels only: no collective in this graph
         for k in range(a.steps):
-            env.random_policy(SEED, a.burnin + k)
+            env.random_policy(SEED, t_step + k)
             env.step()
     torch.cuda.synchronize(env.device)
     graph.replay()  # warm
@@ -489,15 +500,47 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
     if world > 1:
         dist.barrier()
     t = mdist.max_over_ranks(time.perf_counter() - t0, env.device)
+    t_step += a.steps  # (the replays rerun the captured step indices; the policy stream does not care)
+    # the two kernels apart: an eager pass with fence-free events around each launch
+    cur = torch.cuda.current_stream(env.device)
+    n_e = min(a.steps, 20)
+    ev = [[_FenceFreeEvent() for _ in range(4)] for _ in range(n_e)]
+    for k in range(n_e):
+        ev[k][0].record(cur)
+        env.random_policy(SEED, t_step + k)
+        ev[k][1].record(cur)
+        ev[k][2].record(cur)
+        env.step()
+        ev[k][3].record(cur)
+    torch.cuda.synchronize(env.device)
+    t_step += n_e
+    pol_us = 1e3 * float(np.median([ev[k][0].elapsed_time(ev[k][1]) for k in range(n_e)]))
+    stp_us = 1e3 * float(np.median([ev[k][2].elapsed_time(ev[k][3]) for k in range(n_e)]))
+    # fused policy, full masks: one launch per step (not the steady delta state), timed like the headline
+    env.random_policy(SEED, t_step)
+    env.rollout_fused(SEED, t_step + 1, 2)  # warm
+    t_step += 2
+    torch.cuda.synchronize(env.device)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(env.device)
+    t1 = time.perf_counter()
+    env.rollout_fused(SEED, t_step + 1, a.steps)
+    torch.cuda.synchronize(env.device)
+    if world > 1:
+        dist.barrier()
+    tf = mdist.max_over_ranks(time.perf_counter() - t1, env.device)
     assert not env.error_flags().any()
     units = float(np.mean([env.dump_state(s)[4] for s in range(0, min(S, 64), 2)]))
     HW = H * W
     survey = S * (HW * 7 * 4 + C * HW * 4 + HW * K + (16 * units + 2 * HW + 16))
     env.close()
     step_s = t / a.steps
-    # the HBM bytes this leg really moves (the policy launch reads every mask byte the step launch wrote,
-    # and the step re-reads every action row): PMC passes of the same leg, same kernel code
-    # (tools/profile_full_contract.sh + tools/full_contract_pmc.py summarize)
+    # the bytes this leg moves through the L2's memory-side (fabric) request counters: the policy launch reads
+    # every mask byte the step launch wrote, and the step re-reads every action row.  FETCH_SIZE / WRITE_SIZE
+    # count Infinity-Cache (L3, 256 MiB) hits too (MI355X_MICROARCH.md, HBM section), so this is L2-fabric
+    # traffic, an upper bound on HBM bytes — not HBM bytes (tools/profile_full_contract.sh +
+    # tools/full_contract_pmc.py summarize)
     traffic = None
     pf = os.path.join(ROOT, "profiles", f"pmc_full_contract_{a.config}.json")
     if os.path.exists(pf) and a.utt == 1 and world == 1:
@@ -506,10 +549,11 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
             traffic = {"note": f"{os.path.relpath(pf, ROOT)} was taken with other kernel code; not used"}
         elif pj.get("games") == sh["n_slots"] // 2:
             tb = pj["traffic_bytes_per_step"]
-            traffic = {"bytes_per_step": tb, "GBps": tb / step_s / 1e9, "frac": tb / step_s / 1e9 / HBM_PEAK_GBS,
-                       "kernel_GBps": tb / (pj["kernel_us_per_step"] * 1e-6) / 1e9,
-                       "source": f"{os.path.relpath(pf, ROOT)} ({pj['tag']}: 2 x FETCH_SIZE + WRITE_SIZE of the leg's "
-                                 "policy + step launches, separate --pmc passes, same gfx950 code object)"}
+            traffic = {"l2_fabric_bytes_per_step": tb, "l2_fabric_GBps": tb / step_s / 1e9,
+                       "what": "2 x FETCH_SIZE + WRITE_SIZE of the leg's policy + step launches: L2 memory-side requests, "
+                               "Infinity-Cache hits included (the policy's re-read of the just-written masks fits the 256 MiB "
+                               "L3), so an upper bound on HBM traffic, not a fraction of HBM peak",
+                       "source": f"{os.path.relpath(pf, ROOT)} ({pj['tag']}: separate --pmc passes, same gfx950 code object)"}
     out = {
         "value": total_games * a.steps / t,
         "ms_per_step": 1e3 * step_s,
@@ -517,10 +561,18 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
         "policy": "separate masked-uniform policy launch per step (reads every mask byte, writes every action row)",
         "launch": "hipGraph replay of K x (policy launch + step launch)",
         "survey_8d_bytes_per_step": survey,
-        "survey_8d_GBps": survey / step_s / 1e9,
-        "survey_8d_frac": survey / step_s / 1e9 / HBM_PEAK_GBS,
+        "step_only": {"step_kernel_us": stp_us, "survey_8d_GBps": survey / (stp_us * 1e-6) / 1e9,
+                      "survey_8d_frac": survey / (stp_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                      "timing": f"median of {n_e} step launches, fence-free HIP events around each (eager pass)"},
+        "policy_kernel_us": pol_us,
+        "step_plus_policy": {"survey_8d_GBps": survey / step_s / 1e9, "survey_8d_frac": survey / step_s / 1e9 / HBM_PEAK_GBS,
+                             "timing": "wall clock of the graph replay (both kernels, launch gaps)"},
+        "fused_full_masks": {"value": total_games * a.steps / tf, "ms_per_step": 1e3 * tf / a.steps,
+                             "survey_8d_frac": survey / (tf / a.steps) / 1e9 / HBM_PEAK_GBS,
+                             "launch": "mrts_rollout_fused_dev on the full-mask handle: one launch per step, the step kernel "
+                                       "samples the next rows itself and rewrites every mask byte and every action row"},
         "note": "SURVEY.md §8(d): B = A + O + M + S per env-step (all action rows read, int32 observation, uint8 masks, "
-                "live state); time = the whole step (policy + step kernels) from the wall clock",
+                "live state); policy generation excluded from B and timed separately (policy_kernel_us)",
     }
     if traffic is not None:
         out["traffic"] = traffic

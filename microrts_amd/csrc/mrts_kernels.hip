@@ -2535,7 +2535,7 @@ struct Game {
         const int k0 = (int)(D.reward_kinds4 & 15u);
         // the Responses ring (mrts_set_step_responses): reward / done point at the call's ring and each
         // iteration writes its own step there (resp_stride = n_slots * n_rewards; 0 = the plain buffers)
-        const size_t ro = MRTS_RESP_RING ? (size_t)it * (uint32_t)D.resp_stride : 0;
+        const size_t ro = MRTS_RESP_RING ? (size_t)((uint32_t)it * (uint32_t)D.resp_stride) : 0;
         const bool done0 = k0 == RF_WINLOSS ? gameover : (k0 == RF_RESOURCE_GATHER ? !resLeft : false);
         const int L = lid();
         if (R == 1 && k0 == RF_WINLOSS) {  // WinLoss alone (the common case): a wave-uniform branch, no switch
@@ -4979,7 +4979,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
         const bool done0 = G.writeRewards(slot0, nslots, selfplay ? 0 : side, selfplay ? 1 : side, gameover, winner, it);
         const bool reset = done0 || steps >= D.max_steps;
         if (reset && D.done && lane_id() < nslots)
-            D.done[(MRTS_RESP_RING ? (size_t)it * (uint32_t)D.resp_stride : 0) + (size_t)(slot0 + lane_id()) * D.n_rewards] = 1;
+            D.done[(MRTS_RESP_RING ? (size_t)((uint32_t)it * (uint32_t)D.resp_stride) : 0) + (size_t)(slot0 + lane_id()) * D.n_rewards] = 1;
         if (MRTS_UNLIKELY(reset)) {
             G.hset(H_STEPS, 0);  // envSteps[i] = 0 (JNIGridnetVecClient.java:229,264-265,285)
             G.resetFromTemplate();
