@@ -261,7 +261,8 @@ int mrts_render_status(mrts_env* env);
  * every mrts_rollout_{fused,uniform}[_records|_exchange]_dev call also writes the reward / done of its
  * k-th step ([n_slots][n_rewards], as d_reward / d_done; done[.][0] = 1 when the step auto-reset the
  * game) at d_rewards / d_dones + k * n_slots * n_rewards, k = 0 .. n_steps - 1 — inside multi-step
- * launches too.  With a records rollout, step k's observation is its records rendered
+ * launches too — INSTEAD of d_reward / d_done, which such calls leave untouched (the last step's values
+ * are ring step n_steps - 1).  With a records rollout, step k's observation is its records rendered
  * (mrts_render_records_dev at step_offsets[k]): the full per-step Responses without one launch per step.
  * A rollout call of more than max_steps steps returns -EINVAL.  NULL, NULL turns it off. */
 int mrts_set_step_responses(mrts_env* env, double* d_rewards, uint8_t* d_dones, int32_t max_steps);

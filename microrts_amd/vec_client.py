@@ -636,8 +636,9 @@ class DeviceVecEnv:
     def set_step_responses(self, max_steps):
         """Every step's reward / done from each rollout call of at most max_steps steps
         (mrts_set_step_responses; Java's gameStep returns them on every call): step k of the next call
-        lands in self.step_rewards[k] / self.step_dones[k] ([slots] or [slots][R], as reward / done).
-        0 turns it off."""
+        lands in self.step_rewards[k] / self.step_dones[k] ([slots] or [slots][R], as reward / done) INSTEAD
+        of self.reward / self.done, which rollout calls then leave untouched (the last step's values are
+        step_rewards[n_steps - 1]).  0 turns it off."""
         h, T = self._h, self.torch
         if not max_steps:
             _lib.check(h.L.mrts_set_step_responses(h.h, None, None, 0))

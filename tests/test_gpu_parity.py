@@ -823,9 +823,10 @@ def _crowded_32x32(tmp_path, per_player):
 
 
 def test_po_helper_wave_over_64_units(tmp_path):
-    """The partially observable multi-step launch renders through a helper wave (helperLoopPO) only while
-    the game's units fit one wave; a step with more than 64 units is rendered by the game wave itself
-    (after the second barrier) and the helper takes over again after the auto-reset.  The crowded map
+    """The partially observable multi-step launch (c5's shape) renders through a helper wave (helperLoopPO):
+    from the game's packed step (renderPOPacked) while the game's units fit one wave; a step with more than
+    64 units is rendered by the helper from the game's live state (the general writeObsPO) while the game
+    waits at a second barrier, and the packed form takes over again after the auto-reset.  The crowded map
     starts at 60 units and the games produce past 64 (oracle: steps ~249-298 of 300): multi-step = one
     launch per step, bit for bit, across both transitions."""
     torch = _torch()

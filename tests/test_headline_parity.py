@@ -491,7 +491,7 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
             assert torch.equal(g8.to(torch.int32), want[j]), f"step {k - n + j}: rendered byte observation"
             assert torch.equal(B.step_rewards[j], wantR[j]), f"step {k - n + j}: the Responses ring's reward"
             assert torch.equal(B.step_dones[j], wantD[j]), f"step {k - n + j}: the Responses ring's done"
-        for name in ("obs", "reward", "done", "actions") + (() if uniform else ("masks",)):
+        for name in ("obs", "actions") + (() if uniform else ("masks",)):  # (reward / done: the ring's, above)
             assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
         for s in range(0, n_sp, 2):
             assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
@@ -516,8 +516,8 @@ def test_step_responses_every_reward_function():
     """mrts_set_step_responses with all 8 reward functions (reward / done [slots][8]) and
     both rollout forms the benchmark shapes run as multi-step launches (c3's masked fused rollout, c2's
     uniform one): every step's ring entry equals the reward / done a twin returns from one launch per step,
-    across auto-resets (max_steps 60 and gameovers); d_reward / d_done keep the last step's; a call longer
-    than the ring is refused; NULL turns it off."""
+    across auto-resets (max_steps 60 and gameovers); d_reward / d_done are left alone while the ring is on;
+    a call longer than the ring is refused; NULL turns it off (then the plain buffers again)."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
     from microrts_amd._lib import REWARD_FUNCTIONS
@@ -555,12 +555,20 @@ def test_step_responses_every_reward_function():
                 assert torch.equal(B.step_rewards[j], wantR[j]), f"{mp}: step {k - n + j} reward"
                 assert torch.equal(B.step_dones[j], wantD[j]), f"{mp}: step {k - n + j} done"
                 saw_done |= bool(wantD[j][:, 0].any())
-            for name in ("obs", "reward", "done", "actions"):
+            for name in ("obs", "actions"):
                 assert torch.equal(getattr(A, name), getattr(B, name)), f"{mp}: {name} after {k}"
+            assert not bool(B.reward.any()) and not bool(B.done.any()), "the plain buffers are left alone"
         assert saw_done, "no auto-reset inside the checked steps"
         with pytest.raises(RuntimeError):
             B.rollout_uniform(SEED, k, 151) if uniform else B.rollout_fused(SEED, k + 1, 151)
         B.set_step_responses(0)
+        for e in (A, B):  # off again: the plain buffers receive the step
+            if uniform:
+                e.rollout_uniform(SEED, k, 3)
+            else:
+                e.rollout_fused(SEED, k + 1, 3)
+        for name in ("obs", "reward", "done", "actions"):
+            assert torch.equal(getattr(A, name), getattr(B, name)), f"{mp}: {name} with the ring off"
         for e in (A, B):
             assert not e.error_flags().any()
             e.close()
