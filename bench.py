@@ -432,6 +432,23 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     torch.cuda.synchronize(env.device)
     render8_ms = e0.elapsed_time(e1) / n_r
     del out8r
+    # a learner's batch in MicroRTS-Py's one-hot layout straight from the records: B random
+    # slots of the 8-rank volume per step (every "rank" reads this rank's records: rank stride 0)
+    onehot = {}
+    if not a.po:
+        gsel = torch.Generator(device="cpu").manual_seed(1)
+        K = a.steps
+        for B in (1024, 2048, S):  # per step; one launch for the window's K steps
+            sel = torch.randint(0, 8 * S, (K * B,), generator=gsel).to(torch.int32).to(env.device)
+            so = torch.tensor([int(off[j][0]) for j in range(K) for _ in range(B)], dtype=torch.int64, device=env.device)
+            oh = env.render_records_onehot(rx.recv, 0, 0, sel, step_off=so)
+            e0.record(cur)
+            env.render_records_onehot(rx.recv, 0, 0, sel, oh, step_off=so)
+            e1.record(cur)
+            torch.cuda.synchronize(env.device)
+            us = 1e3 * e0.elapsed_time(e1) / K
+            onehot[str(B)] = {"us_per_step": us, "bytes_per_step": oh.numel() / K, "GBps": oh.numel() / K / (us * 1e-6) / 1e9}
+            del oh
     env.set_step_responses(0)
     rec_bytes = (S // 2) * rx.words * 4
     return {
@@ -448,6 +465,11 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
         "render_ms_per_step": render_ms,
         "render_ms_per_step_8_ranks": render8_ms,
         "render_GBps_8_ranks": 8 * env.obs.numel() / (render8_ms * 1e-3) / 1e9,
+        "onehot_batch": onehot or None,
+        "onehot_batch_note": "mrts_render_records_onehot_dev: B random slots of the 8-rank volume at each of the window's K "
+                             "steps, as MicroRTS-Py one-hot uint8 [K x B][H][W][F] (a learner's minibatch), ONE launch, "
+                             "timed alone (per step = / K); it does not overlap the step launches, whose waves hold every "
+                             "SIMD's VGPRs (4 x 128) and the CUs' LDS (16 x 10 KB): tools/consumer_overlap.py",
         "render": f"mrts_render_records_dev: all {world} ranks' observations of one step rebuilt as {'int8' if a.po else 'uint8'} "
                   f"[{world * S}, {env.dims[3]}, {env.dims[1]}, {env.dims[2]}] (not in value: a consumer may read the "
                   "records directly)",

@@ -251,6 +251,16 @@ int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const in
 int32_t mrts_record_words(const mrts_env* env);
 int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,
                             int32_t out_bytes, void* stream);
+/* A learner's minibatch straight from the records (no Java counterpart: MicroRTS-Py's GridnetVecEnv
+ * encoding, gym_microrts `_encode_obs` — clip each plane to its size, one-hot, channels last;
+ * mrts_onehot_dev's layout), in ONE launch: sample i is slot d_sel[i] (int32, global index r * n_slots + slot
+ * over the ranks whose records hold that step, rank r's at + r * rank_stride) of the step whose rank-0
+ * records start at d_rec + d_step_off[i] words (int64; d_step_off NULL: every sample at d_rec) — e.g. random
+ * (step, slot) pairs of a whole records rollout, offsets from its step_offsets table.  Out: d_out
+ * [n_sel][H][W][F] uint8 (F = mrts_onehot_features, 16-byte aligned).  Full observability (else -ENOTSUP);
+ * the render flag of mrts_render_status applies. */
+int mrts_render_records_onehot_dev(mrts_env* env, const uint32_t* d_rec, int64_t rank_stride, const int32_t* d_sel,
+                                   const int64_t* d_step_off, int32_t n_sel, uint8_t* d_out, void* stream);
 /* 1 if a record rendered by this handle since the last call had its overflow bit set (its game held more
  * units than the record, or a value outside the record's range: the rendered observation lacks them —
  * the sender's handle flagged MRTS_ERR_RECORD), else 0; resets the flag.  Synchronises the device. */

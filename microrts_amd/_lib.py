@@ -50,7 +50,7 @@ def device_code_sha256(path=None):
 EXPORTS = [
     "mrts_create", "mrts_dims", "mrts_reset", "mrts_step", "mrts_get_masks", "mrts_step_rows", "mrts_get_masks_i32",
     "mrts_get_masks_host", "mrts_get_masks_i32_host",
-    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_step_fused_dev", "mrts_rollout_fused_dev", "mrts_set_rollout_events", "mrts_rccl_unique_id", "mrts_exchange_init", "mrts_exchange_init_loopback", "mrts_rollout_fused_exchange_dev", "mrts_rollout_uniform_exchange_dev", "mrts_set_exchange_bytes", "mrts_set_records", "mrts_record_words", "mrts_rollout_fused_records_dev", "mrts_rollout_uniform_records_dev", "mrts_render_records_dev", "mrts_render_status", "mrts_set_step_responses", "mrts_capture_begin", "mrts_capture_end", "mrts_replay", "mrts_set_multi_step", "mrts_multi_step_capable", "mrts_set_obs16", "mrts_policy_uniform_dev", "mrts_step_uniform_dev", "mrts_rollout_uniform_dev", "mrts_policy_invalidate", "mrts_set_obs_delta", "mrts_obs_invalidate", "mrts_set_source_output", "mrts_copy_games", "mrts_copy_games_dev", "mrts_playout", "mrts_playout_dev", "mrts_trace_step",
+    "mrts_reset_dev", "mrts_step_dev", "mrts_get_masks_dev", "mrts_step_rows_dev", "mrts_get_masks_i32_dev", "mrts_onehot_features", "mrts_onehot_dev", "mrts_policy_dev", "mrts_step_fused_dev", "mrts_rollout_fused_dev", "mrts_set_rollout_events", "mrts_rccl_unique_id", "mrts_exchange_init", "mrts_exchange_init_loopback", "mrts_rollout_fused_exchange_dev", "mrts_rollout_uniform_exchange_dev", "mrts_set_exchange_bytes", "mrts_set_records", "mrts_record_words", "mrts_rollout_fused_records_dev", "mrts_rollout_uniform_records_dev", "mrts_render_records_dev", "mrts_render_status", "mrts_render_records_onehot_dev", "mrts_set_step_responses", "mrts_capture_begin", "mrts_capture_end", "mrts_replay", "mrts_set_multi_step", "mrts_multi_step_capable", "mrts_set_obs16", "mrts_policy_uniform_dev", "mrts_step_uniform_dev", "mrts_rollout_uniform_dev", "mrts_policy_invalidate", "mrts_set_obs_delta", "mrts_obs_invalidate", "mrts_set_source_output", "mrts_copy_games", "mrts_copy_games_dev", "mrts_playout", "mrts_playout_dev", "mrts_trace_step",
     "mrts_evaluate", "mrts_evaluate_dev", "mrts_utt_json", "mrts_get_state_json",
     "mrts_set_state_json", "mrts_checkpoint_size", "mrts_checkpoint", "mrts_restore", "mrts_get_state", "mrts_error_flags", "mrts_env_steps", "mrts_stream",
     "mrts_destroy", "mrts_last_error",
@@ -149,6 +149,7 @@ def load(path=LIB_PATH):
     L.mrts_rollout_uniform_records_dev.argtypes = [P, P, P, P, P, P, U64, U32, I32, P, P, P]
     L.mrts_render_records_dev.argtypes = [P, P, I32, I64, P, I32, P]
     L.mrts_render_status.argtypes = [P]
+    L.mrts_render_records_onehot_dev.argtypes = [P, P, I64, P, P, I32, P, P]
     L.mrts_set_step_responses.argtypes = [P, P, P, I32]
     L.mrts_capture_begin.argtypes = [P, P]
     L.mrts_capture_end.argtypes = [P, P]

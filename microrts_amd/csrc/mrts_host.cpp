@@ -45,6 +45,9 @@ hipError_t launchCopyGames(int32_t* dst, const int32_t* src, const int32_t* pair
 hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, float* out, hipStream_t stream);
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
                                int64_t rank_stride, void* out, int out_bytes, int32_t* err, hipStream_t stream);
+hipError_t launchRenderRecordsOneHot(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int64_t rank_stride,
+                                     const int32_t* sel, const int64_t* step_off, int n_sel, uint8_t* out, int32_t* err,
+                                     hipStream_t stream);
 }  // namespace mrts
 
 static thread_local std::string g_err;
@@ -1484,6 +1487,26 @@ int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const in
                                stream, nullptr, nullptr, rp);
         });
         ev.done();
+        return 0;
+    } catch (const Fail& f) {
+        return fail(f);
+    }
+}
+
+int mrts_render_records_onehot_dev(mrts_env* env, const uint32_t* d_rec, int64_t rank_stride, const int32_t* d_sel,
+                                   const int64_t* d_step_off, int32_t n_sel, uint8_t* d_out, void* stream) {
+    try {
+        if (!env || !d_rec || !d_out || (n_sel > 0 && !d_sel) || n_sel < 0 || rank_stride < 0) throw Fail{-EINVAL, "bad argument"};
+        if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
+        if (env->partialObs) throw Fail{-ENOTSUP, "one-hot from records: full observability only"};
+        if (((uintptr_t)d_out & 15) || ((uintptr_t)d_rec & 3)) throw Fail{-EINVAL, "misaligned buffer"};
+        HIPCHK(hipSetDevice(env->device));
+        if (!env->d_renderErr) {
+            HIPCHK(hipMalloc(&env->d_renderErr, 4));
+            HIPCHK(hipMemset(env->d_renderErr, 0, 4));
+        }
+        HIPCHK(launchRenderRecordsOneHot(env->hstatic, env->d_static, d_rec, env->recUnits, rank_stride, d_sel, d_step_off, n_sel,
+                                         d_out, env->d_renderErr, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
         return fail(f);

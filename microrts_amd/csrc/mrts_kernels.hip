@@ -5623,6 +5623,74 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
         }
     }
 }
+// A learner's batch straight from the exchanged records, in the layout it consumes: the
+// MicroRTS-Py encoding of the observation (gym_microrts `_encode_obs`, as k_onehot: clip each plane, one-hot,
+// channels last) of n_sel samples: sample i is slot sel[i] (global index r * n_slots + slot over every rank's
+// slots) of the step whose records start at rec + step_off[i] (null: rec) — a minibatch of (step, slot)
+// pairs from a whole rollout window in one launch, with no int32 / uint8 planes of all ranks in between.  Full observability.  One 256-thread block per selected
+// slot: its game's record paints the 5 dynamic planes as bytes in LDS (as k_render_records), each cell's
+// F one-hot bytes are composed in LDS, and the slot's H x W x F bytes leave as aligned 16-byte stores.
+// out = [n_sel][H][W][F] uint8 (HW * F % 16 == 0, the host checks).
+__global__ __launch_bounds__(256) void k_render_records_onehot(const KStatic* __restrict__ PS, const uint32_t* __restrict__ rec,
+                                                               int units, int64_t rank_stride, const int32_t* __restrict__ sel,
+                                                               const int64_t* __restrict__ step_off, uint8_t* __restrict__ out,
+                                                               OneHotParams Q, int32_t* __restrict__ err) {
+    __shared__ uint32_t imgw[5 * 256 / 4];
+    __shared__ __align__(16) uint8_t buf[256 * 40];
+    uint8_t* img = (uint8_t*)imgw;
+    const KStatic& P = *PS;
+    const int t = (int)threadIdx.x, HW = P.HW, S = 2 * P.n_games, F = Q.F;
+    const int gs = sel[blockIdx.x];
+    const int r = gs / S, slot = gs - r * S, g = slot >> 1, p = slot & 1;
+    const uint32_t* rc = rec + (step_off ? step_off[blockIdx.x] : 0) + (size_t)r * (size_t)rank_stride +
+                         (size_t)g * recWords(units, false);
+    for (int i = t; i < 5 * HW / 4; i += 256) imgw[i] = 0u;
+    for (int k = t; k < HW * F / 4; k += 256) ((uint32_t*)buf)[k] = 0u;
+    const uint32_t hdr = rc[0];
+    if (t == 0 && (hdr >> 31)) *err = 1;  // overflow (mrts_render_status)
+    __syncthreads();
+    const int n = min((int)(hdr & 0xFFFFu), units);
+    for (int i = t; i < n; i += 256) {
+        const uint32_t w = rc[1 + i];
+        const int c = (int)(w & 0xFFu);
+        if (c >= HW) continue;
+        img[c] = (uint8_t)(w >> 8);
+        img[HW + c] = (uint8_t)(w >> 16);
+        img[2 * HW + c] = (uint8_t)((w >> 27) & 3u);  // player + 1 (0 = none)
+        img[3 * HW + c] = (uint8_t)((w >> 24) & 7u);
+        img[4 * HW + c] = (uint8_t)(w >> 29);
+    }
+    __syncthreads();
+    const uint8_t* terr = (const uint8_t*)(P.tmpl + P.tmpl_off[g] + T_TERR);
+    for (int c = t; c < HW; c += 256) {
+        const int pl1 = img[2 * HW + c];  // owner plane of slot p: ((player + p) % 2) + 1
+        const int v[6] = {img[c], img[HW + c], pl1 ? ((pl1 - 1 + p) & 1) + 1 : 0, img[3 * HW + c], img[4 * HW + c],
+                          terr[c] ? 1 : 0};
+#pragma unroll
+        for (int q = 0; q < 6; q++) buf[c * F + Q.offs[q] + min(max(v[q], 0), Q.sizes[q] - 1)] = 1;
+    }
+    __syncthreads();
+    uint4* dst = (uint4*)(out + (size_t)blockIdx.x * HW * F);
+    for (int k = t; k < HW * F / 16; k += 256) dst[k] = ((const uint4*)buf)[k];
+}
+hipError_t launchRenderRecordsOneHot(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int64_t rank_stride,
+                                     const int32_t* sel, const int64_t* step_off, int n_sel, uint8_t* out, int32_t* err,
+                                     hipStream_t stream) {
+    OneHotParams Q{};
+    const int base[6] = {5, 5, 3, hs.utt.ntypes + 1, 6, 2};
+    int f = 0;
+    for (int q = 0; q < 6; q++) {
+        Q.sizes[q] = base[q];
+        Q.offs[q] = f;
+        f += base[q];
+    }
+    Q.F = f;
+    if (hs.partial_obs || hs.HW > 256 || f > 40 || ((size_t)hs.HW * f) % 16 || ((uintptr_t)out & 15)) return hipErrorInvalidValue;
+    if (n_sel <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_render_records_onehot, dim3((unsigned)n_sel), dim3(256), 0, stream, ds, rec, units, rank_stride, sel,
+                       step_off, out, Q, err);
+    return hipGetLastError();
+}
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
                                int64_t rank_stride, void* out, int out_bytes, int32_t* err, hipStream_t stream) {
     if (hs.partial_obs) {

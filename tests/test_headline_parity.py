@@ -574,6 +574,58 @@ def test_step_responses_every_reward_function():
             e.close()
 
 
+@pytest.mark.parametrize("mp,spl", [("maps/16x16/basesWorkers16x16.xml", 0), ("maps/8x8/basesWorkers8x8.xml", 7)])
+def test_records_onehot_batch(mp, spl):
+    """mrts_render_records_onehot_dev: a learner's batch — random slots of every rank of an
+    8-rank loopback exchange — rendered from the records straight into MicroRTS-Py's one-hot layout equals
+    the twin's int32 observation of the same slot (rank r's slot s = the twin's slot s + 2 (r - rank), the
+    loopback's rotation) through mrts_onehot_dev, every step of 1 + 30 + 12 records steps."""
+    torch = _torch()
+    from microrts_amd import DeviceVecEnv
+
+    n_sp, world, rank = 64, 8, 3
+    A = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=37)
+    B = DeviceVecEnv(n_sp, 0, 300, [mp] * n_sp, seed=37)
+    A.set_multi_step(False)
+    for e in (A, B):
+        e.reset()
+        e.random_policy(SEED, 0)
+    assert B._h.L.mrts_exchange_init_loopback(B._h.h, world, rank) == 0
+    B.set_records(64, spl)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    S, k = n_sp, 0
+    for n in (1, 30, 12):
+        want = []
+        for j in range(n):
+            A.rollout_fused(SEED, k + j + 1, 1)
+            A.synchronize()
+            want.append(A.onehot_obs().clone())
+        recv = B.records_buffer(n, world)
+        off = B.rollout_fused_records(SEED, k + 1, n, recv)
+        k += n
+        for j in range(n):
+            sel = torch.randperm(world * S, generator=g)[:100].to(torch.int32)
+            got = B.render_records_onehot(recv, off[j, 0], off[j, 1], sel.to(B.device))
+            B.synchronize()
+            r, s = sel // S, sel % S
+            twin = (s + 2 * (r - rank)) % S
+            assert torch.equal(got.cpu(), want[j].cpu()[twin.long()]), f"step {k - n + j}: one-hot batch"
+        # one launch for a minibatch of random (step, slot) pairs over the whole call (per-sample step offsets)
+        js = torch.randint(0, n, (300,), generator=g)
+        sel = torch.randint(0, world * S, (300,), generator=g).to(torch.int32)
+        so = torch.tensor([int(off[j, 0]) for j in js.tolist()], dtype=torch.int64)
+        got = B.render_records_onehot(recv, 0, off[0, 1], sel.to(B.device), step_off=so.to(B.device)).cpu()
+        B.synchronize()
+        r, s = sel // S, sel % S
+        twin = ((s + 2 * (r - rank)) % S).long()
+        for i in range(300):
+            assert torch.equal(got[i], want[int(js[i])][int(twin[i])].cpu()), f"minibatch sample {i}"
+    assert not B.render_overflow()
+    for e in (A, B):
+        assert not e.error_flags().any()
+        e.close()
+
+
 @pytest.mark.parametrize("mp,po,spl,world,rank", [("maps/16x16/basesWorkers16x16.xml", False, 0, 8, 3),
                                                   ("maps/16x16/basesWorkers16x16.xml", False, 7, 8, 7),
                                                   ("maps/BWDistantResources32x32.xml", True, 9, 4, 1)])

@@ -64,12 +64,16 @@ def summarize(a):
     per = {}
     for c, sub in (("FETCH_SIZE", "pmc_fetch"), ("WRITE_SIZE", "pmc_write")):
         ds = dispatches(os.path.join(src, sub, "run_counter_collection.csv"))
-        last = ds[-2 * K:]  # the timed graph replay: K x (policy launch + step launch)
+        # the timed graph replay: K x (policy launch + step launch), followed by the leg's eager pass (min(K, 20)
+        # policy + step pairs) and its fused variant (one policy launch, 2 warm + K fused step launches)
+        tail = 2 * min(K, 20) + 1 + 2 + K
+        last = ds[-2 * K - tail:-tail]
         assert len(last) == 2 * K and sum(1 for x in last if x[1].startswith("k_policy")) == K, "unexpected dispatch list"
         per[c] = sum(v[c] for _, _, v in last) * 1024 / K  # KB -> bytes, per step
         per[c + "_by_kernel"] = {n: sum(v[c] for _, k, v in last if k.startswith(n)) * 1024 / K for n in KERNELS}
     trace = list(csv.DictReader(open(os.path.join(src, "stats", "run_kernel_trace.csv"))))
-    tr = sorted((r for r in trace if r["Kernel_Name"].startswith(KERNELS)), key=lambda r: int(r["Start_Timestamp"]))[-2 * K:]
+    tail = 2 * min(K, 20) + 1 + 2 + K
+    tr = sorted((r for r in trace if r["Kernel_Name"].startswith(KERNELS)), key=lambda r: int(r["Start_Timestamp"]))[-2 * K - tail:-tail]
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr) / K / 1e3  # us per step, kernels only
     t = 2 * per["FETCH_SIZE"] + per["WRITE_SIZE"]
     out.update(fetch_size_bytes=per["FETCH_SIZE"], write_size_bytes=per["WRITE_SIZE"], traffic_bytes_per_step=t,
@@ -84,9 +88,12 @@ def summarize(a):
           "| per step | FETCH_SIZE (x2 = bytes) | WRITE_SIZE |", "|---|---|---|"]
     for n in KERNELS:
         md.append(f"| {n} | {2 * per['FETCH_SIZE_by_kernel'][n] / 1e6:.1f} MB | {per['WRITE_SIZE_by_kernel'][n] / 1e6:.1f} MB |")
-    md += ["", f"HBM traffic {t / 1e6:.1f} MB per step (2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes) = "
+    md += ["", f"L2-fabric traffic {t / 1e6:.1f} MB per step (2 x FETCH_SIZE + WRITE_SIZE, separate --pmc passes) = "
            f"{t / (busy * 1e-6) / 1e9:.0f} GB/s over the kernels' time, {t / (line['ms_per_step'] * 1e-3) / 1e9:.0f} GB/s over "
-           f"the window; SURVEY §8(d) contract bytes {line['survey_8d_bytes_per_step'] / 1e6:.1f} MB.", ""]
+           f"the window; SURVEY §8(d) contract bytes {line['survey_8d_bytes_per_step'] / 1e6:.1f} MB.  These are the L2's "
+           "memory-side requests: Infinity-Cache (256 MiB L3) hits are counted too (MI355X_MICROARCH.md, HBM section), "
+           "and the policy launch re-reads masks the step launch just wrote (165 MB < 256 MiB), so they bound HBM "
+           "bytes from above — they are not a fraction of HBM peak.", ""]
     open(os.path.join(ROOT, "profiles", f"{a.tag}_full_contract_{cfg}.md"), "w").write("\n".join(md) + "\n")
     print("\n".join(md))
 

@@ -52,6 +52,12 @@ __global__ __launch_bounds__(64) void probe(int lanes, Stamp* out, int* sink) {
     else if constexpr (OP == 17) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(x) : "v"(b) : "vcc");     \
     else if constexpr (OP == 18) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(x) : "v"(b));                      \
     else if constexpr (OP == 19) asm volatile("v_max_u32 %0, %0, %1" : "+v"(x) : "v"(b));                      \
+    else if constexpr (OP == 21) asm volatile("v_alignbit_b32 %0, %0, %1, %1" : "+v"(x) : "v"(b));             \
+    else if constexpr (OP == 22) asm volatile("v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"(x) : "v"(b));     \
+    else if constexpr (OP == 23) asm volatile("v_add3_u32 %0, %0, %1, %1" : "+v"(x) : "v"(b));                 \
+    else if constexpr (OP == 24) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(x) : "v"(b));               \
+    else if constexpr (OP == 25) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x) : "v"(b));                      \
+    else if constexpr (OP == 26) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(x) : "v"(b));                  \
     else asm volatile("v_or_b32 %0, %0, %1" : "+v"(x) : "v"(b));
             ONE(a0) ONE(a1) ONE(a2) ONE(a3) ONE(a4) ONE(a5) ONE(a6) ONE(a7)
             ONE(a0) ONE(a1) ONE(a2) ONE(a3) ONE(a4) ONE(a5) ONE(a6) ONE(a7)
@@ -71,6 +77,41 @@ __global__ __launch_bounds__(64) void probe(int lanes, Stamp* out, int* sink) {
         out[blockIdx.x] = s;
     }
     if (a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 == 0x7fffffff) sink[l] = 1;
+}
+
+// 64-bit-result opcodes (register pairs): OP 0 v_mad_u64_u32, 1 v_lshl_add_u64, 2 v_lshrrev_b64
+template <int OP>
+__global__ __launch_bounds__(64) void probe64(int lanes, Stamp* out, int* sink) {
+    const int l = threadIdx.x;
+    unsigned long long a0 = l, a1 = l + 1, a2 = l + 2, a3 = l + 3, a4 = l + 4, a5 = l + 5, a6 = l + 6, a7 = l + 7;
+    const int b = (int)blockIdx.x | 1;
+    const bool on = l < lanes;
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    if (on) {
+        for (int i = 0; i < ITERS; i++) {
+#define ONE(x)                                                                                              \
+    if constexpr (OP == 0) asm volatile("v_mad_u64_u32 %0, vcc, %1, %1, %0" : "+v"(x) : "v"(b) : "vcc");    \
+    else if constexpr (OP == 1) asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(x));                      \
+    else asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(x));
+            ONE(a0) ONE(a1) ONE(a2) ONE(a3) ONE(a4) ONE(a5) ONE(a6) ONE(a7)
+            ONE(a0) ONE(a1) ONE(a2) ONE(a3) ONE(a4) ONE(a5) ONE(a6) ONE(a7)
+#undef ONE
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (l == 0) {
+        Stamp s;
+        s.t0 = t0;
+        s.t1 = t1;
+        s.r0 = r0;
+        s.r1 = r1;
+        s.hw = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));
+        s.xcc = (unsigned)__builtin_amdgcn_s_getreg(20 | (15 << 11));
+        out[blockIdx.x] = s;
+    }
+    if (a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 == 0x7fffffffull) sink[l] = 1;
 }
 
 typedef void (*Kern)(int, Stamp*, int*);
@@ -96,7 +137,16 @@ static Kern kern(int op) {
         case 17: return probe<17>;
         case 18: return probe<18>;
         case 19: return probe<19>;
-        default: return probe<20>;
+        case 20: return probe<20>;
+        case 21: return probe<21>;
+        case 22: return probe<22>;
+        case 23: return probe<23>;
+        case 24: return probe<24>;
+        case 25: return probe<25>;
+        case 26: return probe<26>;
+        case 27: return probe64<0>;
+        case 28: return probe64<1>;
+        default: return probe64<2>;
     }
 }
 
@@ -104,8 +154,10 @@ int main(int argc, char** argv) {
     const char* names[] = {"v_add_u32", "v_xor_b32", "v_lshlrev_b32", "v_bfe_u32", "v_and_or_b32", "v_cndmask_b32",
                            "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u32_u24", "v_readlane_b32", "v_readfirstlane_b32",
                            "v_perm_b32", "v_bcnt_u32_b32", "v_cmp_gt_u32", "v_cndmask_b32_e64_sgpr", "v_bfi_b32",
-                           "v_mov_b32", "v_add_co_u32", "v_sub_u32", "v_max_u32", "v_or_b32"};
-    const int nops = 21;
+                           "v_mov_b32", "v_add_co_u32", "v_sub_u32", "v_max_u32", "v_or_b32", "v_alignbit_b32",
+                           "v_bitop3_b32", "v_add3_u32", "v_lshl_or_b32", "v_and_b32", "v_mul_u32_u24", "v_mad_u64_u32",
+                           "v_lshl_add_u64", "v_lshrrev_b64"};
+    const int nops = 30;
     int only = -1;
     if (argc > 1) only = atoi(argv[1]);
     int* sink;
