@@ -440,7 +440,7 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
         K = a.steps
         for B in (1024, 2048, S):  # per step; one launch for the window's K steps
             sel = torch.randint(0, 8 * S, (K * B,), generator=gsel).to(torch.int32).to(env.device)
-            so = torch.tensor([int(off[j][0]) for j in range(K) for _ in range(B)], dtype=torch.int64, device=env.device)
+            so = torch.tensor([[int(off[j][0]), 0] for j in range(K) for _ in range(B)], dtype=torch.int64, device=env.device)
             oh = env.render_records_onehot(rx.recv, 0, 0, sel, step_off=so)
             e0.record(cur)
             env.render_records_onehot(rx.recv, 0, 0, sel, oh, step_off=so)

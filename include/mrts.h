@@ -254,9 +254,10 @@ int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_rank
 /* A learner's minibatch straight from the records (no Java counterpart: MicroRTS-Py's GridnetVecEnv
  * encoding, gym_microrts `_encode_obs` — clip each plane to its size, one-hot, channels last;
  * mrts_onehot_dev's layout), in ONE launch: sample i is slot d_sel[i] (int32, global index r * n_slots + slot
- * over the ranks whose records hold that step, rank r's at + r * rank_stride) of the step whose rank-0
- * records start at d_rec + d_step_off[i] words (int64; d_step_off NULL: every sample at d_rec) — e.g. random
- * (step, slot) pairs of a whole records rollout, offsets from its step_offsets table.  Out: d_out
+ * over the ranks whose records hold that step) of the step whose rank-0 records start at d_rec +
+ * d_step_off[2i] words with rank stride d_step_off[2i + 1] (int64 pairs: the records rollout's step_offsets
+ * row of that step; d_step_off NULL: every sample at d_rec with rank_stride) — e.g. random (step, slot) pairs
+ * of a whole records rollout.  Out: d_out
  * [n_sel][H][W][F] uint8 (F = mrts_onehot_features, 16-byte aligned).  Full observability (else -ENOTSUP);
  * the render flag of mrts_render_status applies. */
 int mrts_render_records_onehot_dev(mrts_env* env, const uint32_t* d_rec, int64_t rank_stride, const int32_t* d_sel,

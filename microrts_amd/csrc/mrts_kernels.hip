@@ -5626,8 +5626,9 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
 // A learner's batch straight from the exchanged records, in the layout it consumes: the
 // MicroRTS-Py encoding of the observation (gym_microrts `_encode_obs`, as k_onehot: clip each plane, one-hot,
 // channels last) of n_sel samples: sample i is slot sel[i] (global index r * n_slots + slot over every rank's
-// slots) of the step whose records start at rec + step_off[i] (null: rec) — a minibatch of (step, slot)
-// pairs from a whole rollout window in one launch, with no int32 / uint8 planes of all ranks in between.  Full observability.  One 256-thread block per selected
+// slots) of the step whose rank-0 records start at rec + step_off[2i] with rank stride step_off[2i + 1] (the
+// rollout's step_offsets row; null: rec and rank_stride) — a minibatch of (step, slot) pairs from a whole
+// rollout window in one launch, with no int32 / uint8 planes of all ranks in between.  Full observability.  One 256-thread block per selected
 // slot: its game's record paints the 5 dynamic planes as bytes in LDS (as k_render_records), each cell's
 // F one-hot bytes are composed in LDS, and the slot's H x W x F bytes leave as aligned 16-byte stores.
 // out = [n_sel][H][W][F] uint8 (HW * F % 16 == 0, the host checks).
@@ -5642,8 +5643,8 @@ __global__ __launch_bounds__(256) void k_render_records_onehot(const KStatic* __
     const int t = (int)threadIdx.x, HW = P.HW, S = 2 * P.n_games, F = Q.F;
     const int gs = sel[blockIdx.x];
     const int r = gs / S, slot = gs - r * S, g = slot >> 1, p = slot & 1;
-    const uint32_t* rc = rec + (step_off ? step_off[blockIdx.x] : 0) + (size_t)r * (size_t)rank_stride +
-                         (size_t)g * recWords(units, false);
+    const int64_t o = step_off ? step_off[2 * blockIdx.x] : 0, rs = step_off ? step_off[2 * blockIdx.x + 1] : rank_stride;
+    const uint32_t* rc = rec + o + (size_t)r * (size_t)rs + (size_t)g * recWords(units, false);
     for (int i = t; i < 5 * HW / 4; i += 256) imgw[i] = 0u;
     for (int k = t; k < HW * F / 4; k += 256) ((uint32_t*)buf)[k] = 0u;
     const uint32_t hdr = rc[0];

@@ -628,14 +628,14 @@ class DeviceVecEnv:
     def render_records_onehot(self, recv, offset, rank_stride, sel, out=None, step_off=None, stream=None):
         """A learner minibatch from records in one launch: the MicroRTS-Py one-hot observations (onehot_obs'
         layout, uint8 [n][H][W][F]) of the slots sel (int32 tensor of global indices r * slots + slot over the
-        ranks in recv) of the step whose records start at recv[offset] — or, with step_off (int64 tensor,
-        one word offset per sample, from a rollout's offsets table), each sample's own step —
-        mrts_render_records_onehot_dev."""
+        ranks in recv) of the step whose records start at recv[offset] with rank_stride — or, with step_off
+        (int64 tensor [n, 2]: each sample's step's row of the rollout's offsets table), each sample's own
+        step — mrts_render_records_onehot_dev."""
         h, T = self._h, self.torch
         F = h.L.mrts_onehot_features(h.h)
         assert sel.dtype == T.int32 and sel.is_contiguous() and sel.device == self.device
         if step_off is not None:
-            assert step_off.dtype == T.int64 and step_off.is_contiguous() and step_off.numel() == sel.numel()
+            assert step_off.dtype == T.int64 and step_off.is_contiguous() and step_off.numel() == 2 * sel.numel()
         if out is None:
             out = T.empty((sel.numel(), h.H, h.W, F), dtype=T.uint8, device=self.device)
         assert out.dtype == T.uint8 and out.is_contiguous() and out.numel() == sel.numel() * h.H * h.W * F

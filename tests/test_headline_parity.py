@@ -613,8 +613,8 @@ def test_records_onehot_batch(mp, spl):
         # one launch for a minibatch of random (step, slot) pairs over the whole call (per-sample step offsets)
         js = torch.randint(0, n, (300,), generator=g)
         sel = torch.randint(0, world * S, (300,), generator=g).to(torch.int32)
-        so = torch.tensor([int(off[j, 0]) for j in js.tolist()], dtype=torch.int64)
-        got = B.render_records_onehot(recv, 0, off[0, 1], sel.to(B.device), step_off=so.to(B.device)).cpu()
+        so = torch.from_numpy(off[js.numpy()]).contiguous()  # each sample's step's (offset, rank stride)
+        got = B.render_records_onehot(recv, 0, 0, sel.to(B.device), step_off=so.to(B.device)).cpu()
         B.synchronize()
         r, s = sel // S, sel % S
         twin = ((s + 2 * (r - rank)) % S).long()

@@ -52,7 +52,7 @@ def main():
     for B in (1024, 2048, 4096, S):
         # per launch ONE render of K x B samples: B random slots of the 8-rank volume at each of its K steps
         sel = torch.randint(0, 8 * S, (K * B,), generator=g).to(torch.int32).cuda()
-        soff = [torch.tensor([int(offs[i][j][0]) for j in range(K) for _ in range(B)], dtype=torch.int64).cuda()
+        soff = [torch.tensor([[int(offs[i][j][0]), 0] for j in range(K) for _ in range(B)], dtype=torch.int64).cuda()
                 for i in range(L)]
         bufs = [env.render_records_onehot(recvs[0], 0, 0, sel, step_off=soff[0]) for _ in range(2)]
         t = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
