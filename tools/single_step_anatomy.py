@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Diagnostic: where a single-step c3 launch (one k_env launch per step, the neural-learner
+form) spends its ~19 us, from the span build (libmrts_span.so, `make -C microrts_amd/csrc span`; never loaded
+by the package): per game the wave's start and end and 8 milestones (s_memrealtime, 100 MHz, lane 0 of the
+wave): 20 = state load issued, 21 = state in LDS, 1 = rows decoded, 3 = both players issued, 4 = cycle done,
+5 = outcome / reward / reset done, 6 = observation written, 9 = masks + policy rows written; then the store.
+Prints per launch: the launch span, the start spread, the mean time of each phase, the games' end spread and
+the per-SIMD last end; and the same for one K = 20 multi-step launch (per step).  One JSON line per launch."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from microrts_amd import _lib  # noqa: E402
+
+L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_span.so"))
+L.mrts_phase_spans.argtypes = [ctypes.c_void_p, ctypes.c_int]
+from microrts_amd import DeviceVecEnv  # noqa: E402
+
+E = int(os.environ.get("E", 4096))
+SEED = 0x5EEDC0DE
+MAP = os.path.join(ROOT, "maps/16x16/basesWorkers16x16.xml")
+MILES = ["load_issued", "load_done", "decoded", "issued", "cycled", "outcome", "obs", "masks"]
+
+
+def spans():
+    sp = (ctypes.c_ulonglong * (11 * E))()
+    _lib.check(L.mrts_phase_spans(sp, E))
+    a = np.array(sp, dtype=np.float64).reshape(11, E)
+    return a[0], a[1], a[2].astype(np.uint64), a[3:]
+
+
+def main():
+    env = DeviceVecEnv(2 * E, 0, 2000, [MAP] * (2 * E), seed=SEED)
+    env.reset()
+    env.random_policy(SEED, 0)
+    env.rollout_fused(SEED, 1, 1000)
+    torch.cuda.synchronize()
+    k = 1001
+    for mode, K in (("single", 1), ("single", 1), ("single", 1), ("multi", 20)):
+        env.set_multi_step(mode == "multi")
+        env.rollout_fused(SEED, k, K)
+        k += K
+        torch.cuda.synchronize()
+        st, en, place, mi = spans()
+        t0 = st.min()
+        us = lambda v: (v - t0) / 100.0  # noqa: E731
+        hw = (place & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        xcc = ((place >> np.uint64(32)) & np.uint64(15)).astype(np.int64)
+        key = ((xcc * 8 + ((hw >> 13) & 7)) * 2 + ((hw >> 12) & 1)) * 64 + ((hw >> 8) & 15) * 4 + ((hw >> 4) & 3)
+        uniq, inv = np.unique(key, return_inverse=True)
+        last = np.zeros(len(uniq))
+        np.maximum.at(last, inv, us(en))
+        out = {"mode": mode, "K": K, "launch_us": round(float(us(en).max()), 2),
+               "start_spread_us": round(float(us(st).max()), 2), "game_us_mean": round(float(((en - st) / 100).mean()), 2),
+               "game_end_us": {"mean": round(float(us(en).mean()), 2), "max": round(float(us(en).max()), 2)},
+               "simd_last_end_us": {"mean": round(float(last.mean()), 2), "max": round(float(last.max()), 2)}}
+        if mode == "single":  # milestones of the (only) step: mean time from the previous milestone
+            prev = st
+            ph = {}
+            for name, m in zip(MILES, mi):
+                ok = m > 0
+                ph[name] = round(float(((m - prev) / 100)[ok].mean()), 3)
+                prev = np.where(ok, m, prev)
+            ph["store_to_end"] = round(float(((en - prev) / 100).mean()), 3)
+            out["phase_us_mean"] = ph
+        print(json.dumps(out), flush=True)
+    env.close()
+
+
+if __name__ == "__main__":
+    main()
