@@ -176,6 +176,9 @@ DEV int lane_id() { return (int)threadIdx.x; }
 // for a unit that died in the observed step; round 5 found the cause (the renders read the dead unit's
 // fields by readlane inside their divergent chunk loop, from a lane that was off there — writeObsPOFast)
 // and the helper is back on.
+#ifndef MRTS_PO_FAST  // partially observable self-play games through selfPlayFast (round 5); 0 = the generic path
+#define MRTS_PO_FAST 1
+#endif
 #ifndef MRTS_RESP_RING  // the per-step Responses ring (mrts_set_step_responses); 0 = A/B builds without it
 #define MRTS_RESP_RING 1
 #endif
@@ -909,7 +912,15 @@ struct Game {
     // issuePlayer, with each lane's own unit fields (load()'s registers) instead of LDS re-reads.
     // Between steps no unit is dead; decoded rows are never parked in LDS (every idle unit's
     // assignment is written by its issue or its fill).
-    DEV void selfPlayFast(const int32_t* rows0, const int32_t* rows1, int s0) {
+    // Partially observable games too (round 5; all units in one wave, snapBothOk): Java decodes each player's
+    // rows against that player's view (JNIGridnetClientSelfPlay.java:159-189, PlayerAction.fromVectorAction
+    // on the PartiallyObservableGameState), which holds every own unit (sight covers its own cell) with the
+    // assignments it has when the view is made — so the decode, fillWithNones and issueSafe are the full
+    // state's; only the pa's base reservations come from the view (the assignments of the units in it,
+    // baseReservations(p)), and the views' snapshots are taken in order: both memberships + view 0's
+    // assignments before player 0 issues (snapshotBoth, or the helper wave's bytes: snapTaken), view 1's
+    // assignments after (snapshotActions(1)).  The generic predecode + decode path did the same, slower.
+    DEV void selfPlayFast(const int32_t* rows0, const int32_t* rows1, int s0, bool snapTaken = false) {
         const int l = lid();
         const uint32_t cu = lcu;
         const int pl = l < nu ? uplay(cu) : -1;
@@ -922,7 +933,7 @@ struct Game {
         } else if (idle) {
             fetchRow(pl == 0 ? rows0 : rows1, s0 + pl, uy(cu) * W + ux(cu), a);
         }
-        const bool useIx = (HW + 2 * W + 31) / 32 <= 64;
+        const bool useIx = !po && (HW + 2 * W + 31) / 32 <= 64;  // PO: the view's reservations (baseReservations)
         if (useIx) buildIndex();  // while the rows are in flight
 #ifdef MRTS_ABLATE
         if (useIx && ab(AB_INDEX)) buildIndex();
@@ -945,6 +956,13 @@ struct Game {
         const int c = uy(cu) * W + ux(cu);
         MPHASE(1);
         for (int p = 0; p < 2; p++) {
+            if (po) {  // the views, in Java's order (see above)
+                if (p == 0) {
+                    if (!snapTaken) snapshotBoth();
+                } else {
+                    snapshotActions(1);
+                }
+            }
             int run0, run1;
             if (useIx) {
                 if (!ixValid) buildIndex();
@@ -4918,8 +4936,9 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
             G.issuePlayer(1 - side, 10, true);
         } else if (gtype == GT_SELFPLAY) {
             // JNIGridnetClientSelfPlay.gameStep (tests/JNIGridnetClientSelfPlay.java:159-189)
-            if (MRTS_LIKELY(!G.po && G.nu <= 64)) {
-                G.selfPlayFast(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, slot0);
+            if (MRTS_LIKELY(G.nu <= 64 && (!G.po || (MRTS_PO_FAST && G.snapBothOk())))) {
+                G.selfPlayFast(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, slot0,
+                               snapTaken);
             } else {
             G.predecode(D.actions + (size_t)slot0 * rowStride, D.actions + (size_t)(slot0 + 1) * rowStride, -1, slot0, slot0 + 1);
             PHASE(1);

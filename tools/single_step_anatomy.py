@@ -22,9 +22,10 @@ L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_span.so"))
 L.mrts_phase_spans.argtypes = [ctypes.c_void_p, ctypes.c_int]
 from microrts_amd import DeviceVecEnv  # noqa: E402
 
-E = int(os.environ.get("E", 4096))
+CFG = os.environ.get("CFG", "c3")  # c5: 2048 partially observable 32x32 games (render helper wave)
+E = int(os.environ.get("E", 4096 if CFG == "c3" else 2048))
 SEED = 0x5EEDC0DE
-MAP = os.path.join(ROOT, "maps/16x16/basesWorkers16x16.xml")
+MAP = os.path.join(ROOT, "maps/16x16/basesWorkers16x16.xml" if CFG == "c3" else "maps/BWDistantResources32x32.xml")
 MILES = ["load_issued", "load_done", "decoded", "issued", "cycled", "outcome", "obs", "masks"]
 
 
@@ -36,7 +37,8 @@ def spans():
 
 
 def main():
-    env = DeviceVecEnv(2 * E, 0, 2000, [MAP] * (2 * E), seed=SEED)
+    po = CFG == "c5"
+    env = DeviceVecEnv(2 * E, 0, 2000, [MAP] * (2 * E), seed=SEED, partial_obs=po, max_units=256 if po else 0)
     env.reset()
     env.random_policy(SEED, 0)
     env.rollout_fused(SEED, 1, 1000)
@@ -60,6 +62,12 @@ def main():
                "start_spread_us": round(float(us(st).max()), 2), "game_us_mean": round(float(((en - st) / 100).mean()), 2),
                "game_end_us": {"mean": round(float(us(en).mean()), 2), "max": round(float(us(en).max()), 2)},
                "simd_last_end_us": {"mean": round(float(last.mean()), 2), "max": round(float(last.max()), 2)}}
+        if mode == "multi":  # the LAST iteration's milestones (each stamp is overwritten per iteration)
+            m = {name: v for name, v in zip(MILES, mi)}
+            seq = ["decoded", "issued", "cycled", "outcome", "obs", "masks"]
+            ok = np.all([m[n] > 0 for n in seq], axis=0)
+            out["last_step_phase_us_mean"] = {b: round(float(((m[b] - m[a]) / 100)[ok].mean()), 3) for a, b in zip(seq, seq[1:])}
+            out["last_step_masks_to_end_us"] = round(float(((en - m["masks"]) / 100)[ok].mean()), 3)
         if mode == "single":  # milestones of the (only) step: mean time from the previous milestone
             prev = st
             ph = {}
