@@ -43,7 +43,12 @@ __device__ unsigned long long g_span[11 * PH_GAMES];    // last launch: [game] s
 // 3 + mileOf(phase id)); no per-phase accumulation.  Each stamp costs an lgkmcnt drain and a store.
 constexpr int NMILE = 8;
 constexpr int mileOf(int ph) {
+#ifdef MRTS_MILES_STEP  // multi-step analysis (tools/single_step_anatomy.py MILES=step): 0 = iteration start (after the
+                        // view snapshot hand-off), 1 = the rows unpacked + issue index (selfPlayFast) instead of the load
+    return ph == 0 ? 0 : ph == 22 ? 1 : ph == 1 ? 2 : ph == 3 ? 3 : ph == 4 ? 4 : ph == 5 ? 5 : ph == 6 ? 6 : ph == 9 ? 7 : -1;
+#else
     return ph == 20 ? 0 : ph == 21 ? 1 : ph == 1 ? 2 : ph == 3 ? 3 : ph == 4 ? 4 : ph == 5 ? 5 : ph == 6 ? 6 : ph == 9 ? 7 : -1;
+#endif
 }
 #ifdef MRTS_NO_MILESTONES  // start / end / placement only (tools/launch_gap.py)
 #define PHASE_IN(acc, tt, i) \

@@ -18,7 +18,8 @@ import torch  # noqa: E402
 
 from microrts_amd import _lib  # noqa: E402
 
-L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_span.so"))
+STEPM = os.environ.get("MILES") == "step"  # libmrts_span_step.so: iteration start / rows unpacked instead of the load
+L = _lib.load(os.path.join(ROOT, "microrts_amd", "libmrts_span_step.so" if STEPM else "libmrts_span.so"))
 L.mrts_phase_spans.argtypes = [ctypes.c_void_p, ctypes.c_int]
 from microrts_amd import DeviceVecEnv  # noqa: E402
 
@@ -26,7 +27,8 @@ CFG = os.environ.get("CFG", "c3")  # c5: 2048 partially observable 32x32 games (
 E = int(os.environ.get("E", 4096 if CFG == "c3" else 2048))
 SEED = 0x5EEDC0DE
 MAP = os.path.join(ROOT, "maps/16x16/basesWorkers16x16.xml" if CFG == "c3" else "maps/BWDistantResources32x32.xml")
-MILES = ["load_issued", "load_done", "decoded", "issued", "cycled", "outcome", "obs", "masks"]
+MILES = (["it_start", "rows_index", "decoded", "issued", "cycled", "outcome", "obs", "masks"] if STEPM else
+         ["load_issued", "load_done", "decoded", "issued", "cycled", "outcome", "obs", "masks"])
 
 
 def spans():
@@ -64,7 +66,7 @@ def main():
                "simd_last_end_us": {"mean": round(float(last.mean()), 2), "max": round(float(last.max()), 2)}}
         if mode == "multi":  # the LAST iteration's milestones (each stamp is overwritten per iteration)
             m = {name: v for name, v in zip(MILES, mi)}
-            seq = ["decoded", "issued", "cycled", "outcome", "obs", "masks"]
+            seq = (["it_start", "rows_index"] if STEPM else []) + ["decoded", "issued", "cycled", "outcome", "obs", "masks"]
             ok = np.all([m[n] > 0 for n in seq], axis=0)
             out["last_step_phase_us_mean"] = {b: round(float(((m[b] - m[a]) / 100)[ok].mean()), 3) for a, b in zip(seq, seq[1:])}
             out["last_step_masks_to_end_us"] = round(float(((en - m["masks"]) / 100)[ok].mean()), 3)
