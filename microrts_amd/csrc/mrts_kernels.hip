@@ -173,6 +173,18 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SAMPLE_UNIFIED
 #define MRTS_SAMPLE_UNIFIED 1
 #endif
+#ifndef MRTS_REC_LANES  // delta mask records stored lane-parallel (storeRecordsLanes, round 5); 0 = by their own lanes
+#define MRTS_REC_LANES 1
+#endif
+#ifndef MRTS_PHILOX_UNROLL
+#define MRTS_PHILOX_UNROLL 1
+#endif
+#ifndef MRTS_POS_CHECKED  // selfPlayFast's issueBatch skips the position pairs acceptChain settled (round 5)
+#define MRTS_POS_CHECKED 1
+#endif
+#ifndef MRTS_XOR3  // Philox's xors as one three-input bit op (round 5); 0 = plain C
+#define MRTS_XOR3 1
+#endif
 #ifndef MRTS_HELPER_PRIO
 #define MRTS_HELPER_PRIO 0
 #endif
@@ -346,12 +358,30 @@ constexpr int UTT_WORDS = (int)(sizeof(DevUtt) / 4);
 constexpr int UTT_LDS = (int)((sizeof(DevUtt) + 15) & ~(size_t)15);
 static_assert(sizeof(DevUtt) % 4 == 0 && UTT_WORDS <= 192, "DevUtt copy: 3 words per lane");
 
+// a ^ b ^ k in one VALU instruction (gfx950's three-input bit op, truth table 0x96; the compiler emits
+// two v_xor_b32 for it); k is wave-uniform (a Philox key word, in an SGPR)
+DEV uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
+#if MRTS_XOR3
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "s"(k));
+    return d;
+#else
+    return a ^ b ^ k;
+#endif
+}
+// Philox4x32-10, the ten rounds unrolled (rolled, the loop carried two v_mov per round and the xors
+// were not fused: 8 VALU per round against 4)
 DEV void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#if MRTS_PHILOX_UNROLL
+#pragma unroll
+#else
+#pragma unroll 1
+#endif
     for (int r = 0; r < 10; r++) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
         const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n1 = (uint32_t)p1;
-        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1, n3 = (uint32_t)p0;
+        const uint32_t n0 = xor3s((uint32_t)(p1 >> 32), c[1], k0), n1 = (uint32_t)p1;
+        const uint32_t n2 = xor3s((uint32_t)(p0 >> 32), c[3], k1), n3 = (uint32_t)p0;
         c[0] = n0;
         c[1] = n1;
         c[2] = n2;
@@ -1022,7 +1052,7 @@ struct Game {
                 }
                 wsync();
                 MPHASE(24);
-                if (acc) issueBatch(isPA, irank, __popcll(acc), l, tt, prm, ttx, tty, tut, false, &cu);
+                if (acc) issueBatch(isPA, irank, __popcll(acc), l, tt, prm, ttx, tty, tut, false, &cu, nullptr, MRTS_POS_CHECKED);
             }
             // fillWithNones(gs, p, 1): p's idle units left without an action, list order
             const bool fill = mine && !isPA;
@@ -1723,8 +1753,12 @@ struct Game {
     // cuKnown: the lane's unit core word uc[s] (already in a register), or null
     // putAny (trace replay): set when a pair is put with a type other than NONE — GameState.issue's
     // return value (:323-324)
+    // posChecked: the batch's MOVE / PRODUCE positions are known to be distinct and unreserved (the rows
+    // passed acceptChain's ResourceUsage test against this same index: selfPlayFast) — the pairwise
+    // walk then visits the PRODUCE lanes only, for the cost sums (round 5: it read four values per MOVE
+    // lane per batch)
     DEV void issueBatch(bool act, int rank, int n, int s, int t, int prm, int tx, int ty, int ut, bool checkDup = false,
-                        const uint32_t* cuKnown = nullptr, bool* putAny = nullptr) {
+                        const uint32_t* cuKnown = nullptr, bool* putAny = nullptr, bool posChecked = false) {
         const bool mp = act && (t == T_MOVE || t == T_PRODUCE);
         const bool np = act && t == T_PRODUCE;
         if (MRTS_UNLIKELY(D.reward_need & RN_COUNTS)) {  // the pairs as the TraceEntry records them (legality applied)
@@ -1762,11 +1796,17 @@ struct Game {
                     if (mc >= 0 && mc + ncost > 0 && mc + ncost > pr) conf = true;
                 }
             }
-            for (uint64_t mm = mpm; mm; mm &= mm - 1) {  // earlier MOVE/PRODUCE lanes of the batch
+            if (posChecked && ballot(np && ncost > 0 && ncost > (pl == 0 ? pres0 : pres1))) {
+                // a PRODUCE whose cost alone exceeds the resources conflicts with any earlier MOVE / PRODUCE
+                // of the batch (consistentWith: 0 + cost > resources) — the walk below skips the MOVEs
+                const int minRank = wave_min(mp ? rank : INF);
+                if (np && ncost > 0 && ncost > (pl == 0 ? pres0 : pres1) && minRank < rank) conf = true;
+            }
+            for (uint64_t mm = posChecked ? ballot(np) : mpm; mm; mm &= mm - 1) {  // earlier MOVE/PRODUCE lanes of the batch
                 const int k = __builtin_ctzll(mm);
-                const int rk = rl(rank, k), tk = rl(ntgt, k), pk = rl(pl, k), ck = rl(np ? ncost : -1, k);
+                const int rk = rl(rank, k), tk = posChecked ? 0 : rl(ntgt, k), pk = rl(pl, k), ck = rl(np ? ncost : -1, k);
                 if (mp && rk < rank) {
-                    if (tk == ntgt) conf = true;
+                    if (!posChecked && tk == ntgt) conf = true;
                     if (np) {
                         const int sum = ((ck >= 0 && pk == pl) ? ck : 0) + ncost;
                         if (sum > 0 && sum > (pl == 0 ? pres0 : pres1)) conf = true;
@@ -4228,6 +4268,61 @@ struct Game {
             if (b < K) dst[b] = (uint8_t)((b < 64 ? (lo >> b) : (uint64_t)(hi >> (b - 64))) & 1u);
         }
     }
+    // The K = 79 mask records of the lanes with si >= 0 (slot index si, cell c, mask bits w0:w1:w2) stored
+    // lane-parallel: the records are listed in LDS (rseq words 16..63, 12 records of 4 words), then five lanes
+    // store each record — lanes 0..3 of it 16 bytes each, lane 4 the last 12 — from the record's 16-bit
+    // field at their offset (byte k = bit k, expand4), and lanes 0..2 one of its 3 head / tail bytes each.
+    // The record's bytes are storeRecord's; a lane storing its own record (storeRecord) spent ~85 VALU
+    // instructions on it, all of which the other lanes waited through (round 5: ~35 for 12 records).
+    // `mrs` covers the game's records from `mbase`; the caller's rseq words 0..15 are not touched.
+    DEV void storeRecordsLanes(int si, int c, uint32_t w0, uint32_t w1, uint32_t w2, __amdgpu_buffer_rsrc_t mrs,
+                               const uint8_t* mbase, int total) const {
+        const uint64_t m = ballot(si >= 0);
+        const int R = __popcll(m);
+        if (R == 0) return;
+        const int l = lid();
+        const int r = lanes_below(m);
+        uint32_t* rb = (uint32_t*)rseq + 16;
+        const int tr = (l * 13) >> 6, q = l - 5 * tr;  // record tr of a pass, its part q (lanes 0..59)
+        const int sel = q >> 1;                         // words sel, sel + 1 hold the part's bits
+        const uint32_t mbLo = (uint32_t)(uintptr_t)mbase;
+        for (int p0 = 0; p0 < R; p0 += 12) {
+            if (si >= 0 && r >= p0 && r < p0 + 12) {
+                uint32_t* e = rb + 4 * (r - p0);
+                e[0] = w0;
+                e[1] = w1;
+                e[2] = w2;
+                e[3] = ((uint32_t)si << 16) | (uint32_t)c;
+            }
+            wsync();
+            if (l < 60 && p0 + tr < R) {
+                const uint32_t* e = rb + 4 * tr;
+                const uint32_t lo = e[sel], hi = e[sel + 1], meta = e[3];
+                const uint32_t s = (meta >> 16) * (uint32_t)total + (meta & 0xFFFFu) * 79u;
+                const uint32_t h = (0u - (mbLo + s)) & 3u;  // head bytes before the first aligned dword
+                // bits h + 16 q .. + 15 of the record: the low half of the funnel shift of (hi:lo)
+                const uint32_t x = __builtin_amdgcn_alignbit(hi, lo, h + 16u * (uint32_t)(q & 1));
+                const int d0 = (int)expand4(x), d1 = (int)expand4(x >> 4), d2 = (int)expand4(x >> 8),
+                          d3 = (int)expand4(x >> 12);
+                const int off = (int)(s + h) + 16 * q;
+                if (q < 4) {
+                    const i32x4v v = {d0, d1, d2, d3};
+                    __builtin_amdgcn_raw_buffer_store_b128(v, mrs, off, 0, SC1_MASK ? 16 : 0);
+                } else {
+                    typedef int32_t i32x3v __attribute__((ext_vector_type(3)));
+                    const i32x3v v = {d0, d1, d2};
+                    __builtin_amdgcn_raw_buffer_store_b96(v, mrs, off, 0, SC1_MASK ? 16 : 0);
+                }
+                if (q < 3) {  // byte q of the 3 outside the 19 dwords: head byte q, else tail byte 76 + q
+                    const bool head = (uint32_t)q < h;
+                    const uint32_t b = head ? (uint32_t)q : 76u + (uint32_t)q;
+                    const uint32_t v = ((head ? e[0] : (e[2] >> 12)) >> q) & 1u;
+                    __builtin_amdgcn_raw_buffer_store_b8((char)v, mrs, (int)(s + b), 0, SC1_MASK ? 16 : 0);
+                }
+            }
+            wsync();
+        }
+    }
     // Delta mask writes with every unit in one wave (nu <= 64, K <= 96): each own idle unit's lane
     // computes its Unit.getUnitActions mask bits in registers and stores its whole record (and, fused
     // policy, its action row) itself; cells that held an idle unit at the previous write and hold none
@@ -4315,6 +4410,17 @@ struct Game {
             ua[l] = w2 & 0xFFFFu;
         }
         if (recOut && si < 0) recOut[l] = ~0u;  // (no record from this lane)
+        // the records stored lane-parallel (storeRecordsLanes) rather than each by its own lane
+        const bool lanePar = MRTS_REC_LANES && !recOut && K == 79 && NW <= 16;
+        if (lanePar) {
+#ifdef MRTS_ABLATE
+            if (!ab(AB_SKIP_RECORD))
+#endif
+            storeRecordsLanes(si, c, w0, w1, w2, mrs, mbase, total);
+#ifdef MRTS_ABLATE
+            if (ab(AB_RECORD)) storeRecordsLanes(launder(si), launder(c), launder(w0), launder(w1), launder(w2), mrs, mbase, total);
+#endif
+        }
         if (si >= 0) {
             const int slot = slot0 + si;
             const uint64_t lo = (uint64_t)w0 | ((uint64_t)w1 << 32);
@@ -4323,6 +4429,7 @@ struct Game {
                 recOut[64 + l] = w0;
                 recOut[128 + l] = w1;
                 recOut[192 + l] = w2;
+            } else if (lanePar) {
             } else
 #ifdef MRTS_ABLATE
             if (!ab(AB_SKIP_RECORD))
