@@ -182,6 +182,9 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_POS_CHECKED  // selfPlayFast's issueBatch skips the position pairs acceptChain settled (round 5)
 #define MRTS_POS_CHECKED 1
 #endif
+#ifndef MRTS_SAMPLE32  // the sampler's type / produce-type picks in 32-bit operations, the packed word direct (round 5)
+#define MRTS_SAMPLE32 1
+#endif
 #ifndef MRTS_XOR3  // Philox's xors as one three-input bit op (round 5); 0 = plain C
 #define MRTS_XOR3 1
 #endif
@@ -403,8 +406,50 @@ DEV int pickBit(uint32_t r, uint64_t bitsv, int n) {
 // (slot id, step, cell, 0)
 // Masked-uniform random policy of one cell (the bench / rollout agent): mask slots 1..K-1 as bits
 // (lo: slots 1..64, hi: 65..), Philox4x32-10 with key = seed, counter = (slot id, step, cell, 0)
+DEV uint32_t packFwdFree(const int32_t a[7]) {  // = packFwd (defined with the forwarded words below)
+    return ((uint32_t)a[0] & 7u) | (((uint32_t)(a[1] + 1) & 7u) << 3) | (((uint32_t)(a[2] + 1) & 7u) << 6) |
+           (((uint32_t)(a[3] + 1) & 7u) << 9) | (((uint32_t)(a[4] + 1) & 7u) << 12) | (((uint32_t)(a[5] + 1) & 15u) << 15) |
+           (((uint32_t)(a[6] + 1) & 127u) << 19);
+}
+// pickBit of a field of at most 32 bits (already masked): the same pick in 32-bit operations
+DEV int pickBit32(uint32_t r, uint32_t bitsv) {
+    const int cnt = __popc(bitsv);
+    if (cnt == 0) return -1;
+    int k = (int)__umulhi(r, (uint32_t)cnt);
+    while (k--) bitsv &= bitsv - 1;
+    return __builtin_ctz(bitsv);
+}
+// packFwd of a row with every value 0 (each parameter field holds value + 1)
+constexpr uint32_t FWD_ZERO = (1u << 3) | (1u << 6) | (1u << 9) | (1u << 12) | (1u << 15) | (1u << 19);
+// packed (optional): packFwd(a) of the drawn row, built from the picks (no field repacking)
 DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes, int K, uint64_t lo, uint64_t hi, int c,
-                       int32_t a[7]) {
+                       int32_t a[7], uint32_t* packed = nullptr) {
+#if MRTS_SAMPLE_UNIFIED && MRTS_SAMPLE32
+    uint32_t ctr[4] = {slotId, step, (uint32_t)c, 0u};
+    philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+    // mask slots 1..K-1 as bits of lo:hi (slot k -> bit k - 1): the type field is bits 0..5, the produce
+    // types bits 22.., the direction fields bits 6 + 4 (t - 1).., the attack window bits 22 + ntypes..
+    const int t = pickBit32(ctr[0], (uint32_t)lo & 63u);
+    int pv = 0, ut = 0;
+    if (t > 0) {
+        // the parameter of type t from ONE pick over that type's field (as below)
+        const int b = t == 5 ? 22 + ntypes : 2 + 4 * t, n = t == 5 ? K - 23 - ntypes : 4;
+        uint64_t v = b >= 64 ? hi >> (b - 64) : ((lo >> b) | (hi << (64 - b)));  // b >= 6 here
+        v &= n >= 64 ? ~0ull : ((1ull << n) - 1);
+        pv = pickBit(ctr[1], v, 64);
+    }
+    if (t == 4) ut = pickBit32(ctr[2], (uint32_t)(lo >> 22) & ((1u << ntypes) - 1u));
+    a[0] = t > 0 ? t : 0;
+    a[1] = t == 1 ? pv : 0;
+    a[2] = t == 2 ? pv : 0;
+    a[3] = t == 3 ? pv : 0;
+    a[4] = t == 4 ? pv : 0;
+    a[5] = ut;
+    a[6] = t == 5 ? pv : 0;
+    if (packed)
+        *packed = FWD_ZERO + (uint32_t)(t > 0 ? t : 0) + (t > 0 ? (uint32_t)pv << (t == 5 ? 19 : 3 * t) : 0u) +
+                  ((uint32_t)ut << 15);
+#else
     for (int k = 0; k < 7; k++) a[k] = 0;
     uint32_t ctr[4] = {slotId, step, (uint32_t)c, 0u};
     philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -416,7 +461,10 @@ DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes
         return n >= 64 ? v : (v & ((1ull << n) - 1));
     };
     const int t = pickBit(ctr[0], field(1, 6), 6);
-    if (t < 0) return;
+    if (t < 0) {
+        if (packed) *packed = FWD_ZERO;
+        return;
+    }
     a[0] = t;
 #if MRTS_SAMPLE_UNIFIED
     // the parameter of type t from ONE pick over that type's field (move / harvest / return / produce
@@ -447,6 +495,8 @@ DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes
             a[6] = pickBit(ctr[1], field(off, n), n);
         } break;
     }
+#endif
+    if (packed) *packed = packFwdFree(a);
 #endif
 }
 
@@ -2707,7 +2757,8 @@ struct Game {
                 if (q >= npl) break;
                 int w[4];
 #pragma unroll
-                for (int j = 0; j < 4; j++) w[j] = (i && q == 2 && v[q][j]) ? 3 - v[q][j] : v[q][j];  // the other player's owners
+                for (int j = 0; j < 4; j++)  // the other player's owners: 0, 1, 2 -> 0, 2, 1 (bits 2v.. of 0b011000)
+                    w[j] = (i && q == 2) ? (int)__builtin_amdgcn_ubfe(24u, 2u * (uint32_t)v[q][j], 2u) : v[q][j];
                 const uint32_t off = (uint32_t)((i * D.C + q) * HW + c4);
                 if (SC1_OBS) st4sc1(rs, off * 4u, w[0], w[1], w[2], w[3]);
                 else st4<WT_OBS>(o0 + off, w[0], w[1], w[2], w[3]);
@@ -4450,17 +4501,18 @@ struct Game {
                     keepv(a2[0] + a2[1] + a2[2] + a2[3] + a2[4] + a2[5] + a2[6]);
                 }
 #endif
+                uint32_t pk;
                 sampleBitsRaw(D.pol_seed, polStep, D.pol_slot_base + (uint32_t)slot, NT, K, (lo >> 1) | ((uint64_t)w2 << 63),
-                              (uint64_t)(w2 >> 1), c, a);
+                              (uint64_t)(w2 >> 1), c, a, &pk);
                 if (recOut) {
-                    recOut[256 + l] = packFwd(a);
+                    recOut[256 + l] = pk;
                 } else {
                     int32_t* dst = D.pol_actions + ((size_t)slot * HW + c) * 7;
                     st4u<WT_MASK>(dst, a[0], a[1], a[2], a[3]);
                     st3u<WT_MASK>(dst + 4, a[4], a[5], a[6]);
                 }
                 if (fwdW) {
-                    lfwd = packFwd(a);  // the next iteration of a multi-step launch decodes from it
+                    lfwd = pk;  // packFwd(a): the next iteration of a multi-step launch decodes from it
                     if (lastIt) st1<WT_STATE>(st() + stateFwdOff(CAP, HW) + l, (int32_t)lfwd);  // the next launch's
                 }
             }
