@@ -185,6 +185,15 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SAMPLE32  // the sampler's type / produce-type picks in 32-bit operations, the packed word direct (round 5)
 #define MRTS_SAMPLE32 1
 #endif
+#ifndef MRTS_INDEX_WALK  // buildIndex's PRODUCE costs by a walk over their lanes (round 5); 0 = wave reductions
+#define MRTS_INDEX_WALK 1
+#endif
+#ifndef MRTS_PICK_SPLIT  // the sampler's direction picks as 32-bit picks apart from the attack pick (round 5)
+#define MRTS_PICK_SPLIT 1
+#endif
+#ifndef MRTS_ETA_FLAT  // cycleLanes' ready test with the branch-free duration lookup (round 5)
+#define MRTS_ETA_FLAT 1
+#endif
 #ifndef MRTS_XOR3  // Philox's xors as one three-input bit op (round 5); 0 = plain C
 #define MRTS_XOR3 1
 #endif
@@ -431,10 +440,14 @@ DEV void sampleBitsRaw(uint64_t seed, uint32_t step, uint32_t slotId, int ntypes
     // types bits 22.., the direction fields bits 6 + 4 (t - 1).., the attack window bits 22 + ntypes..
     const int t = pickBit32(ctr[0], (uint32_t)lo & 63u);
     int pv = 0, ut = 0;
-    if (t > 0) {
-        // the parameter of type t from ONE pick over that type's field (as below)
+    if (MRTS_PICK_SPLIT && t > 0 && t < 5) {
+        // a direction: 4 bits at 2 + 4 t (below 32) — one 32-bit pick
+        pv = pickBit32(ctr[1], ((uint32_t)lo >> (2 + 4 * t)) & 15u);
+    } else if (t > 0) {
+        // the attack window: K - 23 - ntypes bits from 22 + ntypes (across lo / hi); without
+        // MRTS_PICK_SPLIT every type's field in this one 64-bit pick
         const int b = t == 5 ? 22 + ntypes : 2 + 4 * t, n = t == 5 ? K - 23 - ntypes : 4;
-        uint64_t v = b >= 64 ? hi >> (b - 64) : ((lo >> b) | (hi << (64 - b)));  // b >= 6 here
+        uint64_t v = b >= 64 ? hi >> (b - 64) : ((lo >> b) | (hi << (64 - b)));
         v &= n >= 64 ? ~0ull : ((1ull << n) - 1);
         pv = pickBit(ctr[1], v, 64);
     }
@@ -655,6 +668,10 @@ struct Game {
     DEV void helperLane() { asm volatile("" : "=v"(lidv) : "0"((int)threadIdx.x - 64)); }
     bool ixValid;
     bool anyMP;
+    // the PRODUCE costs of the issue index, the batch and the candidates summed by a walk over their
+    // lanes instead of whole-wave reductions (the masked-policy 16x16 instances: few PRODUCE lanes;
+    // c2's uniform rows make many, where the reductions are cheaper; round 5)
+    bool walk;
     uint32_t lcu, lua;     // load(): lane l's unit core / assignment words (units 0..63) as loaded
     uint32_t lfwd;         // load(): lane l's forwarded action word (KDyn.fwd_read)
     bool fwdOn;            // this game's forwarded action words are current (H_FWD == fwd_stamp - 1)
@@ -683,9 +700,9 @@ struct Game {
     // h, w, hw, cap: the map dimensions — compile-time constants in a specialised kernel (every LDS
     // array offset then folds to an immediate), else the kernel arguments
     DEV Game(const KStatic& p, const KDyn& d /* k_env's argument D; other fields read through kdynArg */, int32_t* stb, int stw, uint8_t* smem, int h, int w, int hw, int cap, bool partial,
-             int k, int nt, int r, bool iterating = false, int game = -1)
+             int k, int nt, int r, bool iterating = false, int game = -1, bool walk = false)
         : P(p), Dp(kdynArg(false)), U(*(const DevUtt*)smem), g(game >= 0 ? game : (int)blockIdx.x), H(h), W(w), HW(hw), CAP(cap), K(k), NT(nt), R(r),
-          po(partial), iter(iterating), stBase(stb), stWords(stw) {
+          po(partial), iter(iterating), stBase(stb), stWords(stw), walk(walk) {
         uint8_t* q = smem + UTT_LDS;  // the unit-type table copy comes first (see copyUtt)
         uc = (uint32_t*)q; q += 4 * CAP;
         ua = (uint32_t*)q; q += 4 * CAP;
@@ -755,6 +772,20 @@ struct Game {
             case T_PRODUCE: return U.produceT[ut];
         }
         return 0;
+    }
+    // eta without the per-type branches (lane-varying t: the switch ran each case under its own exec mask):
+    // produceT, moveT, attackT, harvestT are consecutive MAX_TYPES arrays of DevUtt, so the duration is one
+    // LDS read at [array(t)][t == PRODUCE ? ut : unitType]; NONE keeps its parameter, unknown types 0
+    DEV int etaFlat(int t, int prm, int ut, int unitType) const {
+        static_assert(offsetof(DevUtt, moveT) == offsetof(DevUtt, produceT) + 4 * MAX_TYPES &&
+                          offsetof(DevUtt, attackT) == offsetof(DevUtt, produceT) + 8 * MAX_TYPES &&
+                          offsetof(DevUtt, harvestT) == offsetof(DevUtt, produceT) + 12 * MAX_TYPES,
+                      "DevUtt duration arrays");
+        // array per type (4 bits each): MOVE moveT (1), HARVEST harvestT (3), RETURN moveT (1), PRODUCE produceT (0),
+        // ATTACK attackT (2)
+        const int arr = (int)((0x201310u >> (4 * (t & 7))) & 15u);
+        const int v = U.produceT[arr * MAX_TYPES + (t == T_PRODUCE ? ut : unitType)];
+        return t == T_NONE ? prm : (t <= T_ATTACK ? v : 0);
     }
     DEV int etaSlot(int s) const {
         const uint32_t a = ua[s];
@@ -1479,7 +1510,12 @@ struct Game {
                     const int tk = rl(tpos, k);  // read in uniform flow: lane k itself is off inside the test below
                     if (up && k != l && tk == tpos) conf = true;
                 }
-                const int sumc = ballot(cand && cost > 0) ? wave_sum(cand ? cost : 0) : 0;
+                int sumc = 0;
+                if (walk) {  // the candidates' PRODUCE costs (a few lanes): one lane read each
+                    for (uint64_t mm = ballot(cand && cost > 0); mm; mm &= mm - 1) sumc += uni(rl(cost, __builtin_ctzll(mm)));
+                } else if (ballot(cand && cost > 0)) {
+                    sumc = wave_sum(cand ? cost : 0);
+                }
                 if (!ballot(conf) && runP + sumc <= presP) {
                     if (p == 0) run0 = runP + sumc;
                     else run1 = runP + sumc;
@@ -1759,36 +1795,74 @@ struct Game {
         for (int i = lid(); i < NB; i += 64) bits[i] = 0;
         wsync();
         bool mp = false;
-        int mc0 = -1, mc1 = -1, s0 = 0, s1 = 0;
-        for (int o = lid(); o < nu; o += 64) {
-            const uint32_t a = ua[o];
-            const int t = ua_type(a);
-            if (!(a & UA_PRESENT) || (t != T_MOVE && t != T_PRODUCE)) continue;
-            mp = true;
-            const uint32_t c = uc[o];
-            const int d = par[o];
-            const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
-            atomicOr(&bits[pos >> 5], 1u << (pos & 31));
-            if (t == T_PRODUCE) {
-                const int k = U.cost[ua_ut(a)];
-                if (uplay(c) == 0) {
-                    mc0 = max(mc0, k);
-                    s0 += k;
-                } else {
-                    mc1 = max(mc1, k);
-                    s1 += k;
+        if (walk) {
+            // the present PRODUCEs' costs per player (largest, sum) by walking their few lanes: one lane read
+            // each (cost | player << 16), scalar max / add, instead of four whole-wave reductions
+            int mc0 = -1, mc1 = -1, s0 = 0, s1 = 0;
+            for (int o0 = 0; o0 < nu; o0 += 64) {
+                const int o = o0 + lid();
+                int key = -1;
+                if (o < nu) {
+                    const uint32_t a = ua[o];
+                    const int t = ua_type(a);
+                    if ((a & UA_PRESENT) && (t == T_MOVE || t == T_PRODUCE)) {
+                        mp = true;
+                        const uint32_t c = uc[o];
+                        const int d = par[o];
+                        const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
+                        atomicOr(&bits[pos >> 5], 1u << (pos & 31));
+                        if (t == T_PRODUCE) key = U.cost[ua_ut(a)] | ((uplay(c) == 0 ? 0 : 1) << 16);
+                    }
+                }
+                for (uint64_t mm = ballot(key >= 0); mm; mm &= mm - 1) {
+                    const int kv = uni(rl(key, __builtin_ctzll(mm)));
+                    const int k = kv & 0xFFFF;
+                    if ((kv >> 16) == 0) {
+                        mc0 = max(mc0, k);
+                        s0 += k;
+                    } else {
+                        mc1 = max(mc1, k);
+                        s1 += k;
+                    }
                 }
             }
-        }
-        anyMP = ballot(mp) != 0;
-        if (ballot(mc0 >= 0 || mc1 >= 0)) {  // any present PRODUCE (rare)
-            maxProd0 = -wave_min(-mc0);
-            maxProd1 = -wave_min(-mc1);
-            sumProd0 = wave_sum(s0);
-            sumProd1 = wave_sum(s1);
+            anyMP = ballot(mp) != 0;
+            maxProd0 = mc0;
+            maxProd1 = mc1;
+            sumProd0 = s0;
+            sumProd1 = s1;
         } else {
-            maxProd0 = maxProd1 = -1;
-            sumProd0 = sumProd1 = 0;
+            int mc0 = -1, mc1 = -1, s0 = 0, s1 = 0;
+            for (int o = lid(); o < nu; o += 64) {
+                const uint32_t a = ua[o];
+                const int t = ua_type(a);
+                if (!(a & UA_PRESENT) || (t != T_MOVE && t != T_PRODUCE)) continue;
+                mp = true;
+                const uint32_t c = uc[o];
+                const int d = par[o];
+                const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
+                atomicOr(&bits[pos >> 5], 1u << (pos & 31));
+                if (t == T_PRODUCE) {
+                    const int k = U.cost[ua_ut(a)];
+                    if (uplay(c) == 0) {
+                        mc0 = max(mc0, k);
+                        s0 += k;
+                    } else {
+                        mc1 = max(mc1, k);
+                        s1 += k;
+                    }
+                }
+            }
+            anyMP = ballot(mp) != 0;
+            if (ballot(mc0 >= 0 || mc1 >= 0)) {  // any present PRODUCE (rare)
+                maxProd0 = -wave_min(-mc0);
+                maxProd1 = -wave_min(-mc1);
+                sumProd0 = wave_sum(s0);
+                sumProd1 = wave_sum(s1);
+            } else {
+                maxProd0 = maxProd1 = -1;
+                sumProd0 = sumProd1 = 0;
+            }
         }
         ixValid = true;
         wsync();
@@ -1876,11 +1950,26 @@ struct Game {
             seq += n;
             if (mpm) {
                 anyMP = true;
-                if (ballot(np)) {  // PRODUCE is rare: skip the four reductions otherwise
-                    maxProd0 = max(maxProd0, -wave_min(np && pl == 0 ? -ncost : 1));
-                    maxProd1 = max(maxProd1, -wave_min(np && pl == 1 ? -ncost : 1));
-                    sumProd0 += wave_sum(np && pl == 0 ? ncost : 0);
-                    sumProd1 += wave_sum(np && pl == 1 ? ncost : 0);
+                if (walk) {
+                    // the batch's PRODUCEs (a few lanes): one lane read each, scalar max / add
+                    for (uint64_t mm = ballot(np); mm; mm &= mm - 1) {
+                        const int kv = uni(rl(ncost | (pl << 16), __builtin_ctzll(mm)));
+                        const int k = kv & 0xFFFF;
+                        if ((kv >> 16) == 0) {
+                            maxProd0 = max(maxProd0, k);
+                            sumProd0 += k;
+                        } else if ((kv >> 16) == 1) {
+                            maxProd1 = max(maxProd1, k);
+                            sumProd1 += k;
+                        }
+                    }
+                } else {
+                    if (ballot(np)) {  // PRODUCE is rare: skip the four reductions otherwise
+                        maxProd0 = max(maxProd0, -wave_min(np && pl == 0 ? -ncost : 1));
+                        maxProd1 = max(maxProd1, -wave_min(np && pl == 1 ? -ncost : 1));
+                        sumProd0 += wave_sum(np && pl == 0 ? ncost : 0);
+                        sumProd1 += wave_sum(np && pl == 1 ? ncost : 0);
+                    }
                 }
             }
             wsync();
@@ -2499,7 +2588,7 @@ struct Game {
             prm = par[l];
             sq = as[l];
             const int t0 = at[l];
-            if (a & UA_PRESENT) ready = eta(ua_type(a), prm, ua_ut(a), utyp(cu)) + t0 <= time;
+            if (a & UA_PRESENT) ready = (MRTS_ETA_FLAT ? etaFlat(ua_type(a), prm, ua_ut(a), utyp(cu)) : eta(ua_type(a), prm, ua_ut(a), utyp(cu))) + t0 <= time;
         }
         if (ready) ua[l] = a & ~(UA_READY | UA_PRESENT);
         const bool wk = ready && ua_type(a) != T_NONE;
@@ -4888,7 +4977,8 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
     const bool rebalance = balanced && D.n_iter >= MRTS_BAL_MIN_ITER;  // this launch writes the next permutation
     const int game = balanced ? balancedGame(D) : -1;
     Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
-           FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI, game);
+           FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI, game,
+           MRTS_INDEX_WALK && FIX == 16);
     // the partially observable helper wave: one packed render per step (helperLoopPO)
     uint32_t* const poHelpHdr = (HELP && FPO) ? (uint32_t*)(smem + D.help_off) : nullptr;
     if (HELP && FPO && threadIdx.x >= 64) {
