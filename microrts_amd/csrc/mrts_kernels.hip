@@ -194,6 +194,12 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_ETA_FLAT  // cycleLanes' ready test with the branch-free duration lookup (round 5)
 #define MRTS_ETA_FLAT 1
 #endif
+#ifndef MRTS_DECODE_FWD  // selfPlayFast decodes forwarded words directly (decodeFwd, round 5)
+#define MRTS_DECODE_FWD 0
+#endif
+#ifndef MRTS_CONF_LDS  // acceptChainReg's parallel-path conflict test through an LDS copy of the reservations (round 5)
+#define MRTS_CONF_LDS 0
+#endif
 #ifndef MRTS_XOR3  // Philox's xors as one three-input bit op (round 5); 0 = plain C
 #define MRTS_XOR3 1
 #endif
@@ -1044,8 +1050,8 @@ struct Game {
         int32_t a[7] = {0, 0, 0, 0, 0, 0, 0};
         if (fwdOn) {
             // the previous launch's fused policy sampled this unit's row (the values it wrote to the
-            // action tensor at this cell) and forwarded it in the state block
-            if (idle) unpackFwd(lfwd, a);
+            // action tensor at this cell) and forwarded it in the state block (decoded below)
+            if (!MRTS_DECODE_FWD && idle) unpackFwd(lfwd, a);
         } else if (idle) {
             fetchRow(pl == 0 ? rows0 : rows1, s0 + pl, uy(cu) * W + ux(cu), a);
         }
@@ -1066,7 +1072,7 @@ struct Game {
             keepv(t2 + pr2 + ut2 + tx2 + ty2 + (int)bad2);
         }
 #endif
-        if (idle) bad = decodeFields(cu, a, t, pr, ut, tx, ty);
+        if (idle) bad = (MRTS_DECODE_FWD && fwdOn) ? decodeFwd(cu, lfwd, t, pr, ut, tx, ty) : decodeFields(cu, a, t, pr, ut, tx, ty);
         if (ballot(bad)) addErr(E_PRODUCE_TYPE);
         const uint32_t adec = pack_ua(t, ut, tx, ty);
         const int c = uy(cu) * W + ux(cu);
@@ -1219,6 +1225,26 @@ struct Game {
     // with core word cu
     // Branch-free (selects only): the lanes of one wave hold rows of every type, and a divergent switch
     // runs each present case's instructions for the whole wave.
+    // decodeFields(cu, unpackFwd(w)) straight from a forwarded action word: the direction field picked by
+    // the type with one bit-field extract instead of unpacking all seven values and selecting among them
+    DEV bool decodeFwd(uint32_t cu, uint32_t w, int& t, int& pr, int& ut, int& tx, int& ty) const {
+        const int ctr = R / 2;
+        const int x = ux(cu), y = uy(cu);
+        const int a0 = (int)(w & 7u);
+        t = a0 <= 5 ? a0 : ACT_INVALID;
+        const bool dirT = t >= T_MOVE && t <= T_PRODUCE;
+        const int d = (int)__builtin_amdgcn_ubfe(w, 3u * (uint32_t)(dirT ? t : T_PRODUCE), 3u) - 1;  // a[t] (a[4] otherwise)
+        pr = dirT ? clampdir(d) : -1;
+        const bool prod = t == T_PRODUCE;
+        const int a5 = (int)((w >> 15) & 15u) - 1, a6 = (int)((w >> 19) & 127u) - 1;
+        const bool badType = a5 < 0 || a5 >= NT;
+        ut = (prod && !badType) ? a5 : 0;
+        const int ax = x + (a6 % R - ctr), ay = y + (a6 / R - ctr);
+        const bool att = t == T_ATTACK, on = inb(ax, ay);
+        tx = att ? (on ? ax : 255) : 0;
+        ty = att ? (on ? ay : 255) : 0;
+        return prod && badType;
+    }
     DEV bool decodeFields(uint32_t cu, const int32_t a[7], int& t, int& pr, int& ut, int& tx, int& ty) const {
         const int ctr = R / 2;
         const int x = ux(cu), y = uy(cu);
@@ -1504,11 +1530,23 @@ struct Game {
             const int runP = p == 0 ? run0 : run1;
             const bool cand = rank >= 0, up = cand && usesPos;
             if (!(runQ != 0 && runQ > 0 && runQ > presQ)) {
-                bool conf = up && ((bits[tpos >> 5] >> (tpos & 31)) & 1u);
-                for (uint64_t mm = ballot(up); mm; mm &= mm - 1) {
-                    const int k = __builtin_ctzll(mm);
-                    const int tk = rl(tpos, k);  // read in uniform flow: lane k itself is off inside the test below
-                    if (up && k != l && tk == tpos) conf = true;
+                bool conf = false;
+                if (MRTS_CONF_LDS) {
+                    // reserved already, or used by another candidate: each candidate ORs its position into a
+                    // copy of the reservation words (rseq, free here) and is in conflict when the bit was set —
+                    // by the base reservations or by another candidate (one of each equal pair sees it)
+                    uint32_t* cp = (uint32_t*)rseq;
+                    if (l < NB) cp[l] = bits[l];
+                    wsync();
+                    if (up) conf = (atomicOr(&cp[tpos >> 5], 1u << (tpos & 31)) >> (tpos & 31)) & 1u;
+                    wsync();
+                } else {
+                    conf = up && ((bits[tpos >> 5] >> (tpos & 31)) & 1u);
+                    for (uint64_t mm = ballot(up); mm; mm &= mm - 1) {
+                        const int k = __builtin_ctzll(mm);
+                        const int tk = rl(tpos, k);  // read in uniform flow: lane k itself is off inside the test below
+                        if (up && k != l && tk == tpos) conf = true;
+                    }
                 }
                 int sumc = 0;
                 if (walk) {  // the candidates' PRODUCE costs (a few lanes): one lane read each
