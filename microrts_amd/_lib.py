@@ -17,10 +17,31 @@ ERR_BITS = {
     1 << 4: "NEG_RESOURCES", 1 << 5: "MOVE_COLLISION", 1 << 6: "RECORD",
 }
 
+def _code_sections(obj):
+    """The .text and .rodata sections (the kernels' machine code and kernel descriptors) of an amdgcn code
+    object, concatenated: what the kernels run, without the symbol tables (hipcc's per-compile __hip_cuid_*
+    symbol differs between builds of the same source under different -D flags)."""
+    import struct
+
+    shoff = struct.unpack_from("<Q", obj, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", obj, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQ", obj, shoff + i * shentsize) for i in range(shnum)]
+    stroff = secs[shstrndx][4]
+    out = b""
+    for want in (b".text", b".rodata"):
+        for name, _, _, _, off, size in secs:
+            if obj[stroff + name:obj.index(b"\0", stroff + name)] == want:
+                out += obj[off:off + size]
+    if not out:
+        raise RuntimeError("amdgcn code object without .text")
+    return out
+
+
 def device_code_sha256(path=None):
-    """SHA-256 of the gfx950 code object inside libmrts.so (the .hip_fatbin offload bundle's amdgcn entry):
-    the kernels' machine code.  Counter files (profiles/pmc_*.json) name the code they describe with it,
-    so a host-only change to the library keeps them valid and any kernel change voids them."""
+    """SHA-256 of the gfx950 code inside libmrts.so (the .hip_fatbin offload bundle's amdgcn entry): its
+    .text and .rodata, the kernels' machine code and descriptors.  Counter files (profiles/pmc_*.json) name
+    the code they describe with it, so a host-only change to the library keeps them valid and any kernel
+    change voids them."""
     import hashlib
     import struct
 
@@ -42,7 +63,7 @@ def device_code_sha256(path=None):
             triple = b[p:p + tl].decode()
             p += tl
             if "amdgcn" in triple:
-                return hashlib.sha256(b[eoff:eoff + esize]).hexdigest()
+                return hashlib.sha256(_code_sections(b[eoff:eoff + esize])).hexdigest()
     raise RuntimeError(f"{path or LIB_PATH}: no amdgcn code object in .hip_fatbin")
 
 

@@ -195,10 +195,10 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #define MRTS_ETA_FLAT 1
 #endif
 #ifndef MRTS_DECODE_FWD  // selfPlayFast decodes forwarded words directly (decodeFwd, round 5)
-#define MRTS_DECODE_FWD 0
+#define MRTS_DECODE_FWD 1
 #endif
 #ifndef MRTS_CONF_LDS  // acceptChainReg's parallel-path conflict test through an LDS copy of the reservations (round 5)
-#define MRTS_CONF_LDS 0
+#define MRTS_CONF_LDS 1
 #endif
 #ifndef MRTS_XOR3  // Philox's xors as one three-input bit op (round 5); 0 = plain C
 #define MRTS_XOR3 1
