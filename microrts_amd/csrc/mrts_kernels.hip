@@ -200,9 +200,6 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_CONF_LDS  // acceptChainReg's parallel-path conflict test through an LDS copy of the reservations (round 5)
 #define MRTS_CONF_LDS 1
 #endif
-#ifndef MRTS_ACCEPT_BASE  // acceptChainReg accepts in parallel when every conflict is with the base reservations
-#define MRTS_ACCEPT_BASE 0
-#endif
 #ifndef MRTS_XOR3  // Philox's xors as one three-input bit op (round 5); 0 = plain C
 #define MRTS_XOR3 1
 #endif
@@ -1533,7 +1530,7 @@ struct Game {
             const int runP = p == 0 ? run0 : run1;
             const bool cand = rank >= 0, up = cand && usesPos;
             if (!(runQ != 0 && runQ > 0 && runQ > presQ)) {
-                bool conf = false, inBase = false;
+                bool conf = false;
                 if (MRTS_CONF_LDS) {
                     // reserved already, or used by another candidate: each candidate ORs its position into a
                     // copy of the reservation words (rseq, free here) and is in conflict when the bit was set —
@@ -1541,10 +1538,7 @@ struct Game {
                     uint32_t* cp = (uint32_t*)rseq;
                     if (l < NB) cp[l] = bits[l];
                     wsync();
-                    if (up) {
-                        inBase = (bits[tpos >> 5] >> (tpos & 31)) & 1u;
-                        conf = (atomicOr(&cp[tpos >> 5], 1u << (tpos & 31)) >> (tpos & 31)) & 1u;
-                    }
+                    if (up) conf = (atomicOr(&cp[tpos >> 5], 1u << (tpos & 31)) >> (tpos & 31)) & 1u;
                     wsync();
                 } else {
                     conf = up && ((bits[tpos >> 5] >> (tpos & 31)) & 1u);
@@ -1567,28 +1561,6 @@ struct Game {
                     if (cand) irank = rank;
                     wsync();
                     return ballot(cand);
-                }
-                // Every conflict with the base reservations only (no two candidates share a position), no
-                // PRODUCE among the rejected and the costs fit: the sequential chain rejects exactly the
-                // candidates whose position is reserved (each test below reads the base bits and the earlier
-                // accepted positions, which no other candidate shares) and accepts the rest — in parallel
-                // (round 5, MRTS_ACCEPT_BASE)
-                if (MRTS_CONF_LDS && MRTS_ACCEPT_BASE && !ballot(conf && !inBase) && !ballot(inBase && cost > 0) &&
-                    runP + sumc <= presP) {
-                    const bool acc = cand && !inBase;
-                    if (p == 0) run0 = runP + sumc;
-                    else run1 = runP + sumc;
-                    if (!keepBits && acc && up) atomicOr(&bits[tpos >> 5], 1u << (tpos & 31));
-                    // rank among the accepted: the rank minus the rejected ranked below (lane reads in uniform
-                    // flow: the rejected lanes are off inside `if (acc)`)
-                    int ir = rank;
-                    for (uint64_t mm = ballot(cand && inBase); mm; mm &= mm - 1) {
-                        const int rk = rl(rank, __builtin_ctzll(mm));
-                        if (rk < rank) ir--;
-                    }
-                    if (acc) irank = ir;
-                    wsync();
-                    return ballot(acc);
                 }
             }
         }
