@@ -1344,7 +1344,7 @@ struct Game {
     // [player, x, y, type, parameter, target x, target y, unit type], the player's rows in the given
     // order.  Each action's legality is judged on the trace's own Unit object, whose fields equal those
     // of the state's unit at (x, y) whenever the replay is in sync; that unit is then the one issued —
-    // the first unit at (x, y) in list order (:356-382; one unit per cell).  No fillWithNones.
+    // the first unit at (x, y) in list order (GameState.java:356-382; one unit per cell).  No fillWithNones.
     // Returns issue()'s value: a pair was put with a type other than NONE.
     DEV bool traceIssue(int p, const int32_t* rows, int n, uint32_t& flags) {
         curP = p;
@@ -2281,7 +2281,7 @@ struct Game {
 
     // ------------------------------------------------------------------ PO snapshot
     // new PartiallyObservableGameState(gs, p) (rts/PartiallyObservableGameState.java:35-54):
-    // the list keeps p's units and every other unit whose cell p observes (:116-126); the
+    // the list keeps p's units and every other unit whose cell p observes (`observable`, :61-71); the
     // assignment map is the live one at this moment (UAA objects shared).
     // Sight disks (dx^2 + dy^2 <= sightRadius^2 of the seeing unit's type) painted into per-row bitmaps:
     // lane = seeing unit, one atomicOr per covered row word; a cell is seen iff its bit is set.
@@ -3149,7 +3149,7 @@ struct Game {
     }
     // PartiallyObservableGameState.getVectorObservation (rts/PartiallyObservableGameState.java:82-154):
     // the snapshot's units (live fields, possibly dead) in list order, last writer per cell; the
-    // snapshot's assignments; walls; own / enemy sight disks of the snapshot units (:211-234).
+    // snapshot's assignments; walls; own / enemy sight disks of the snapshot units (calculateVisibility, :156-179).
     // delta: the buffer holds this game's view-p render of the previous observation write and the PO
     // record (poVis / poPend / lsnap) describes it.  A cell's planes 0-5 come from the last snapshot
     // unit on it (its current hp, resources, owner, type and snapshot assignment), planes 6-7 from

@@ -653,7 +653,7 @@ int oref_botclient_set_rewards(void* h, const int32_t* kinds, int n) {
     b->rfs.assign(kinds, kinds + n);
     return 0;
 }
-// JNIBotClient.gameStep (:108-135) + VecClient bot-only auto-reset (:214-238); returns 0
+// JNIBotClient.gameStep (:108-135) + VecClient bot-only auto-reset (JNIGridnetVecClient.java:214-238); returns 0
 int oref_botclient_step(void* h, int player, double* reward, uint8_t* done) {
     try {
         auto b = (BotVec*)h;

@@ -581,7 +581,7 @@ void PlayerAction::fillWithNones(const GameState& s, int pID, int duration) {  /
         }
     }
 }
-bool PlayerAction::integrityCheck() const {  // :355-370
+bool PlayerAction::integrityCheck() const {  // :244-259
     int player = -1;
     for (auto& p : actions) {
         if (player == -1) player = p->m_a->player;
@@ -786,7 +786,7 @@ PartiallyObservableGameState::PartiallyObservableGameState(const GameState& gs, 
             if (!observable(u->x, u->y)) toDelete.push_back(u.get());
     for (const Unit* u : toDelete) removeUnit(u);
 }
-bool PartiallyObservableGameState::observable(int x, int y) const {  // :116-126
+bool PartiallyObservableGameState::observable(int x, int y) const {  // :61-71
     for (auto& u : pgs->units) {
         if (u->player == observer) {
             int d = (u->x - x) * (u->x - x) + (u->y - y) * (u->y - y);
@@ -795,7 +795,7 @@ bool PartiallyObservableGameState::observable(int x, int y) const {  // :116-126
     }
     return false;
 }
-static void calculateVisibility(const std::vector<std::array<int, 3>>& us, int W, int H, int32_t* vis) {  // :211-234
+static void calculateVisibility(const std::vector<std::array<int, 3>>& us, int W, int H, int32_t* vis) {  // :156-179
     for (auto& un : us) {
         int ux = un[0], uy = un[1], sr = un[2], sr2 = sr * sr;
         for (int dy = -sr; dy <= sr; dy++)

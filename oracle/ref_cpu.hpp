@@ -192,7 +192,7 @@ struct PlayerAction {
     void addUnitAction(const UnitP& u, const UnitActionP& a) { actions.push_back(std::make_shared<Pair>(Pair{u, a})); }
     bool isEmpty() const { return actions.empty(); }
     void fillWithNones(const GameState& s, int pID, int duration);  // :217-235
-    bool integrityCheck() const;                                    // :355-370
+    bool integrityCheck() const;                                    // :244-259
     static PlayerAction fromVectorAction(const std::vector<int>& rows, int nrows, const GameState& gs,
                                          const UnitTypeTable& utt, int currentPlayer, int maxAttackRadius);
 };
@@ -226,7 +226,7 @@ struct GameState {
     bool integrityCheck() const;       // :703-719
     bool gameover() const { return pgs->gameover(); }
     int winner() const { return pgs->winner(); }
-    // :922-968; out = int32[C][H][W]
+    // GameState.java:922-968; out = int32[C][H][W]
     virtual void getVectorObservation(int player, int32_t* out) const;
     virtual int numObservationPlanes() const { return 6; }
 };
@@ -236,7 +236,7 @@ using GSP = std::shared_ptr<GameState>;
 struct PartiallyObservableGameState : GameState {
     int observer;
     PartiallyObservableGameState(const GameState& gs, int a_player);  // :35-54
-    bool observable(int x, int y) const override;                      // :116-126
+    bool observable(int x, int y) const override;                      // :61-71
     void getVectorObservation(int player, int32_t* out) const override;  // :82-154
     int numObservationPlanes() const override { return 8; }
 };
