@@ -102,6 +102,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=None,
                     help="threads of the all-cores CPU baseline (default: every CPU this process may use, capped by "
                          "the cgroup's CPU quota)")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="c3 at N = 1: skip the c2 and c5 sub-blocks (each BASELINE single-GPU config run as a child "
+                         "bench.py with the same K / W, its line nested under configs)")
     ap.add_argument("--pmc-traffic", type=float, default=None,
                     help="HBM bytes per step-kernel launch from a rocprofv3 --pmc pass (profiles/), for roofline.traffic")
     a = ap.parse_args()
@@ -420,35 +423,44 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
     e1.record(cur)
     torch.cuda.synchronize(env.device)
     render_ms = e0.elapsed_time(e1) / n_r
-    # the render of an 8-rank step on this one GPU (every "rank" reads this rank's records: rank stride 0) —
-    # what each rank of c4 writes per step if it materialises every rank's observations
+    # the render of an 8-rank step on this one GPU — what each rank of c4 writes per step if it materialises every
+    # rank's observations — over an 8-rank receive buffer laid out as one chunk of an 8-rank all-gather
+    # ([rank][step][game][words], rank stride K x games x words): rank r's place holds this rank's records of each
+    # step with the games rotated by r (a rank stride of 0 would read one rank's records 8 times, cache-hot)
+    K = a.steps
+    G2, per = S // 2, (S // 2) * rx.words
+    own = torch.stack([rx.recv[int(off[j][0]):int(off[j][0]) + per] for j in range(K)]).view(K, G2, rx.words)
+    rx8 = torch.empty((8, K, G2, rx.words), dtype=torch.int32, device=env.device)
+    for r in range(8):
+        rx8[r] = torch.roll(own, -r, 1)
+    rx8 = rx8.view(-1)
+    del own
     out8r = torch.zeros((8 * S,) + tuple(env.obs.shape[1:]), dtype=b8, device=env.device)
-    o0, _ = off[0]
-    env.render_records(rx.recv, int(o0), 0, 8, out8r)
+    env.render_records(rx8, 0, K * per, 8, out8r)
     e0.record(cur)
     for j in range(n_r):
-        env.render_records(rx.recv, int(off[j][0]), 0, 8, out8r)
+        env.render_records(rx8, j * per, K * per, 8, out8r)
     e1.record(cur)
     torch.cuda.synchronize(env.device)
     render8_ms = e0.elapsed_time(e1) / n_r
     del out8r
     # a learner's batch in MicroRTS-Py's one-hot layout straight from the records: B random
-    # slots of the 8-rank volume per step (every "rank" reads this rank's records: rank stride 0)
+    # slots of the 8-rank volume per step, from the same 8-rank buffer
     onehot = {}
     if not a.po:
         gsel = torch.Generator(device="cpu").manual_seed(1)
-        K = a.steps
         for B in (1024, 2048, S):  # per step; one launch for the window's K steps
             sel = torch.randint(0, 8 * S, (K * B,), generator=gsel).to(torch.int32).to(env.device)
-            so = torch.tensor([[int(off[j][0]), 0] for j in range(K) for _ in range(B)], dtype=torch.int64, device=env.device)
-            oh = env.render_records_onehot(rx.recv, 0, 0, sel, step_off=so)
+            so = torch.tensor([[j * per, K * per] for j in range(K) for _ in range(B)], dtype=torch.int64, device=env.device)
+            oh = env.render_records_onehot(rx8, 0, 0, sel, step_off=so)
             e0.record(cur)
-            env.render_records_onehot(rx.recv, 0, 0, sel, oh, step_off=so)
+            env.render_records_onehot(rx8, 0, 0, sel, oh, step_off=so)
             e1.record(cur)
             torch.cuda.synchronize(env.device)
             us = 1e3 * e0.elapsed_time(e1) / K
             onehot[str(B)] = {"us_per_step": us, "bytes_per_step": oh.numel() / K, "GBps": oh.numel() / K / (us * 1e-6) / 1e9}
             del oh
+    del rx8
     env.set_step_responses(0)
     rec_bytes = (S // 2) * rx.words * 4
     return {
@@ -464,10 +476,13 @@ def records_window(env, a, mode, base, total_games, world, mdist, torch, dist):
         "observation_bytes_per_rank_per_step": {"uint8": env.obs.numel(), "int32": 4 * env.obs.numel()},
         "render_ms_per_step": render_ms,
         "render_ms_per_step_8_ranks": render8_ms,
+        "render_8_ranks_buffer": "one chunk of an 8-rank all-gather: rank r's place = this rank's records rotated by r games, "
+                                 "rank stride K x games x words (not a stride-0 re-read of one rank)",
         "render_GBps_8_ranks": 8 * env.obs.numel() / (render8_ms * 1e-3) / 1e9,
         "onehot_batch": onehot or None,
         "onehot_batch_note": "mrts_render_records_onehot_dev: B random slots of the 8-rank volume at each of the window's K "
-                             "steps, as MicroRTS-Py one-hot uint8 [K x B][H][W][F] (a learner's minibatch), ONE launch, "
+                             "steps (an 8-rank receive buffer: rank r's place = this rank's records rotated by r games, real "
+                             "rank stride), as MicroRTS-Py one-hot uint8 [K x B][H][W][F] (a learner's minibatch), ONE launch, "
                              "timed alone (per step = / K); it does not overlap the step launches, whose waves hold every "
                              "SIMD's VGPRs (4 x 128) and the CUs' LDS (16 x 10 KB): tools/consumer_overlap.py",
         "render": f"mrts_render_records_dev: all {world} ranks' observations of one step rebuilt as {'int8' if a.po else 'uint8'} "
@@ -599,6 +614,34 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
     if traffic is not None:
         out["traffic"] = traffic
     return out
+
+
+def other_configs(a, timeout=240.0):
+    """the other single-GPU BASELINE configs in the driver's own line — c2 (configs[1]: 8x8, 1024
+    games, unmasked uniform rows) and c5 (configs[4] per GPU: 32x32, 2048 partially observable games, masked
+    policy) — each a child bench.py with the same K / W / burn-in, run after this process has released its
+    handle and process group; its JSON line (value, ms_per_step, roofline with the matching-hash PMC file,
+    cpu_baseline, ...) nested under its name.  A child that fails or overruns leaves {"error": ...} there."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    res = {}
+    for cfg in ("c2", "c5"):
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--steps", str(a.steps), "--warmup", str(a.warmup),
+               "--burnin", str(a.burnin)]
+        t0 = time.perf_counter()
+        try:
+            p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout, cwd=ROOT)
+            lines = [ln for ln in p.stdout.decode().splitlines() if ln.startswith("{")]
+            if p.returncode != 0 or not lines:
+                res[cfg] = {"error": f"exit {p.returncode}: {p.stderr.decode()[-400:]}"}
+            else:
+                res[cfg] = json.loads(lines[-1])
+        except subprocess.TimeoutExpired:
+            res[cfg] = {"error": f"timed out after {timeout:.0f} s"}
+        res[cfg]["command"] = " ".join(["python3", "bench.py"] + cmd[2:])
+        res[cfg]["run_s"] = time.perf_counter() - t0
+    return res
 
 
 def main_c1(a, json_fd):
@@ -1075,6 +1118,17 @@ def main():
             "survey_8d_equivalent_GBps": survey / (kern_ms * 1e-3) / 1e9,
         },
     }
+    if traffic:
+        # the PMC bytes against the contract: below it, the outputs rewritten every step stay in L2 / MALL between
+        # launches (c2: 1024 games' planes), so frac is a fraction of the contract's bytes, not of HBM bytes moved
+        rf = out["roofline"]
+        rf["traffic_GBps"] = traffic / (kern_ms * steps_per_launch * 1e-3) / 1e9
+        rf["traffic_frac"] = rf["traffic_GBps"] / HBM_PEAK_GBS
+        rf["traffic_over_contract"] = traffic / (contract * steps_per_launch)
+        rf["frac_basis"] = ("contract bytes (L2-resident: the PMC-measured HBM traffic is {:.2f} of the contract, so the "
+                            "HBM fraction actually moved is traffic_frac)".format(rf["traffic_over_contract"])
+                            if rf["traffic_over_contract"] < 0.8 else "contract bytes (PMC traffic {:.2f} of them)"
+                            .format(rf["traffic_over_contract"]))
     if world == 1 and (native or graph is not None) and gather_buf is None and not a.no_compare and not uniform:
         # the other policy form over the next K steps, for comparison (same contract otherwise)
         mode["fused"] = not fused
@@ -1162,12 +1216,14 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, a.map), a.cpu_threads or all_cores(), a.burnin, uniform, po=a.po,
                                            utt=a.utt)
-    if rank == 0:
-        sys.stdout.flush()
-        os.write(json_fd, (json.dumps(out) + "\n").encode())
     env.close()
     if use_pg:
         dist.destroy_process_group()
+    if rank == 0 and world == 1 and a.config == "c3" and not a.no_other_configs and a.utt == 1 and a.envs == CONFIGS["c3"][1]:
+        out["configs"] = other_configs(a)
+    if rank == 0:
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
 
 
 if __name__ == "__main__":

@@ -239,7 +239,8 @@ int mrts_rollout_uniform_exchange_dev(mrts_env* env, int32_t* d_actions, const i
  * mrts_render_records_dev: records of n_ranks x n_games games (rank r's game g at d_rec + r * rank_stride
  * + g * mrts_record_words words; the terrain of game g from this handle's map of game g) into
  * d_out [n_ranks][2 * n_games][C][H][W] as uint8 (out_bytes 1; int8 for partially observable handles,
- * whose dead units' hp may be negative) or int32 (out_bytes 4, 16-byte aligned). */
+ * whose dead units' hp may be negative) or int32 (out_bytes 4, 16-byte aligned).  rec_words: the words of
+ * d_rec from d_rec on; every rank's records must lie inside them (else -EINVAL). */
 int mrts_set_records(mrts_env* env, int32_t units_per_record, int32_t steps_per_launch);
 int mrts_rollout_fused_records_dev(mrts_env* env, int32_t* d_actions, const int32_t* d_players, int32_t* d_obs,
                                    double* d_reward, uint8_t* d_done, uint8_t* d_masks, int32_t mask_player, uint64_t seed,
@@ -249,8 +250,8 @@ int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const in
                                      double* d_reward, uint8_t* d_done, uint64_t seed, uint32_t first_step, int32_t n_steps,
                                      uint32_t* d_recv, int64_t* step_offsets, void* stream);
 int32_t mrts_record_words(const mrts_env* env);
-int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,
-                            int32_t out_bytes, void* stream);
+int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int64_t rec_words, int32_t n_ranks, int64_t rank_stride,
+                            void* d_out, int32_t out_bytes, void* stream);
 /* A learner's minibatch straight from the records (no Java counterpart: MicroRTS-Py's GridnetVecEnv
  * encoding, gym_microrts `_encode_obs` — clip each plane to its size, one-hot, channels last;
  * mrts_onehot_dev's layout), in ONE launch: sample i is slot d_sel[i] (int32, global index r * n_slots + slot
@@ -259,9 +260,11 @@ int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_rank
  * row of that step; d_step_off NULL: every sample at d_rec with rank_stride) — e.g. random (step, slot) pairs
  * of a whole records rollout.  Out: d_out
  * [n_sel][H][W][F] uint8 (F = mrts_onehot_features, 16-byte aligned).  Full observability (else -ENOTSUP);
- * the render flag of mrts_render_status applies. */
-int mrts_render_records_onehot_dev(mrts_env* env, const uint32_t* d_rec, int64_t rank_stride, const int32_t* d_sel,
-                                   const int64_t* d_step_off, int32_t n_sel, uint8_t* d_out, void* stream);
+ * the render flag of mrts_render_status applies.  rec_words: the words of d_rec from d_rec on, n_ranks: the
+ * ranks it holds — a sample whose index is outside [0, n_ranks x n_slots) or whose record lies outside the
+ * rec_words renders as zeros and raises the render flag (never a read past the buffer). */
+int mrts_render_records_onehot_dev(mrts_env* env, const uint32_t* d_rec, int64_t rec_words, int32_t n_ranks, int64_t rank_stride,
+                                   const int32_t* d_sel, const int64_t* d_step_off, int32_t n_sel, uint8_t* d_out, void* stream);
 /* 1 if a record rendered by this handle since the last call had its overflow bit set (its game held more
  * units than the record, or a value outside the record's range: the rendered observation lacks them —
  * the sender's handle flagged MRTS_ERR_RECORD), else 0; resets the flag.  Synchronises the device. */

@@ -168,9 +168,9 @@ def load(path=LIB_PATH):
     L.mrts_record_words.argtypes = [P]
     L.mrts_rollout_fused_records_dev.argtypes = [P, P, P, P, P, P, P, I32, U64, U32, I32, P, P, P]
     L.mrts_rollout_uniform_records_dev.argtypes = [P, P, P, P, P, P, U64, U32, I32, P, P, P]
-    L.mrts_render_records_dev.argtypes = [P, P, I32, I64, P, I32, P]
+    L.mrts_render_records_dev.argtypes = [P, P, I64, I32, I64, P, I32, P]
     L.mrts_render_status.argtypes = [P]
-    L.mrts_render_records_onehot_dev.argtypes = [P, P, I64, P, P, I32, P, P]
+    L.mrts_render_records_onehot_dev.argtypes = [P, P, I64, I32, I64, P, P, I32, P, P]
     L.mrts_set_step_responses.argtypes = [P, P, P, I32]
     L.mrts_capture_begin.argtypes = [P, P]
     L.mrts_capture_end.argtypes = [P, P]

@@ -45,9 +45,9 @@ hipError_t launchCopyGames(int32_t* dst, const int32_t* src, const int32_t* pair
 hipError_t launchEvaluate(const KStatic& hs, const KStatic* ds, int maxplayer, float* out, hipStream_t stream);
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,
                                int64_t rank_stride, void* out, int out_bytes, int32_t* err, hipStream_t stream);
-hipError_t launchRenderRecordsOneHot(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int64_t rank_stride,
-                                     const int32_t* sel, const int64_t* step_off, int n_sel, uint8_t* out, int32_t* err,
-                                     hipStream_t stream);
+hipError_t launchRenderRecordsOneHot(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int64_t rec_words, int n_ranks,
+                                     int units, int64_t rank_stride, const int32_t* sel, const int64_t* step_off, int n_sel,
+                                     uint8_t* out, int32_t* err, hipStream_t stream);
 }  // namespace mrts
 
 static thread_local std::string g_err;
@@ -1046,6 +1046,9 @@ struct RespScope {
 int mrts_set_step_responses(mrts_env* env, double* d_rewards, uint8_t* d_dones, int32_t max_steps) {
     if (!env) return fail(Fail{-EINVAL, "null handle"});
     if (!d_rewards != !d_dones || (d_rewards && max_steps < 1)) return fail(Fail{-EINVAL, "both rings and max_steps >= 1, or both NULL"});
+    // the kernel forms a ring step's offset as a 32-bit product (it x n_slots x n_rewards)
+    if (d_rewards && (uint64_t)max_steps * (uint64_t)env->nSlots * (uint64_t)env->hstatic.n_rewards >= (1ull << 32))
+        return fail(Fail{-EINVAL, "the Responses ring exceeds 2^32 entries"});
     env->respRew = d_rewards;
     env->respDone = d_dones;
     env->respMax = d_rewards ? max_steps : 0;
@@ -1451,6 +1454,18 @@ int mrts_set_records(mrts_env* env, int32_t units_per_record, int32_t steps_per_
                                 64 * 1024))
         return fail(Fail{-ENOTSUP, "records (partial observability): <= 15 unit types, the receiver's render state and one "
                                    "record in 64 KB of LDS"});
+    try {  // the renders' overflow flag: allocated and zeroed here, never on a render path (a lazy
+           // hipMalloc there would break a stream capture, and a null-stream memset is unordered with a
+           // non-blocking render stream)
+        if (!env->d_renderErr) {
+            HIPCHK(hipSetDevice(env->device));
+            HIPCHK(hipMalloc(&env->d_renderErr, 4));
+            HIPCHK(hipMemset(env->d_renderErr, 0, 4));
+            HIPCHK(hipDeviceSynchronize());
+        }
+    } catch (const Fail& f) {
+        return fail(f);
+    }
     env->recUnits = units_per_record;
     env->recSteps = steps_per_launch;
     return 0;
@@ -1493,20 +1508,17 @@ int mrts_rollout_uniform_records_dev(mrts_env* env, int32_t* d_actions, const in
     }
 }
 
-int mrts_render_records_onehot_dev(mrts_env* env, const uint32_t* d_rec, int64_t rank_stride, const int32_t* d_sel,
-                                   const int64_t* d_step_off, int32_t n_sel, uint8_t* d_out, void* stream) {
+int mrts_render_records_onehot_dev(mrts_env* env, const uint32_t* d_rec, int64_t rec_words, int32_t n_ranks, int64_t rank_stride,
+                                   const int32_t* d_sel, const int64_t* d_step_off, int32_t n_sel, uint8_t* d_out, void* stream) {
     try {
-        if (!env || !d_rec || !d_out || (n_sel > 0 && !d_sel) || n_sel < 0 || rank_stride < 0) throw Fail{-EINVAL, "bad argument"};
-        if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
+        if (!env || !d_rec || !d_out || (n_sel > 0 && !d_sel) || n_sel < 0 || rank_stride < 0 || rec_words < 0 || n_ranks < 1)
+            throw Fail{-EINVAL, "bad argument"};
+        if (!env->recUnits || !env->d_renderErr) throw Fail{-EINVAL, "mrts_set_records first"};
         if (env->partialObs) throw Fail{-ENOTSUP, "one-hot from records: full observability only"};
         if (((uintptr_t)d_out & 15) || ((uintptr_t)d_rec & 3)) throw Fail{-EINVAL, "misaligned buffer"};
         HIPCHK(hipSetDevice(env->device));
-        if (!env->d_renderErr) {
-            HIPCHK(hipMalloc(&env->d_renderErr, 4));
-            HIPCHK(hipMemset(env->d_renderErr, 0, 4));
-        }
-        HIPCHK(launchRenderRecordsOneHot(env->hstatic, env->d_static, d_rec, env->recUnits, rank_stride, d_sel, d_step_off, n_sel,
-                                         d_out, env->d_renderErr, pickStream(env, stream)));
+        HIPCHK(launchRenderRecordsOneHot(env->hstatic, env->d_static, d_rec, rec_words, n_ranks, env->recUnits, rank_stride, d_sel,
+                                         d_step_off, n_sel, d_out, env->d_renderErr, pickStream(env, stream)));
         return 0;
     } catch (const Fail& f) {
         return fail(f);
@@ -1533,18 +1545,17 @@ int32_t mrts_record_words(const mrts_env* env) {
     return env->recUnits ? recWords(env->recUnits, env->partialObs) : 0;
 }
 
-int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int32_t n_ranks, int64_t rank_stride, void* d_out,
-                            int32_t out_bytes, void* stream) {
+int mrts_render_records_dev(mrts_env* env, const uint32_t* d_rec, int64_t rec_words, int32_t n_ranks, int64_t rank_stride,
+                            void* d_out, int32_t out_bytes, void* stream) {
     try {
-        if (!env || !d_rec || !d_out || n_ranks < 1 || rank_stride < 0) throw Fail{-EINVAL, "bad argument"};
-        if (!env->recUnits) throw Fail{-EINVAL, "mrts_set_records first"};
+        if (!env || !d_rec || !d_out || n_ranks < 1 || rank_stride < 0 || rec_words < 0) throw Fail{-EINVAL, "bad argument"};
+        if (!env->recUnits || !env->d_renderErr) throw Fail{-EINVAL, "mrts_set_records first"};
         if (out_bytes != 1 && out_bytes != 4) throw Fail{-EINVAL, "out_bytes: 1 (uint8) or 4 (int32)"};
         if (((uintptr_t)d_out & (out_bytes == 4 ? 15 : 3)) || ((uintptr_t)d_rec & 3)) throw Fail{-EINVAL, "misaligned buffer"};
+        // every rank's records inside the buffer (the kernel reads n_games records per rank)
+        const int64_t span = (int64_t)(n_ranks - 1) * rank_stride + (int64_t)env->nGames * recWords(env->recUnits, env->partialObs);
+        if (span > rec_words) throw Fail{-EINVAL, "the ranks' records reach past the receive buffer (rec_words)"};
         HIPCHK(hipSetDevice(env->device));
-        if (!env->d_renderErr) {
-            HIPCHK(hipMalloc(&env->d_renderErr, 4));
-            HIPCHK(hipMemset(env->d_renderErr, 0, 4));
-        }
         HIPCHK(launchRenderRecords(env->hstatic, env->d_static, d_rec, env->recUnits, n_ranks, rank_stride, d_out, out_bytes,
                                    env->d_renderErr, pickStream(env, stream)));
         return 0;

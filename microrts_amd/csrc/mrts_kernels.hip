@@ -377,9 +377,10 @@ constexpr int UTT_LDS = (int)((sizeof(DevUtt) + 15) & ~(size_t)15);
 static_assert(sizeof(DevUtt) % 4 == 0 && UTT_WORDS <= 192, "DevUtt copy: 3 words per lane");
 
 // a ^ b ^ k in one VALU instruction (gfx950's three-input bit op, truth table 0x96; the compiler emits
-// two v_xor_b32 for it); k is wave-uniform (a Philox key word, in an SGPR)
+// two v_xor_b32 for it).  k MUST be wave-uniform (a Philox key word, in an SGPR): the "s" constraint would
+// silently readfirstlane a per-lane value.  Other targets (ARCH overridden) take the plain C form.
 DEV uint32_t xor3s(uint32_t a, uint32_t b, uint32_t k) {
-#if MRTS_XOR3
+#if MRTS_XOR3 && defined(__gfx950__)
     uint32_t d;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "s"(k));
     return d;
@@ -5946,7 +5947,8 @@ __global__ __launch_bounds__(256) void k_render_records_po(const KStatic* __rest
 __global__ __launch_bounds__(256) void k_render_records_onehot(const KStatic* __restrict__ PS, const uint32_t* __restrict__ rec,
                                                                int units, int64_t rank_stride, const int32_t* __restrict__ sel,
                                                                const int64_t* __restrict__ step_off, uint8_t* __restrict__ out,
-                                                               OneHotParams Q, int32_t* __restrict__ err) {
+                                                               OneHotParams Q, int32_t* __restrict__ err, int64_t rec_words,
+                                                               int n_ranks) {
     __shared__ uint32_t imgw[5 * 256 / 4];
     __shared__ __align__(16) uint8_t buf[256 * 40];
     uint8_t* img = (uint8_t*)imgw;
@@ -5955,7 +5957,16 @@ __global__ __launch_bounds__(256) void k_render_records_onehot(const KStatic* __
     const int gs = sel[blockIdx.x];
     const int r = gs / S, slot = gs - r * S, g = slot >> 1, p = slot & 1;
     const int64_t o = step_off ? step_off[2 * blockIdx.x] : 0, rs = step_off ? step_off[2 * blockIdx.x + 1] : rank_stride;
-    const uint32_t* rc = rec + o + (size_t)r * (size_t)rs + (size_t)g * recWords(units, false);
+    // a sample outside the buffer (a bad sel index or step_off row): a zero image and the render flag
+    // (mrts_render_status), never a read past the receive buffer.  Block-uniform: the whole block returns.
+    const int64_t at = o + (int64_t)r * rs + (int64_t)g * recWords(units, false);
+    if (gs < 0 || r >= n_ranks || o < 0 || rs < 0 || at + recWords(units, false) > rec_words) {
+        if (t == 0) *err = 1;
+        uint4* dz = (uint4*)(out + (size_t)blockIdx.x * HW * F);
+        for (int k = t; k < HW * F / 16; k += 256) dz[k] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
+    const uint32_t* rc = rec + at;
     for (int i = t; i < 5 * HW / 4; i += 256) imgw[i] = 0u;
     for (int k = t; k < HW * F / 4; k += 256) ((uint32_t*)buf)[k] = 0u;
     const uint32_t hdr = rc[0];
@@ -5985,9 +5996,9 @@ __global__ __launch_bounds__(256) void k_render_records_onehot(const KStatic* __
     uint4* dst = (uint4*)(out + (size_t)blockIdx.x * HW * F);
     for (int k = t; k < HW * F / 16; k += 256) dst[k] = ((const uint4*)buf)[k];
 }
-hipError_t launchRenderRecordsOneHot(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int64_t rank_stride,
-                                     const int32_t* sel, const int64_t* step_off, int n_sel, uint8_t* out, int32_t* err,
-                                     hipStream_t stream) {
+hipError_t launchRenderRecordsOneHot(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int64_t rec_words, int n_ranks,
+                                     int units, int64_t rank_stride, const int32_t* sel, const int64_t* step_off, int n_sel,
+                                     uint8_t* out, int32_t* err, hipStream_t stream) {
     OneHotParams Q{};
     const int base[6] = {5, 5, 3, hs.utt.ntypes + 1, 6, 2};
     int f = 0;
@@ -6000,7 +6011,7 @@ hipError_t launchRenderRecordsOneHot(const KStatic& hs, const KStatic* ds, const
     if (hs.partial_obs || hs.HW > 256 || f > 40 || ((size_t)hs.HW * f) % 16 || ((uintptr_t)out & 15)) return hipErrorInvalidValue;
     if (n_sel <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_render_records_onehot, dim3((unsigned)n_sel), dim3(256), 0, stream, ds, rec, units, rank_stride, sel,
-                       step_off, out, Q, err);
+                       step_off, out, Q, err, rec_words, n_ranks);
     return hipGetLastError();
 }
 hipError_t launchRenderRecords(const KStatic& hs, const KStatic* ds, const uint32_t* rec, int units, int n_ranks,

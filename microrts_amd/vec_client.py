@@ -378,8 +378,9 @@ class DeviceVecEnv:
         S, H, W, C, K = h.S, h.H, h.W, h.C, h.K
         self.obs = torch.zeros((S, C, H, W), dtype=torch.int32, device=dev)
         rshape = (S,) if h.R == 1 else (S, h.R)
-        self.reward = torch.zeros(rshape, dtype=torch.float64, device=dev)
-        self.done = torch.zeros(rshape, dtype=torch.uint8, device=dev)
+        self._reward = torch.zeros(rshape, dtype=torch.float64, device=dev)
+        self._done = torch.zeros(rshape, dtype=torch.uint8, device=dev)
+        self._ring_last = None  # ring step holding the last rollout call's responses (set_step_responses)
         self.masks = torch.zeros((S, H, W, K), dtype=torch.uint8, device=dev) if with_masks else None
         self.actions = torch.zeros((S, H * W, 7), dtype=torch.int32, device=dev)
         self.players = torch.zeros((S,), dtype=torch.int32, device=dev)
@@ -395,6 +396,23 @@ class DeviceVecEnv:
         self._ptr_cache = None
         torch.cuda.synchronize(dev)
 
+    @property
+    def reward(self):
+        """The last step's reward ([slots] or [slots][R], float64).  After a rollout call that wrote the Responses
+        ring (set_step_responses), this is the ring's last step of that call (a view: no copy), else
+        the plain buffer the step calls write."""
+        return self._reward if self._ring_last is None else self.step_rewards[self._ring_last]
+
+    @property
+    def done(self):
+        """The last step's done flags (uint8, as reward; the ring's last step after a ring-writing rollout)."""
+        return self._done if self._ring_last is None else self.step_dones[self._ring_last]
+
+    def _ring_written(self, n_steps):
+        """After a rollout call: with the ring on, its responses are in ring steps 0 .. n_steps - 1."""
+        if self.step_rewards is not None and n_steps > 0:
+            self._ring_last = n_steps - 1
+
     @staticmethod
     def _p(t):
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
@@ -407,7 +425,7 @@ class DeviceVecEnv:
     def _bufs(self):
         """actions, players, obs, reward, done, masks as ctypes pointers, cached while the same tensor
         objects stay attached (the rollout calls' per-call host cost)."""
-        key = (self.actions, self.players, self.obs, self.reward, self.done, self.masks)
+        key = (self.actions, self.players, self.obs, self._reward, self._done, self.masks)
         c = self._ptr_cache
         if c is None or any(a is not b for a, b in zip(c[0], key)):
             c = self._ptr_cache = (key, tuple(self._p(t) for t in key))
@@ -430,8 +448,9 @@ class DeviceVecEnv:
     def reset(self, stream=None):
         h = self._h
         self._obs_guard()
-        _lib.check(h.L.mrts_reset_dev(h.h, self._p(self.players), self._p(self.obs), self._p(self.reward),
-                                      self._p(self.done), self._p(self.masks), self.mask_player, self._s(stream)))
+        _lib.check(h.L.mrts_reset_dev(h.h, self._p(self.players), self._p(self.obs), self._p(self._reward),
+                                      self._p(self._done), self._p(self.masks), self.mask_player, self._s(stream)))
+        self._ring_last = None
         self._obs_written()
 
     def step(self, actions=None, stream=None, masks=True):
@@ -439,9 +458,10 @@ class DeviceVecEnv:
         h = self._h
         a = self.actions if actions is None else actions
         self._obs_guard()
-        _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self.reward),
-                                     self._p(self.done), self._p(self.masks) if masks else None, self.mask_player,
+        _lib.check(h.L.mrts_step_dev(h.h, self._p(a), self._p(self.players), self._p(self.obs), self._p(self._reward),
+                                     self._p(self._done), self._p(self.masks) if masks else None, self.mask_player,
                                      self._s(stream)))
+        self._ring_last = None
         self._obs_written()
 
     def uniform_policy(self, seed, step, out=None, stream=None):
@@ -458,9 +478,10 @@ class DeviceVecEnv:
         h = self._h
         self._obs_guard()
         _lib.check(h.L.mrts_step_uniform_dev(h.h, self._p(self.actions), self._p(self.players), self._p(self.obs),
-                                             self._p(self.reward), self._p(self.done),
+                                             self._p(self._reward), self._p(self._done),
                                              self._p(self.masks) if masks else None, self.mask_player, seed, step,
                                              self._s(stream)))
+        self._ring_last = None
         self._obs_written()
 
     def rollout_uniform(self, seed, first_step, n_steps, fused=True, stream=None):
@@ -472,6 +493,7 @@ class DeviceVecEnv:
         a, pl, o, r, d, _ = self._bufs()
         _lib.check(h.L.mrts_rollout_uniform_dev(h.h, a, pl, o, r, d, seed, first_step, n_steps, 1 if fused else 0,
                                                 self._s(stream)))
+        self._ring_written(n_steps)
         self._obs_written()
 
     def step_fused(self, seed, next_step, stream=None):
@@ -484,6 +506,7 @@ class DeviceVecEnv:
         self._obs_guard()
         a, pl, o, r, d, m = self._bufs()
         _lib.check(h.L.mrts_step_fused_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, next_step, self._s(stream)))
+        self._ring_last = None
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
@@ -526,6 +549,7 @@ class DeviceVecEnv:
         a, pl, o, r, d, m = self._bufs()
         _lib.check(h.L.mrts_rollout_fused_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, first_next_step, n_steps,
                                               self._s(stream)))
+        self._ring_written(n_steps)
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
@@ -540,6 +564,7 @@ class DeviceVecEnv:
         _lib.check(h.L.mrts_rollout_fused_exchange_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, first_next_step,
                                                        n_steps, self._p(send[0]), self._p(send[1]), self._p(recv),
                                                        self._s(stream)))
+        self._ring_written(n_steps)
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
 
@@ -567,6 +592,7 @@ class DeviceVecEnv:
         a, pl, o, r, d, _ = self._bufs()
         _lib.check(h.L.mrts_rollout_uniform_exchange_dev(h.h, a, pl, o, r, d, seed, first_step, n_steps, self._p(send[0]),
                                                          self._p(send[1]), self._p(recv), self._s(stream)))
+        self._ring_written(n_steps)
         self._obs_written()
 
     def set_records(self, units_per_record=64, steps_per_launch=0):
@@ -594,6 +620,7 @@ class DeviceVecEnv:
         off = np.zeros((max(n_steps, 1), 2), dtype=np.int64)
         _lib.check(h.L.mrts_rollout_fused_records_dev(h.h, a, pl, o, r, d, m, self.mask_player, seed, first_next_step, n_steps,
                                                       self._p(recv), off.ctypes.data_as(ctypes.c_void_p), self._s(stream)))
+        self._ring_written(n_steps)
         self._obs_written()
         self._policy_out, self._policy_version = self.actions, self.actions._version
         return off[:n_steps]
@@ -607,6 +634,7 @@ class DeviceVecEnv:
         off = np.zeros((max(n_steps, 1), 2), dtype=np.int64)
         _lib.check(h.L.mrts_rollout_uniform_records_dev(h.h, a, pl, o, r, d, seed, first_step, n_steps, self._p(recv),
                                                         off.ctypes.data_as(ctypes.c_void_p), self._s(stream)))
+        self._ring_written(n_steps)
         self._obs_written()
         return off[:n_steps]
 
@@ -621,16 +649,19 @@ class DeviceVecEnv:
         ok = (T.int8, T.int32) if self.partial_obs else (T.uint8, T.int32)
         assert out.dtype in ok, f"render_records: out must be one of {ok}, not {out.dtype}"
         assert out.is_contiguous() and out.numel() == n_ranks * self.obs.numel()
+        assert recv.dtype == T.int32 and recv.is_contiguous() and 0 <= int(offset) <= recv.numel()
         ptr = ctypes.c_void_p(recv.data_ptr() + 4 * int(offset))
-        _lib.check(h.L.mrts_render_records_dev(h.h, ptr, int(n_ranks), int(rank_stride), self._p(out), ob, self._s(stream)))
+        _lib.check(h.L.mrts_render_records_dev(h.h, ptr, recv.numel() - int(offset), int(n_ranks), int(rank_stride), self._p(out),
+                                               ob, self._s(stream)))
         return out
 
-    def render_records_onehot(self, recv, offset, rank_stride, sel, out=None, step_off=None, stream=None):
+    def render_records_onehot(self, recv, offset, rank_stride, sel, out=None, step_off=None, stream=None, n_ranks=None):
         """A learner minibatch from records in one launch: the MicroRTS-Py one-hot observations (onehot_obs'
         layout, uint8 [n][H][W][F]) of the slots sel (int32 tensor of global indices r * slots + slot over the
         ranks in recv) of the step whose records start at recv[offset] with rank_stride — or, with step_off
         (int64 tensor [n, 2]: each sample's step's row of the rollout's offsets table), each sample's own
-        step — mrts_render_records_onehot_dev."""
+        step — mrts_render_records_onehot_dev.  n_ranks (default: as many as recv holds) bounds sel; a sample
+        outside recv or n_ranks renders as zeros and raises render_overflow()."""
         h, T = self._h, self.torch
         F = h.L.mrts_onehot_features(h.h)
         assert sel.dtype == T.int32 and sel.is_contiguous() and sel.device == self.device
@@ -639,9 +670,13 @@ class DeviceVecEnv:
         if out is None:
             out = T.empty((sel.numel(), h.H, h.W, F), dtype=T.uint8, device=self.device)
         assert out.dtype == T.uint8 and out.is_contiguous() and out.numel() == sel.numel() * h.H * h.W * F
+        assert recv.dtype == T.int32 and recv.is_contiguous() and 0 <= int(offset) <= recv.numel()
+        if n_ranks is None:  # every rank place a records buffer of this handle's games can hold
+            n_ranks = max(1, recv.numel() // max(1, (h.S // 2) * self.record_words))
         ptr = ctypes.c_void_p(recv.data_ptr() + 4 * int(offset))
-        _lib.check(h.L.mrts_render_records_onehot_dev(h.h, ptr, int(rank_stride), self._p(sel), self._p(step_off),
-                                                      int(sel.numel()), self._p(out), self._s(stream)))
+        _lib.check(h.L.mrts_render_records_onehot_dev(h.h, ptr, recv.numel() - int(offset), int(n_ranks), int(rank_stride),
+                                                      self._p(sel), self._p(step_off), int(sel.numel()), self._p(out),
+                                                      self._s(stream)))
         return out
 
     def render_overflow(self):
@@ -656,15 +691,18 @@ class DeviceVecEnv:
         """Every step's reward / done from each rollout call of at most max_steps steps
         (mrts_set_step_responses; Java's gameStep returns them on every call): step k of the next call
         lands in self.step_rewards[k] / self.step_dones[k] ([slots] or [slots][R], as reward / done) INSTEAD
-        of self.reward / self.done, which rollout calls then leave untouched (the last step's values are
-        step_rewards[n_steps - 1]).  0 turns it off."""
+        of the plain reward / done buffers, which rollout calls then leave untouched; after such a call
+        self.reward / self.done are views of its last ring step (step_rewards[n_steps - 1]), so they never
+        read stale.  0 turns it off."""
         h, T = self._h, self.torch
         if not max_steps:
             _lib.check(h.L.mrts_set_step_responses(h.h, None, None, 0))
             self.step_rewards = self.step_dones = None
+            self._ring_last = None
             return
-        self.step_rewards = T.zeros((max_steps,) + tuple(self.reward.shape), dtype=T.float64, device=self.device)
-        self.step_dones = T.zeros((max_steps,) + tuple(self.done.shape), dtype=T.uint8, device=self.device)
+        self._ring_last = None
+        self.step_rewards = T.zeros((max_steps,) + tuple(self._reward.shape), dtype=T.float64, device=self.device)
+        self.step_dones = T.zeros((max_steps,) + tuple(self._done.shape), dtype=T.uint8, device=self.device)
         _lib.check(h.L.mrts_set_step_responses(h.h, self._p(self.step_rewards), self._p(self.step_dones), int(max_steps)))
 
     def step_rows(self, rows, stream=None):
@@ -674,9 +712,10 @@ class DeviceVecEnv:
         assert rows.shape[0] == h.S and rows.device == self.device
         self._obs_guard()
         _lib.check(h.L.mrts_step_rows_dev(h.h, self._p(rows), rows.shape[1], self._p(self.players), self._p(self.obs),
-                                          self._p(self.reward), self._p(self.done),
+                                          self._p(self._reward), self._p(self._done),
                                           self._p(self.masks) if self.masks is not None else None, self.mask_player,
                                           self._s(stream)))
+        self._ring_last = None
         self._obs_written()
 
     def onehot_obs(self, obs=None, out=None, stream=None):

@@ -557,7 +557,9 @@ def test_step_responses_every_reward_function():
                 saw_done |= bool(wantD[j][:, 0].any())
             for name in ("obs", "actions"):
                 assert torch.equal(getattr(A, name), getattr(B, name)), f"{mp}: {name} after {k}"
-            assert not bool(B.reward.any()) and not bool(B.done.any()), "the plain buffers are left alone"
+            assert not bool(B._reward.any()) and not bool(B._done.any()), "the plain buffers are left alone"
+            #  env.reward / env.done read the call's last ring step, not the stale plain buffers
+            assert torch.equal(B.reward, wantR[-1]) and torch.equal(B.done, wantD[-1])
         assert saw_done, "no auto-reset inside the checked steps"
         with pytest.raises(RuntimeError):
             B.rollout_uniform(SEED, k, 151) if uniform else B.rollout_fused(SEED, k + 1, 151)
@@ -621,6 +623,20 @@ def test_records_onehot_batch(mp, spl):
         for i in range(300):
             assert torch.equal(got[i], want[int(js[i])][int(twin[i])].cpu()), f"minibatch sample {i}"
     assert not B.render_overflow()
+    # a sample outside the buffer — an index outside [0, ranks x slots), a step_off row past the
+    # receive buffer — renders as zeros and raises the render flag instead of reading past the buffer
+    o, st = int(off[-1, 0]), int(off[-1, 1])
+    bad = torch.tensor([-1, world * S, 5], dtype=torch.int32, device=B.device)
+    got = B.render_records_onehot(recv, o, st, bad, n_ranks=world).cpu()
+    assert not got[0].any() and not got[1].any() and got[2].any() and B.render_overflow()
+    so = torch.tensor([[o, st], [recv.numel(), st], [o, 10 * recv.numel()]], dtype=torch.int64, device=B.device)
+    bad = torch.tensor([5, 5, S + 5], dtype=torch.int32, device=B.device)  # (rank 1: its stride is out of range)
+    got = B.render_records_onehot(recv, 0, 0, bad, step_off=so).cpu()
+    assert got[0].any() and not got[1].any() and not got[2].any() and B.render_overflow()
+    assert not B.render_overflow(), "the flag resets when read"
+    with pytest.raises(RuntimeError):  # a rank stride reaching past the receive buffer
+        B.render_records(recv, o, recv.numel(), 2, torch.zeros((2 * S,) + tuple(B.obs.shape[1:]), dtype=torch.int32,
+                                                                device=B.device))
     for e in (A, B):
         assert not e.error_flags().any()
         e.close()
