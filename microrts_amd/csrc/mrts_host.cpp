@@ -28,6 +28,10 @@ hipError_t launchEnv(int mode, const KStatic& hs, const KStatic* ds, const KDyn&
 bool envIterable(const KStatic& hs);
 hipError_t launchPolicyUniform(int32_t* actions, int n_slots, int HW, int ntypes, int natt, uint64_t seed, uint32_t step,
                                uint32_t slot_base, hipStream_t stream);
+#ifdef MRTS_LANE_AUDIT
+hipError_t laneAudit(int32_t* out, int reset);
+hipError_t laneAuditProbe(int32_t* scratch);
+#endif
 #ifdef MRTS_ABLATE
 hipError_t setAblate(uint32_t v);
 hipError_t getDbg(unsigned long long* out, int reset);
@@ -2472,6 +2476,22 @@ int mrts_evaluate(mrts_env* env, int32_t maxplayer, float* out) {
     }
 }
 
+#ifdef MRTS_LANE_AUDIT
+// diagnostic build only: the cross-lane read audit (tests/test_zz_lane_audit.py); synchronises the device
+int mrts_lane_audit(int32_t* out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -EIO;
+    return mrts::laneAudit(out, reset) == hipSuccess ? 0 : -EIO;
+}
+// the negative control: one launch whose readlane reads an inactive lane (the audit must report it)
+int mrts_lane_audit_probe(void) {
+    int32_t* d = nullptr;
+    if (hipMalloc(&d, 64 * sizeof(int32_t)) != hipSuccess) return -ENOMEM;
+    const hipError_t e = mrts::laneAuditProbe(d);
+    const hipError_t s = hipDeviceSynchronize();
+    (void)hipFree(d);
+    return e == hipSuccess && s == hipSuccess ? 0 : -EIO;
+}
+#endif
 #ifdef MRTS_ABLATE
 // diagnostic build only: g_ablate (tools/ablate_price.py)
 int mrts_set_ablate(unsigned v) { return mrts::setAblate(v) == hipSuccess ? 0 : -EIO; }

@@ -298,14 +298,44 @@ DEV int dxo(int d) { return d == 1 ? 1 : (d == 3 ? -1 : 0); }
 DEV int dyo(int d) { return d == 0 ? -1 : (d == 2 ? 1 : 0); }
 DEV int clampdir(int d) { return (d >= 0 && d <= 3) ? d : ACT_INVALID; }
 
+// Diagnostic build only (-DMRTS_LANE_AUDIT, `make audit`; tests/test_zz_lane_audit.py): every cross-lane read
+// checks at run time that the lanes it reads are active where it executes — a readlane's source lane, every lane
+// for the DPP reductions and ballots (which the code treats as whole-wave) — and records the source line of a
+// violation in g_laneAudit (one vector store per lane, its own slot).  A readlane of an inactive lane returns
+// whatever its register last held (the round-4 soak's stale PO value).  Not in libmrts.so.
+#ifdef MRTS_LANE_AUDIT
+__device__ int32_t g_laneAudit[256];
+DEV void laneAuditHit(int line, int kind) { g_laneAudit[threadIdx.x & 255] = line | (kind << 24); }
+DEV bool laneOn(int k) { return (__builtin_amdgcn_read_exec() >> k) & 1ull; }
+DEV bool waveOn() { return __builtin_amdgcn_read_exec() == ~0ull; }
+DEV int rlAudit(int v, int k, int line) {
+    if (!laneOn(k)) laneAuditHit(line, 1);
+    return __builtin_amdgcn_readlane(v, k);
+}
+#define rl(v, k) rlAudit((v), (k), __LINE__)
+#define LANE_AUDIT_WAVE(kind)                              \
+    do {                                                   \
+        if (!waveOn()) laneAuditHit(__LINE__, (kind));     \
+    } while (0)
+#else
 DEV int rl(int v, int k) { return __builtin_amdgcn_readlane(v, k); }
+#define LANE_AUDIT_WAVE(kind) ((void)0)
+#endif
 // four int32 values (each within int16) as four packed int16
 DEV uint2 pk16(int4 w) {
     return make_uint2(((uint32_t)w.x & 0xFFFFu) | ((uint32_t)w.y << 16), ((uint32_t)w.z & 0xFFFFu) | ((uint32_t)w.w << 16));
 }
 DEV int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 DEV uint32_t uniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+#ifdef MRTS_LANE_AUDIT
+#define ballot(p) ballotAudit((p), __LINE__)
+DEV uint64_t ballotAudit(bool p, int line) {
+    if (!waveOn()) laneAuditHit(line, 3);
+    return __ballot(p);
+}
+#else
 DEV uint64_t ballot(bool p) { return __ballot(p); }
+#endif
 DEV int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
@@ -321,6 +351,7 @@ DEV void wsync() {
 // reduce each 16-lane row; row_bcast:15/31 chain the rows; lane 63 holds the result.
 template <bool MIN>
 DEV int wave_reduce(int v) {
+    LANE_AUDIT_WAVE(2);
     const int id = MIN ? INF : 0;
     auto op = [](int a, int b) { return MIN ? min(a, b) : a + b; };
     v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
@@ -329,11 +360,12 @@ DEV int wave_reduce(int v) {
     v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xF, 0xF, false));  // row_mirror
     v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
     v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
-    return __builtin_amdgcn_readlane(v, 63);
+    return rl(v, 63);
 }
 // Inclusive prefix sum over the wave's lanes with DPP: row_shr 1/2/4/8 scan each 16-lane row
 // (lanes shifted in from outside the row read 0), row_bcast:15 / :31 carry the row totals.
 DEV int wave_incl_sum(int v) {
+    LANE_AUDIT_WAVE(2);
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
     v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
@@ -5601,7 +5633,7 @@ __global__ __launch_bounds__(64) void k_policy_delta(PolicyParams Q) {
     const uint32_t dirty = cur | old;
     const int n = __popc(dirty);
     const int incl = wave_incl_sum(n);  // inclusive prefix sum over lanes
-    const int total = __builtin_amdgcn_readlane(incl, 63);
+    const int total = rl(incl, 63);
     if (total == 0) return;
     const uint32_t slot = item / MW, w = item - slot * MW;
     int k = incl - n;
@@ -5633,9 +5665,32 @@ __global__ __launch_bounds__(64) void k_policy(PolicyParams Q) {
     for (int k = 0; k < 7; k++) out[k] = a[k];
 }
 
+#ifdef MRTS_LANE_AUDIT
+// the audit's negative control: a readlane of lane 40 from a branch only lanes 0..31 take
+__global__ __launch_bounds__(64) void k_lane_audit_probe(int32_t* out) {
+    int v = 0;
+    if (threadIdx.x < 32) v = rl((int)threadIdx.x * 3, 40);
+    out[threadIdx.x] = v;
+}
+#endif
 }  // namespace
 
 namespace mrts {
+#ifdef MRTS_LANE_AUDIT
+hipError_t laneAuditProbe(int32_t* scratch) {
+    hipLaunchKernelGGL(k_lane_audit_probe, dim3(1), dim3(64), 0, 0, scratch);
+    return hipGetLastError();
+}
+// out[256]: per thread slot the last violation (source line | kind << 24: 1 readlane, 2 DPP, 3 ballot), 0 = none
+hipError_t laneAudit(int32_t* out, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_laneAudit), sizeof(int32_t) * 256);
+    if (e == hipSuccess && reset) {
+        int32_t z[256] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_laneAudit), z, sizeof(z));
+    }
+    return e;
+}
+#endif
 #ifdef MRTS_ABLATE
 hipError_t setAblate(uint32_t v) { return hipMemcpyToSymbol(HIP_SYMBOL(g_ablate), &v, sizeof(v)); }
 hipError_t getDbg(unsigned long long* out, int reset) {
