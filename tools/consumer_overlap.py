@@ -4,7 +4,9 @@ the records rollout on a second stream?  c3 workload (4096 games), records over 
 transport, L launches of K steps.  Times, with HIP events: the rollout alone, the renders alone (B random
 slots of the 8-rank volume per step, rank stride 0, one render launch per rollout launch for its K steps), and
 both with the render of launch i on a second stream waiting only for launch i (so it may run beside launch
-i + 1).  Prints one JSON line."""
+i + 1).  Each of the three is warmed once and timed as the median of 3 passes (round 6: round 5's first B had
+timed the side stream's first use — its one-time queue setup — inside the two-stream window: 3.29x at B = 1,024
+against 1.22x serial).  Prints one JSON line."""
 import json
 import os
 import sys
@@ -64,25 +66,34 @@ def main():
                         stream.wait_event(evs[i])
                     env.render_records_onehot(recvs[i], 0, 0, sel, bufs[i & 1], step_off=soff[i], stream=stream)
 
-        t[0].record(main_s)
-        offs = rollouts()
-        t[1].record(main_s)
-        torch.cuda.synchronize()
-        t_c = t[0].elapsed_time(t[1]) / (L * K)
-        t[0].record(main_s)
-        renders(main_s, offs)
-        t[1].record(main_s)
-        torch.cuda.synchronize()
-        t_r = t[0].elapsed_time(t[1]) / (L * K)
+        import statistics
+
+        def timed(fn):
+            vals = []
+            for rep in range(4):  # pass 0 warms (first use of a stream / event pattern), then the median of 3
+                t[0].record(main_s)
+                fn()
+                t[1].record(main_s)
+                torch.cuda.synchronize()
+                if rep:
+                    vals.append(t[0].elapsed_time(t[1]) / (L * K))
+            return statistics.median(vals)
+
+        def compute_only():
+            nonlocal offs
+            offs = rollouts()
+
+        t_c = timed(compute_only)
+        t_r = timed(lambda: renders(main_s, offs))
         evs = [torch.cuda.Event() for _ in range(L)]
-        t[0].record(main_s)
-        side.wait_event(t[0])
-        offs2 = rollouts(evs)
-        renders(side, offs2, evs)
-        main_s.wait_stream(side)
-        t[1].record(main_s)
-        torch.cuda.synchronize()
-        t_o = t[0].elapsed_time(t[1]) / (L * K)
+
+        def both():
+            side.wait_event(t[0])
+            offs2 = rollouts(evs)
+            renders(side, offs2, evs)
+            main_s.wait_stream(side)
+
+        t_o = timed(both)
         out[str(B)] = {"compute_ms_per_step": t_c, "render_ms_per_step": t_r, "both_two_streams_ms_per_step": t_o,
                        "ratio_vs_compute": t_o / t_c, "serial_ratio": (t_c + t_r) / t_c,
                        "onehot_MB_per_step": bufs[0].numel() / K / 1e6}
