@@ -173,6 +173,9 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SAMPLE_UNIFIED
 #define MRTS_SAMPLE_UNIFIED 1
 #endif
+#ifndef MRTS_MASK_QUADS  // c3: each idle unit's mask bits computed by a quad of lanes, one per direction (round 6)
+#define MRTS_MASK_QUADS 1
+#endif
 #ifndef MRTS_REC_LANES  // delta mask records stored lane-parallel (storeRecordsLanes, round 5); 0 = by their own lanes
 #define MRTS_REC_LANES 1
 #endif
@@ -4191,6 +4194,128 @@ struct Game {
         w1 = (uint32_t)(lo >> 32);
         w2 = hi;
     }
+    // maskBitsFast's bits of ONE direction d (the lane of a quad that computes d; VERDICT r5 #4: the per-idle-unit
+    // phases spread over lanes so that their instruction count falls): the unit-type and NONE bits, and what the
+    // neighbour cell d holds — an enemy (range-1 attack), a resource (harvest), an own stockpile (return), an empty
+    // cell (produce direction, move).  The quad's OR of its four results is maskBitsFast's, but for the produce-type
+    // bits, which the caller adds once the OR shows a free cell (they need any of the four).  Every bit below the
+    // attack window is in w0 (slot 1 + 6 + 12 + 3 = 22 < 32).
+    DEV void maskBitsDir(const MaskTables& T, uint32_t cu, int carried, int d, uint32_t& w0, uint32_t& w1,
+                         uint32_t& w2) const {
+        const int x = ux(cu), y = uy(cu), typ = utyp(cu), pl = uplay(cu);
+        const int ctr = R / 2, atkBase = 1 + 6 + 16 + NT;
+        const int ddx = dxo(d), ddy = dyo(d), nx = x + ddx, ny = y + ddy;
+        const int n = inb(nx, ny) ? cell[ny * W + nx] : WALL;
+        const uint32_t oc = n < CAP ? uc[n] : 0u;
+        const bool atk = (T.attack1 >> typ) & 1u, harv = (T.harvest >> typ) & 1u, mov = (T.move >> typ) & 1u;
+        const uint32_t canProd = (uint32_t)(T.prod >> (8 * typ)) & 0xFFu & (pl == 0 ? T.aff0 : T.aff1);
+        uint32_t lo = 1u | (1u << (1 + T_NONE)), mid = 0, hi = 0;
+        if (n < CAP) {
+            const int op = uplay(oc), ot = utyp(oc);
+            if (atk && op >= 0 && op != pl) {
+                lo |= 1u << (1 + T_ATTACK);
+                const int k = atkBase + (ctr + ddy) * R + (ctr + ddx);
+                if (k < 32) lo |= 1u << k;
+                else if (k < 64) mid |= 1u << (k - 32);
+                else hi |= 1u << (k - 64);
+            }
+            if (harv && carried == 0 && ((T.resource >> ot) & 1u)) lo |= (1u << (1 + T_HARVEST)) | (1u << (1 + 6 + 4 + d));
+            if (harv && carried > 0 && ((T.stockpile >> ot) & 1u) && op == pl) lo |= (1u << (1 + T_RETURN)) | (1u << (1 + 6 + 8 + d));
+        } else if (n == EMPTY) {
+            if (canProd) lo |= (1u << (1 + T_PRODUCE)) | (1u << (1 + 6 + 12 + d));
+            if (mov) lo |= (1u << (1 + T_MOVE)) | (1u << (1 + 6 + d));
+        }
+        w0 = lo;
+        w1 = mid;
+        w2 = hi;
+    }
+    // farAttackRows for the quad lane of direction d: its rows dy = d - ctr and d - ctr + 4 of the 2 ctr + 1 <= 7
+    // (attack range <= 3: K <= 80), the same bits; the whole wave calls it
+    DEV void farAttackRowsDir(bool far, uint32_t cu, int d, const uint32_t* rows, uint32_t& w0, uint32_t& w1,
+                              uint32_t& w2) const {
+        if (!ballot(far)) return;
+        const int x = ux(cu), y = uy(cu), pl = uplay(cu);
+        const int r = far ? U.range[utyp(cu)] : 0, ctr = R / 2, atkBase = 1 + 6 + 16 + NT;
+        const uint32_t* er = rows + (far ? (1 - pl) * H : 0);
+        uint64_t lo = 0;
+        uint32_t hi = 0;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int dy = d - ctr + 4 * j, yy = y + dy;
+            if (!far || dy > ctr || dy < -r || dy > r || yy < 0 || yy >= H) continue;
+            const uint64_t word = er[yy];
+            uint64_t win = x >= r ? (word >> (x - r)) : (word << (r - x));  // bit j = column x - r + j
+            // the disk's columns of row dy: |dx| <= half, half^2 + dy^2 <= r^2
+            int half = 0;
+            while (half < r && (half + 1) * (half + 1) + dy * dy <= r * r) half++;
+            win &= ((2ull << (2 * half)) - 1ull) << (r - half);
+            if (!win) continue;
+            const int base = atkBase + (ctr + dy) * R + (ctr - r);
+            if (base < 64) {
+                lo |= win << base;
+                if (base > 0) hi |= (uint32_t)(win >> (64 - base));
+            } else {
+                hi |= (uint32_t)(win << (base - 64));
+            }
+            lo |= 1ull << (1 + T_ATTACK);
+        }
+        w0 |= (uint32_t)lo;
+        w1 |= (uint32_t)(lo >> 32);
+        w2 |= hi;
+    }
+    static DEV uint32_t quadOr(uint32_t v) {  // OR over the lane's quad (DPP quad_perm; whole wave)
+        v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+        v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+        return v;
+    }
+    // maskBitsFast + farAttackRows of every idle unit (si >= 0), four lanes per unit: the units' words go to LDS
+    // in rank order (16 per pass), lane 4 q + d computes direction d (and rows d - ctr, d - ctr + 4 of the
+    // ranged window) of unit q, the quad ORs its words, and the unit's own lane reads them back — the same bits
+    // as one lane per unit, in about a quarter of the instructions.  rows complete (wsync'd);
+    // rseq words 16..63 are scratch here.  Whole wave.
+    DEV void maskBitsQuads(const MaskTables& T, int si, uint32_t cu, int carried, const uint32_t* rows, uint32_t& w0,
+                           uint32_t& w1, uint32_t& w2) {
+        const int l = lid();
+        const uint64_t m = ballot(si >= 0);
+        const int RI = __popcll(m), r = lanes_below(m);
+        uint32_t* qb = (uint32_t*)rseq + 16;  // [16][3]
+        const int q = l >> 2, d = l & 3;
+        for (int p0 = 0; p0 < RI; p0 += 16) {
+            const bool mine = si >= 0 && r >= p0 && r < p0 + 16;
+            if (mine) {
+                qb[3 * (r - p0)] = cu;
+                qb[3 * (r - p0) + 1] = (uint32_t)carried;
+            }
+            wsync();
+            const bool qa = p0 + q < RI;
+            uint32_t qcu = 0, v0 = 0, v1 = 0, v2 = 0;
+            if (qa) {
+                qcu = qb[3 * q];
+                maskBitsDir(T, qcu, (int)qb[3 * q + 1], d, v0, v1, v2);
+            }
+            farAttackRowsDir(qa && ((T.attackFar >> utyp(qcu)) & 1u), qcu, d, rows, v0, v1, v2);
+            v0 = quadOr(v0);
+            v1 = quadOr(v1);
+            v2 = quadOr(v2);
+            // produce-type bits 23 + ut, when a direction of the quad found a free cell (produce direction bits)
+            const uint32_t canProd =
+                (uint32_t)(T.prod >> (8 * utyp(qcu))) & 0xFFu & (uplay(qcu) == 0 ? T.aff0 : T.aff1);
+            if (((v0 >> (1 + 6 + 12)) & 0xFu) != 0u) v0 |= canProd << (1 + 6 + 16);
+            wsync();  // every lane of a quad has read its entry
+            if (qa && d == 0) {
+                qb[3 * q] = v0;
+                qb[3 * q + 1] = v1;
+                qb[3 * q + 2] = v2;
+            }
+            wsync();
+            if (mine) {
+                w0 = qb[3 * (r - p0)];
+                w1 = qb[3 * (r - p0) + 1];
+                w2 = qb[3 * (r - p0) + 2];
+            }
+            wsync();  // read before the next pass rewrites the entries
+        }
+    }
     // The range > 1 attack bits of unitMask (Unit.java:424-434: every enemy unit within the disk) for
     // lanes with far = true, from the unit list held one unit per lane (cuLane = unit core word of
     // lane j, all units in one wave, none dead): one pass over the live owned units instead of a
@@ -4575,6 +4700,10 @@ struct Game {
 #endif
             MPHASE(17);
             const int carried = l < nu ? res[l] : 0;
+            if (MRTS_MASK_QUADS && rowB && !recOut) {  // four lanes per idle unit (c3, 8x8: the row bitmaps exist)
+                wsync();
+                maskBitsQuads(T, si, cu, carried, rows, w0, w1, w2);
+            } else {
             if (si >= 0) maskBitsFast(T, cu, carried, w0, w1, w2);
             MPHASE(18);
             const bool far = si >= 0 && ((T.attackFar >> utyp(cu)) & 1u);
@@ -4583,6 +4712,7 @@ struct Game {
                 farAttackRows(far, cu, rows, w0, w1, w2);
             } else {
                 farAttackBits(far, cu, cu, ballot(l < nu && !(cu & UC_DEAD) && uplay(cu) >= 0), w0, w1, w2);
+            }
             }
 #ifdef MRTS_ABLATE
             if (ab(AB_MASKBITS) && rowB) {

@@ -1,7 +1,7 @@
 """Every game of the benchmark configurations against the CPU oracle (VERDICT r4 "next" #2).
 
 test_headline_parity.py replays a 65-game sample of each bench shape; round 4's hand-run soak
-(tests/soak_full_parity.py) compared every game and found a bit-exactness bug the sample had missed.
+(now tools/soak_full_parity.py) compared every game and found a bit-exactness bug the sample had missed.
 These tests are that soak in the driver's `-m gpu` suite: the shipped benchmark form of c3 (4096 self-play
 games on basesWorkers16x16, fused masked policy, delta masks), c5 (2048 partially observable games on
 BWDistantResources32x32, max_units 256, the render helper wave) and c2 (1024 games on basesWorkers8x8,

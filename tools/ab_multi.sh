@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=$1; CFGS=$2; REPS=$3; shift 3
 mkdir -p gpurun_out/$TAG
-A="--no-cpu-baseline --no-other-configs --no-compare"
+A="--no-cpu-baseline --no-other-configs --no-compare ${AB_EXTRA:-}"
 for i in $(seq 1 $REPS); do
   for c in $CFGS; do
     for nv in "$@"; do

@@ -1,4 +1,4 @@
-"""Full-size parity soak (test infrastructure; run by hand on an MI355X, not collected by pytest):
+"""Full-size parity soak (a diagnostic tool since round 6 — tests/test_full_size_every_game.py runs the same check in the driver suite):
 EVERY game of the headline configuration — not the 65-game sample of test_headline_parity.py — checked
 bit for bit against the trace-pinned oracle, in bench.py's form (fused masked policy, delta masks,
 multi-step launches): after the 1000-step burn-in, after a K = 20 launch and after a K = 200 launch,
@@ -7,7 +7,7 @@ each slot's observation, reward, done, mask buffer, next action rows and full st
 The GPU run saves its snapshots; oracle replicas of all games then run on CPU worker processes (shards
 of games), each comparing its shard.  Prints one JSON line.
 
-  python tests/soak_full_parity.py [--config c3|c5] [--workers 16] [--out profiles/round4/soak_c3.json]
+  python tools/soak_full_parity.py [--config c3|c5] [--workers 16] [--out profiles/round4/soak_c3.json]
 """
 import argparse
 import json
