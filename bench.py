@@ -625,22 +625,40 @@ def other_configs(a, timeout=240.0):
     import subprocess
 
     env = {k: v for k, v in os.environ.items() if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE")}
-    res = {}
-    for cfg in ("c2", "c5"):
-        cmd = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--steps", str(a.steps), "--warmup", str(a.warmup),
-               "--burnin", str(a.burnin)]
+
+    def child(cfg, extra):
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--warmup", str(a.warmup), "--burnin", str(a.burnin)]
+        cmd += extra
         t0 = time.perf_counter()
         try:
             p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout, cwd=ROOT)
             lines = [ln for ln in p.stdout.decode().splitlines() if ln.startswith("{")]
             if p.returncode != 0 or not lines:
-                res[cfg] = {"error": f"exit {p.returncode}: {p.stderr.decode()[-400:]}"}
+                r = {"error": f"exit {p.returncode}: {p.stderr.decode()[-400:]}"}
             else:
-                res[cfg] = json.loads(lines[-1])
+                r = json.loads(lines[-1])
         except subprocess.TimeoutExpired:
-            res[cfg] = {"error": f"timed out after {timeout:.0f} s"}
-        res[cfg]["command"] = " ".join(["python3", "bench.py"] + cmd[2:])
-        res[cfg]["run_s"] = time.perf_counter() - t0
+            r = {"error": f"timed out after {timeout:.0f} s"}
+        r["command"] = " ".join(["python3", "bench.py"] + cmd[2:])
+        r["run_s"] = time.perf_counter() - t0
+        return r
+
+    res = {}
+    for cfg in ("c2", "c5"):
+        res[cfg] = child(cfg, ["--steps", str(a.steps)])
+    if a.steps != 200:
+        # the bench default K = 200 beside the driver's K (round 5's c2 / c5 figures were K = 200 windows): the
+        # timed window only (no CPU baseline, exchange, full-contract or comparison windows)
+        quick = ["--steps", "200", "--no-cpu-baseline", "--no-gather-window", "--no-full-contract", "--no-compare",
+                 "--no-other-configs"]
+        keep = ("value", "ms_per_step", "step_kernel_ms", "launch_ms", "roofline", "command", "run_s", "error")
+        for cfg in ("c2", "c3", "c5"):
+            r = child(cfg, quick)
+            k200 = {k: r[k] for k in keep if k in r}
+            if cfg == "c3":
+                res["c3_k200"] = k200
+            else:
+                res[cfg]["k200"] = k200
     return res
 
 

@@ -4264,6 +4264,7 @@ struct Game {
         w2 |= hi;
     }
     static DEV uint32_t quadOr(uint32_t v) {  // OR over the lane's quad (DPP quad_perm; whole wave)
+        LANE_AUDIT_WAVE(2);
         v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
         v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
         return v;

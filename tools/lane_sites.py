@@ -49,6 +49,10 @@ WHY = {
              "for lanes k < R and read only from lanes of work ⊂ {k < R}",
     "cycleLanes": "sq / cu / a / prm written for lanes l < nu under `if (l < nu)`; read only from lanes of "
                   "work = ballot(wk) ⊂ {l < nu}, in a uniform loop",
+    "quadOr": "helper: DPP quad_perm OR within each quad — called by maskBitsQuads in uniform flow (outside its lane "
+              "tests) with v defined on every lane (0 for lanes without a unit)",
+    "maskBitsQuads": "quadOr of v0..v2, each set on every lane (0 unless the lane's quad has a unit) before the calls, in "
+                     "the uniform pass loop",
     "closerMin": "wave_min of per-lane minima of a uniform `for (o ...)` loop",
     "farAttackBits": "`if (!ballot(far)) return` is uniform; the loop over the owned mask is uniform; cuLane is the "
                      "caller's unit word of every lane < nu (owned ⊂ {l < nu})",
@@ -76,7 +80,7 @@ def sites():
         if "#define" in l or "DEV int rl(" in l or "DEV int rlAudit" in l:
             continue
         code = l.split("//")[0]
-        if re.search(r"\brl\(|\bwave_(sum|min|incl_sum)\s*\(|\bwave_reduce\s*<", code):
+        if re.search(r"\brl\(|\bwave_(sum|min|incl_sum)\s*\(|\bwave_reduce\s*<|update_dpp\(|\bquadOr\(", code):
             out.append((i, fn, l.strip()))
     return out
 

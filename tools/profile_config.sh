@@ -12,7 +12,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG/$CFG
 mkdir -p "$OUT"
-BARGS="--config $CFG --steps 100 --warmup 10 --burnin 1000 --no-cpu-baseline --no-compare --no-gather-window --no-full-contract $*"
+BARGS="--config $CFG --steps 100 --warmup 10 --burnin 1000 --no-cpu-baseline --no-compare --no-gather-window --no-full-contract --no-other-configs $*"
 SQ="SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_INSTS_LDS GRBM_GUI_ACTIVE"
 # the counters describe THIS library: bench.py ignores a pmc_<cfg>.json whose hash differs
 python -c "from microrts_amd._lib import device_code_sha256; print(device_code_sha256())" > "$OUT/code.sha256" || exit $?
