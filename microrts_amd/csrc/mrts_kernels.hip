@@ -173,6 +173,9 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SAMPLE_UNIFIED
 #define MRTS_SAMPLE_UNIFIED 1
 #endif
+#ifndef MRTS_PO_ROWS  // PO maps up to 32 wide: the ranged attack bits from unit row bitmaps too (round 6)
+#define MRTS_PO_ROWS 1
+#endif
 #ifndef MRTS_MASK_QUADS  // c3: each idle unit's mask bits computed by a quad of lanes, one per direction (round 6)
 #define MRTS_MASK_QUADS 1
 #endif
@@ -3786,6 +3789,9 @@ struct Game {
         int32_t* out = D.obs + (size_t)(2 * g) * D.C * HW;
         const __amdgpu_buffer_rsrc_t rs = bufRsrc(out, (uint32_t)(2 * D.C * HW * 4));
         const uint64_t deadAny = deadM0 | deadM1;
+#ifdef MRTS_DIAG_HELPER_NORENDER  // diagnostic build only: the helper skips the render items (output wrong)
+        n = 0;
+#endif
         for (int it = l; it < n; it += 64) {
             const uint32_t e = poList[it];
             const int v = (int)(e >> 15), c4 = (int)(e & 0x7FFFu);  // lane = 4 consecutive cells of one row
@@ -4671,8 +4677,13 @@ struct Game {
         uint32_t* nb = (uint32_t*)rseq;  // cycle() scratch, free here: [slot i][MW] new bits
         if (l < NW) nb[l] = 0;
         // per-player unit row bitmaps for the range > 1 attack bits (rslot scratch, free here)
-        uint32_t* rows = (uint32_t*)rslot;
-        const bool rowB = W <= 32 && 2 * H <= 32;
+        // (partially observable games on maps of 16 to 32 columns: in the tail of `scell`, free during the masks —
+        // the general render's scratch map is done with, and a helper wave's packs and cell map end at word 896 of
+        // 32x32's 1,024 (round 6: c5's ranged units had taken farAttackBits' walk over every live unit))
+        const bool rowS = W <= 32 && 2 * H <= 32;
+        const bool rowP = MRTS_PO_ROWS && !rowS && po && W <= 32 && W >= 16 && 2 * H <= 64;
+        uint32_t* rows = rowS ? (uint32_t*)rslot : rowP ? scell + (HW - 2 * H) : nullptr;
+        const bool rowB = rowS || rowP;
         if (rowB && l < 2 * H) rows[l] = 0;
         int si = -1;  // slot index of this lane's unit record, -1 = none
         uint32_t cu = 0;
@@ -4701,7 +4712,9 @@ struct Game {
 #endif
             MPHASE(17);
             const int carried = l < nu ? res[l] : 0;
-            if (MRTS_MASK_QUADS && rowB && !recOut) {  // four lanes per idle unit (c3, 8x8: the row bitmaps exist)
+            // four lanes per idle unit (c3, 8x8: the row bitmaps exist; its scratch, rseq words 16..63, lies past
+            // the new row sets nb only while they take <= 16 words)
+            if (MRTS_MASK_QUADS && rowB && !recOut && NW <= 16) {
                 wsync();
                 maskBitsQuads(T, si, cu, carried, rows, w0, w1, w2);
             } else {
@@ -5144,7 +5157,9 @@ DEV void helperLoopPO(Game& G, uint32_t* hdr, int niter) {
             }
             G.renderPOPacked(pk, ph, rows0, hcell, k == niter - 1);
             if (k + 1 == niter) ldsBarrier();  // S_last: the game's masks of the last step are out
+#ifndef MRTS_DIAG_HELPER_NORECORDS  // diagnostic build only: the helper skips the record stores (output wrong)
             G.storeRecordsHelp(recs);  // step k's mask records and policy rows (written before S_k)
+#endif
         } else if (f & 8u) {
             // the game's live state, as its own writeObsPO call would see it (the general render
             // overwrites `scell`, so the pack's record words are taken first)
