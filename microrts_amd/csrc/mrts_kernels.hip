@@ -191,6 +191,12 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SAMPLE32  // the sampler's type / produce-type picks in 32-bit operations, the packed word direct (round 5)
 #define MRTS_SAMPLE32 1
 #endif
+#ifndef MRTS_QUADS_PO  // the quads on the partially observable 32x32 instances too (round 6)
+#define MRTS_QUADS_PO 1
+#endif
+#ifndef MRTS_WALK32  // the cost walks on the 32x32 partially observable instances too, base reservations included (round 6)
+#define MRTS_WALK32 1
+#endif
 #ifndef MRTS_INDEX_WALK  // buildIndex's PRODUCE costs by a walk over their lanes (round 5); 0 = wave reductions
 #define MRTS_INDEX_WALK 1
 #endif
@@ -1432,25 +1438,40 @@ struct Game {
         ixValid = false;  // `bits` now holds this view's set
         for (int i = lid(); i < NB; i += 64) bits[i] = 0;
         wsync();
-        int s0 = 0, s1 = 0;
-        for (int o = lid(); o < nu; o += 64) {
-            const uint32_t a = ua[o];
-            if (!(a & UA_PRESENT)) continue;
-            if (po && !snap_in(snap[o], p)) continue;
-            const int t = ua_type(a);
-            if (t == T_MOVE || t == T_PRODUCE) {
-                const uint32_t c = uc[o];
-                const int d = par[o];
-                const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
-                atomicOr(&bits[pos >> 5], 1u << (pos & 31));
-                if (t == T_PRODUCE) {
-                    if (uplay(c) == 0) s0 += U.cost[ua_ut(a)];
-                    else s1 += U.cost[ua_ut(a)];
+        int s0 = 0, s1 = 0, w0 = 0, w1 = 0;
+        for (int o0 = 0; o0 < nu; o0 += 64) {
+            const int o = o0 + lid();
+            int key = -1;  // walk: a PRODUCE's cost | player << 16
+            if (o < nu) {
+                const uint32_t a = ua[o];
+                const int t = ua_type(a);
+                if ((a & UA_PRESENT) && (!po || snap_in(snap[o], p)) && (t == T_MOVE || t == T_PRODUCE)) {
+                    const uint32_t c = uc[o];
+                    const int d = par[o];
+                    const int pos = (uy(c) + dyo(d)) * W + ux(c) + dxo(d) + W;
+                    atomicOr(&bits[pos >> 5], 1u << (pos & 31));
+                    if (t == T_PRODUCE) {
+                        key = U.cost[ua_ut(a)] | ((uplay(c) == 0 ? 0 : 1) << 16);
+                        if (uplay(c) == 0) s0 += U.cost[ua_ut(a)];
+                        else s1 += U.cost[ua_ut(a)];
+                    }
+                }
+            }
+            if (walk) {  // the few PRODUCE lanes: one lane read each (buildIndex's walk)
+                for (uint64_t mm = ballot(key >= 0); mm; mm &= mm - 1) {
+                    const int kv = uni(rl(key, __builtin_ctzll(mm)));
+                    if ((kv >> 16) == 0) w0 += kv & 0xFFFF;
+                    else w1 += kv & 0xFFFF;
                 }
             }
         }
-        r0 = wave_sum(s0);
-        r1 = wave_sum(s1);
+        if (walk) {
+            r0 = w0;
+            r1 = w1;
+        } else {
+            r0 = wave_sum(s0);
+            r1 = wave_sum(s1);
+        }
         wsync();
     }
 
@@ -4281,11 +4302,10 @@ struct Game {
     // as one lane per unit, in about a quarter of the instructions.  rows complete (wsync'd);
     // rseq words 16..63 are scratch here.  Whole wave.
     DEV void maskBitsQuads(const MaskTables& T, int si, uint32_t cu, int carried, const uint32_t* rows, uint32_t& w0,
-                           uint32_t& w1, uint32_t& w2) {
+                           uint32_t& w1, uint32_t& w2, uint32_t* qb /* [16][3] scratch words */) {
         const int l = lid();
         const uint64_t m = ballot(si >= 0);
         const int RI = __popcll(m), r = lanes_below(m);
-        uint32_t* qb = (uint32_t*)rseq + 16;  // [16][3]
         const int q = l >> 2, d = l & 3;
         for (int p0 = 0; p0 < RI; p0 += 16) {
             const bool mine = si >= 0 && r >= p0 && r < p0 + 16;
@@ -4712,11 +4732,13 @@ struct Game {
 #endif
             MPHASE(17);
             const int carried = l < nu ? res[l] : 0;
-            // four lanes per idle unit (c3, 8x8: the row bitmaps exist; its scratch, rseq words 16..63, lies past
-            // the new row sets nb only while they take <= 16 words)
-            if (MRTS_MASK_QUADS && rowB && !recOut && NW <= 16) {
+            // four lanes per idle unit wherever the row bitmaps exist: its 48 scratch words are rseq words 16..63
+            // while the new row sets nb take <= 16 words, else (32x32 views) the 48 words of scell's tail below
+            // the rows (past a helper wave's packs and cell map, which end at word 896 of 1,024)
+            uint32_t* const qb = NW <= 16 ? (uint32_t*)rseq + 16 : (rowP && HW - 2 * H - 48 >= 896) ? rows - 48 : nullptr;
+            if (MRTS_MASK_QUADS && rowB && qb && (MRTS_QUADS_PO || !po)) {
                 wsync();
-                maskBitsQuads(T, si, cu, carried, rows, w0, w1, w2);
+                maskBitsQuads(T, si, cu, carried, rows, w0, w1, w2, qb);
             } else {
             if (si >= 0) maskBitsFast(T, cu, carried, w0, w1, w2);
             MPHASE(18);
@@ -5195,7 +5217,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
     const int game = balanced ? balancedGame(D) : -1;
     Game G(P, D, stateArg, FIX ? stateWords(FCAP, FIX * FIX) : D.state_words, smem, FIX ? FIX : D.H, FIX ? FIX : D.W, FIX ? FIX * FIX : D.HW, FIX ? FCAP : D.CAP,
            FIX ? FPO : P.partial_obs != 0, FIX ? 79 : P.utt.K, FIX ? 7 : P.utt.ntypes, FIX ? 7 : P.utt.maxAttackRadius, MULTI, game,
-           MRTS_INDEX_WALK && FIX == 16);
+           MRTS_INDEX_WALK && (FIX == 16 || (MRTS_WALK32 && FIX == 32)));
     // the partially observable helper wave: one packed render per step (helperLoopPO)
     uint32_t* const poHelpHdr = (HELP && FPO) ? (uint32_t*)(smem + D.help_off) : nullptr;
     if (HELP && FPO && threadIdx.x >= 64) {
