@@ -191,6 +191,9 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_SAMPLE32  // the sampler's type / produce-type picks in 32-bit operations, the packed word direct (round 5)
 #define MRTS_SAMPLE32 1
 #endif
+#ifndef MRTS_PO_VRES  // PO self-play: the views' base reservations in their own bitmap (round 6: measured -0.5 %, off)
+#define MRTS_PO_VRES 0
+#endif
 #ifndef MRTS_QUADS_PO  // the quads on the partially observable 32x32 instances too (round 6)
 #define MRTS_QUADS_PO 1
 #endif
@@ -1102,6 +1105,12 @@ struct Game {
         }
         const bool useIx = !po && (HW + 2 * W + 31) / 32 <= 64;  // PO: the view's reservations (baseReservations)
         if (useIx) buildIndex();  // while the rows are in flight
+        // PO (round 6): each view's base reservations go to a bitmap of their own in the top words of `scell` (free
+        // during the issue: the general render's scratch map is done with; a helper wave's packs and cell map end at
+        // word 896 of 32x32's 1,024), so the issue index in `bits` stays valid across both players' issues instead of
+        // being rebuilt after each view's acceptance chain
+        const int NBv = (HW + 2 * W + 31) / 32;
+        uint32_t* const vres = (MRTS_PO_VRES && po && NBv <= 64 && HW - NBv >= (HW == 1024 ? 896 : 0)) ? scell + (HW - NBv) : nullptr;
 #ifdef MRTS_ABLATE
         if (useIx && ab(AB_INDEX)) buildIndex();
 #endif
@@ -1136,7 +1145,7 @@ struct Game {
                 run0 = sumProd0;
                 run1 = sumProd1;
             } else {
-                baseReservations(p, run0, run1);
+                baseReservations(p, run0, run1, vres);
             }
             curP = p;
             const bool mine = idle && pl == p;
@@ -1156,7 +1165,7 @@ struct Game {
 #endif
                 MPHASE(23);
                 int irank = 0;
-                const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), t, pr, c, adec, useIx, irank);
+                const uint64_t acc = acceptChain(p, run0, run1, cand, rank, __popcll(m), t, pr, c, adec, useIx || vres, irank, vres);
                 MPHASE(2);
                 isPA = (acc >> l) & 1ull;
                 int tt = 0, prm = 0, ttx = 0, tty = 0, tut = 0;
@@ -1433,9 +1442,11 @@ struct Game {
 
     // Base reservations of every current assignment the deciding view holds (PlayerAction.java:387-394,
     // merged as ResourceUsage.java:92-97); in a PO view only snapshot units' assignments count.
-    DEV void baseReservations(int p, int& r0, int& r1) {
+    // tgt: the bitmap to fill (null: `bits`, which then no longer holds the issue index)
+    DEV void baseReservations(int p, int& r0, int& r1, uint32_t* tgt = nullptr) {
         const int NB = (HW + 2 * W + 31) / 32;
-        ixValid = false;  // `bits` now holds this view's set
+        uint32_t* const bits = tgt ? tgt : this->bits;
+        if (!tgt) ixValid = false;  // `bits` now holds this view's set
         for (int i = lid(); i < NB; i += 64) bits[i] = 0;
         wsync();
         int s0 = 0, s1 = 0, w0 = 0, w1 = 0;
@@ -1579,7 +1590,7 @@ struct Game {
     // player's running sum cannot change during p's chain: if it blocks (ResourceUsage.java:38-46),
     // every candidate is rejected.
     DEV uint64_t acceptChainReg(int p, int& run0, int& run1, int rank, int n, bool usesPos, int tpos, int cost, int NB,
-                                bool keepBits, int& irank) {
+                                bool keepBits, int& irank, uint32_t* RB) {
         const int l = lid();
         {
             // Parallel form for the common case: when no candidate's used position is reserved already,
@@ -1596,12 +1607,12 @@ struct Game {
                     // copy of the reservation words (rseq, free here) and is in conflict when the bit was set —
                     // by the base reservations or by another candidate (one of each equal pair sees it)
                     uint32_t* cp = (uint32_t*)rseq;
-                    if (l < NB) cp[l] = bits[l];
+                    if (l < NB) cp[l] = RB[l];
                     wsync();
                     if (up) conf = (atomicOr(&cp[tpos >> 5], 1u << (tpos & 31)) >> (tpos & 31)) & 1u;
                     wsync();
                 } else {
-                    conf = up && ((bits[tpos >> 5] >> (tpos & 31)) & 1u);
+                    conf = up && ((RB[tpos >> 5] >> (tpos & 31)) & 1u);
                     for (uint64_t mm = ballot(up); mm; mm &= mm - 1) {
                         const int k = __builtin_ctzll(mm);
                         const int tk = rl(tpos, k);  // read in uniform flow: lane k itself is off inside the test below
@@ -1617,14 +1628,14 @@ struct Game {
                 if (!ballot(conf) && runP + sumc <= presP) {
                     if (p == 0) run0 = runP + sumc;
                     else run1 = runP + sumc;
-                    if (!keepBits && up) atomicOr(&bits[tpos >> 5], 1u << (tpos & 31));
+                    if (!keepBits && up) atomicOr(&RB[tpos >> 5], 1u << (tpos & 31));
                     if (cand) irank = rank;
                     wsync();
                     return ballot(cand);
                 }
             }
         }
-        uint32_t bv = l < NB ? bits[l] : 0u;
+        uint32_t bv = l < NB ? RB[l] : 0u;
         if (rank >= 0) rseq[rank] = (int)(((uint32_t)usesPos << 31) | ((uint32_t)cost << 16) | ((uint32_t)tpos & 0xFFFFu));
         wsync();
         const int keyR = l < n ? rseq[l] : 0;
@@ -1652,7 +1663,7 @@ struct Game {
         if (p == 0) run0 = runP;
         else run1 = runP;
         wsync();  // rseq is read again by the next chain
-        if (!keepBits && l < NB) bits[l] = bv;
+        if (!keepBits && l < NB) RB[l] = bv;
         const bool isAcc = rank >= 0 && ((accR >> rank) & 1ull);
         if (isAcc) irank = __popcll(accR & ((1ull << rank) - 1ull));
         return ballot(isAcc);
@@ -1662,12 +1673,12 @@ struct Game {
     // keepBits: `bits` is left as it was (the chain's additions stay in registers)
     // irank: each accepted lane's rank among the accepted (the pa's issue order)
     DEV uint64_t acceptChain(int p, int& run0, int& run1, bool cand, int rank, int n, int t, int pr, int c, uint32_t a,
-                             bool keepBits, int& irank) {
+                             bool keepBits, int& irank, uint32_t* RB = nullptr) {
         const bool usesPos = cand && (t == T_MOVE || t == T_PRODUCE);
         const int tpos = c + dyo(pr) * W + dxo(pr) + W;  // ResourceUsage position (UnitAction.java:254-291)
         const int cost = (cand && t == T_PRODUCE) ? U.cost[ua_ut(a)] : 0;
         const int NB = (HW + 2 * W + 31) / 32;
-        if (NB <= 64) return acceptChainReg(p, run0, run1, rank, n, usesPos, tpos, cost, NB, keepBits, irank);
+        if (NB <= 64) return acceptChainReg(p, run0, run1, rank, n, usesPos, tpos, cost, NB, keepBits, irank, RB ? RB : bits);
         uint64_t acc = 0;
         int nacc = 0;
         for (int r = 0; r < n; r++) {
