@@ -433,7 +433,8 @@ def test_exchange_needs_an_observation_buffer():
                                                          ("maps/BWDistantResources32x32.xml", False, 9, 17, True),
                                                          ("maps/16x16/basesWorkers16x16.xml", False, 0, 300, True),
                                                          ("maps/8x8/basesWorkers8x8.xml", True, 0, 300, True),
-                                                         ("maps/8x8/basesWorkers8x8.xml", False, 0, 400, "dead")])
+                                                         ("maps/8x8/basesWorkers8x8.xml", False, 0, 400, "dead"),
+                                                         ("maps/16x16/EightBasesWorkers16x16.xml", False, 0, 300, "many")])
 def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
     """the compact observation exchange (mrts_rollout_*_records_dev) on a one-rank
     RCCL communicator.  Every step's records, all-gathered and rendered back on the receiving side
@@ -444,12 +445,17 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
     po: partially observable handles (two record words per unit of either view; the receiver paints the
     sight disks) — the 32x32 map runs c5's helper-wave kernel in the records rollout; po = "dead": 266
     masked random steps on 8x8, long enough that a view shows units that died in the step (their hp <= 0,
-    kept by the view's snapshot until the compaction), and the test checks that one did."""
+    kept by the view's snapshot until the compaction), and the test checks that one did.  po = "many"
+    (the 64-unit record): full observability on a map that starts with 64 units, records
+    sized to the map's cell count (one unit per cell at most, so no game can overflow them) — the games pass
+    64 live units (the general paths beyond one wave) and every step still renders exactly."""
     torch = _torch()
     from microrts_amd import DeviceVecEnv
 
+    many = po == "many"
+    po = False if many else po
     n_sp = 64
-    kw = dict(partial_obs=True, max_units=256) if po else {}
+    kw = dict(partial_obs=True, max_units=256) if po else dict(max_units=256) if many else {}
     A = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform, **kw)
     B = DeviceVecEnv(n_sp, 0, max_steps, [mp] * n_sp, seed=23, with_masks=not uniform, **kw)
     A.set_multi_step(False)
@@ -458,11 +464,14 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
         if not uniform:
             e.random_policy(SEED, 0)
     _exchange_env(B)
-    words = B.set_records(64, spl)
+    units = 256 if many else 64
+    words = B.set_records(units, spl)
+    assert words == units + 1 or po
     B.set_step_responses(100)  # every step's reward / done
     S = n_sp
     k = 0
     dead_seen = False
+    most = 0
     for n in (1, 40, 25) + ((100, 100) if po == "dead" else ()):
         want, wantR, wantD = [], [], []
         for j in range(n):
@@ -494,11 +503,15 @@ def test_record_exchange_one_rank(mp, uniform, spl, max_steps, po):
         for name in ("obs", "actions") + (() if uniform else ("masks",)):  # (reward / done: the ring's, above)
             assert torch.equal(getattr(A, name), getattr(B, name)), f"{name} after {k}"
         for s in range(0, n_sp, 2):
-            assert np.array_equal(A.dump_state(s), B.dump_state(s)), f"state slot {s} after {k}"
+            d = A.dump_state(s)
+            assert np.array_equal(d, B.dump_state(s)), f"state slot {s} after {k}"
+            most = max(most, int(d[4]))
     for e in (A, B):
         assert not e.error_flags().any()
     if po == "dead":
         assert dead_seen, "no view showed a unit that died in its step"
+    if many:
+        assert most > 64, f"the games never passed 64 units (most {most})"
     # a record too small for the games' unit lists is an error, not a silent truncation
     assert B.set_records(2, 0) == (5 if po else 3)
     recv = B.records_buffer(2)
