@@ -621,7 +621,9 @@ def other_configs(a, timeout=240.0):
     games, unmasked uniform rows) and c5 (configs[4] per GPU: 32x32, 2048 partially observable games, masked
     policy) — each a child bench.py with the same K / W / burn-in, run after this process has released its
     handle and process group; its JSON line (value, ms_per_step, roofline with the matching-hash PMC file,
-    cpu_baseline, ...) nested under its name.  A child that fails or overruns leaves {"error": ...} there."""
+    cpu_baseline, ...) nested under its name.  When the driver's K is not 200, each of c2 / c3 / c5 also gets a
+    quick K = 200 child without the CPU baseline (`configs.c2.k200`, `configs.c5.k200`, `configs.c3_k200`), the
+    window the builder's own figures are quoted at.  A child that fails or overruns leaves {"error": ...} there."""
     import subprocess
 
     env = {k: v for k, v in os.environ.items() if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE")}

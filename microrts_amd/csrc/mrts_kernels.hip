@@ -4762,11 +4762,16 @@ struct Game {
             }
             }
 #ifdef MRTS_ABLATE
-            if (ab(AB_MASKBITS) && rowB) {
+            if (ab(AB_MASKBITS) && rowB) {  // a second copy of whichever form ran above
                 uint32_t v0 = 0, v1 = 0, v2 = 0;
                 const uint32_t cu2 = launder(cu);
-                if (si >= 0) maskBitsFast(T, cu2, launder(carried), v0, v1, v2);
-                farAttackRows(far, cu2, rows, v0, v1, v2);
+                if (MRTS_MASK_QUADS && qb && (MRTS_QUADS_PO || !po)) {
+                    wsync();
+                    maskBitsQuads(T, launder(si), cu2, launder(carried), rows, v0, v1, v2, qb);
+                } else {
+                    if (si >= 0) maskBitsFast(T, cu2, launder(carried), v0, v1, v2);
+                    farAttackRows(si >= 0 && ((T.attackFar >> utyp(cu2)) & 1u), cu2, rows, v0, v1, v2);
+                }
                 keepv(v0 ^ v1 ^ v2);
             }
 #endif
