@@ -163,6 +163,11 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_BAL_MIN_ITER
 #define MRTS_BAL_MIN_ITER 64
 #endif
+// the cost a game posts for the next placement: 0 = its unit count, 1 = units + own idle units (the estimate the
+// SIMD rank uses: the step's decode / issue / mask / policy work grows with the idle ones)
+#ifndef MRTS_BAL_COST_IDLE
+#define MRTS_BAL_COST_IDLE 0
+#endif
 // 1: rollout timing events ride on the kernel dispatch (hipExtLaunchKernelGGL); 0: separate records
 #ifndef MRTS_EXT_EVENTS
 #define MRTS_EXT_EVENTS 1
@@ -5626,9 +5631,11 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
     if (rebalance) {  // post this game's final unit count; the launch's LAST wave writes the next placement
         const uint32_t tag = D.fwd_stamp & 0xFFFFu;
         uint32_t last = 0;
+        const int cost = MRTS_BAL_COST_IDLE ? G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0))
+                                            : G.nu;
         if (lane_id() == 0) {
             // agent scope, written through: the last wave may sit on another XCD (another L2)
-            __hip_atomic_store(D.bal + BAL_COST + G.g, (int32_t)((tag << 16) | (uint32_t)(G.nu < 255 ? G.nu : 255)),
+            __hip_atomic_store(D.bal + BAL_COST + G.g, (int32_t)((tag << 16) | (uint32_t)(cost < 255 ? cost : 255)),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             drainStores();  // the cost is in memory before this wave counts itself
             // waves of this block's class (b % 8) finished in this launch, wrapping to 0 at the last
