@@ -163,10 +163,19 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_BAL_MIN_ITER
 #define MRTS_BAL_MIN_ITER 64
 #endif
-// the cost a game posts for the next placement: 0 = its unit count, 1 = units + own idle units (the estimate the
-// SIMD rank uses: the step's decode / issue / mask / policy work grows with the idle ones)
+// c5 (partially observable 32x32 self-play with helper waves) placed the same way: the dispatcher puts the game
+// waves of blocks b and b + n / 2 on one SIMD (round 6 span data, profiles/round6/placement_c5.json); c5 +0.6 %
+#ifndef MRTS_BALANCE_PO
+#define MRTS_BALANCE_PO 1
+#endif
+#ifndef MRTS_BAL_PO_GS
+#define MRTS_BAL_PO_GS 2
+#endif
+// the cost a game posts for the next placement: 0 = its unit count, 1 = units + own idle units at the launch's
+// last step (the estimate the SIMD rank uses: a step's decode / issue / mask / policy work grows with the idle
+// ones; round 6: c3 K = 20 kernel -0.6 %, c5 +0.4 % over 0; the estimate averaged over the launch's steps was worse)
 #ifndef MRTS_BAL_COST_IDLE
-#define MRTS_BAL_COST_IDLE 0
+#define MRTS_BAL_COST_IDLE 1
 #endif
 // 1: rollout timing events ride on the kernel dispatch (hipExtLaunchKernelGGL); 0: separate records
 #ifndef MRTS_EXT_EVENTS
@@ -5074,13 +5083,13 @@ DEV int simdRankStep(SimdRank& r, uint32_t est) {
     return rank;
 }
 
-// Balanced game placement (multi-step c3 launches, KDyn.bal).  With the rank priority above the four
+// Balanced game placement (multi-step c3 and c5 launches, KDyn.bal).  With the rank priority above the four
 // games of a SIMD finish together, and a launch ends with its slowest SIMD: round 3 span data, a SIMD's
 // end time correlates 0.86-0.96 with its games' total unit count and the slowest SIMD ends 8 % after the
 // mean.  The dispatcher places blocks b, b + n/4, b + 2n/4, b + 3n/4 on one SIMD (one dispatch round of
-// four waves per SIMD; identical in every launch and process measured), so a permutation of games over
-// blocks that gives each such group a heavy-to-light mix balances the SIMDs.  Each game posts its unit
-// count at the end of a launch; the last wave of each XCD class counting-sorts that class's posted
+// four waves per SIMD; identical in every launch and process measured; c5's 128-thread blocks: the game waves
+// of b and b + n/2), so a permutation of games over blocks that gives each such group a heavy-to-light mix
+// balances the SIMDs.  Each game posts its cost (units + own idle units, MRTS_BAL_COST_IDLE) at the end of a launch; the last wave of each XCD class counting-sorts that class's posted
 // counts and writes its part of the permutation for the next launches — snake order over the groups,
 // so a group gets one game from each quarter of the order, heavy paired with light — and the stamp.  A launch whose predecessor on the
 // handle left a permutation uses it (block b runs game perm[b]), else identity.  The permutation is
@@ -5095,12 +5104,13 @@ DEV int balancedGame(const KDyn& D) {
     const int32_t pg = __builtin_nontemporal_load(D.bal + BAL_COST + n + (int)blockIdx.x);
     return hdr1 != 0 ? pg : (int)blockIdx.x;
 }
-DEV void balancePerm(const KDyn& D, uint32_t* hist, int c) {
+DEV void balancePerm(const KDyn& D, uint32_t* hist, int c, int GS) {
     // games stay on their XCD: block b runs on XCD b % 8 and the four blocks of a SIMD group share b % 8,
     // so the permutation only moves games between blocks of the same residue class c (the state a game
     // left in that XCD's L2 stays near), and each class's LAST wave sorts that class alone: n / 8
     // games, n / 32 SIMD groups, the snake order as above (1/8 of the work on the launch's tail)
-    const int n = (int)gridDim.x, l = lane_id(), Q = n >> 5, per = n >> 9;  // per: games per lane
+    // GS: games per SIMD group (c3: four game waves per SIMD; c5: MRTS_BAL_PO_GS), blocks n / GS apart
+    const int n = (int)gridDim.x, l = lane_id(), Q = (int)((uint32_t)n / (8u * (uint32_t)GS)), per = n >> 9;  // per: games per lane
     int32_t* const cost = D.bal + BAL_COST;
     int32_t* const perm = cost + n;
     const uint32_t tag = D.fwd_stamp & 0xFFFFu;
@@ -5230,9 +5240,10 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
         return;
     }
     const KStatic& P = *PS;
-    // balanced placement (c3's multi-step kernel): this block's game from the previous launch's permutation
+    // balanced placement (c3's and c5's multi-step kernels): this block's game from the previous launch's permutation
     // (balancePerm: a multiple of 512 games, at most 8 per lane and class)
-    const bool balanced = MULTI && MRTS_BALANCE && FIX == 16 && !FPO && D.bal != nullptr && (gridDim.x & 511) == 0 &&
+    const bool balanced = MULTI && MRTS_BALANCE && ((FIX == 16 && !FPO) || (MRTS_BALANCE_PO && FIX == 32 && FPO && HELP)) &&
+                          D.bal != nullptr && (gridDim.x & 511) == 0 &&
                           gridDim.x <= 4096;
     const bool rebalance = balanced && D.n_iter >= MRTS_BAL_MIN_ITER;  // this launch writes the next permutation
     const int game = balanced ? balancedGame(D) : -1;
@@ -5646,7 +5657,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
         }
         if (uniu(last)) {
             wsync();
-            balancePerm(D, (uint32_t*)smem, (int)(blockIdx.x & 7u));
+            balancePerm(D, (uint32_t*)smem, (int)(blockIdx.x & 7u), FIX == 16 ? 4 : MRTS_BAL_PO_GS);
         }
     }
     PHASE(10);

@@ -64,6 +64,17 @@ def main():
                "start_spread_us": round(float(us(st).max()), 2), "game_us_mean": round(float(((en - st) / 100).mean()), 2),
                "game_end_us": {"mean": round(float(us(en).mean()), 2), "max": round(float(us(en).max()), 2)},
                "simd_last_end_us": {"mean": round(float(last.mean()), 2), "max": round(float(last.max()), 2)}}
+        if mode == "multi" and os.environ.get("PLACEMENT"):  # which blocks share a SIMD (game waves only)
+            groups = [np.flatnonzero(inv == u) for u in range(len(uniq))]
+            sizes = np.bincount([len(gq) for gq in groups])
+            offs = {}
+            for gq in groups:
+                t = tuple(int(x) for x in (gq - gq[0]))
+                offs[t] = offs.get(t, 0) + 1
+            top = sorted(offs.items(), key=lambda kv: -kv[1])[:4]
+            out["placement"] = {"simds": len(uniq), "games_per_simd_hist": sizes.tolist(),
+                                "block_offset_patterns": [[list(k), v] for k, v in top],
+                                "first_groups": [gq.tolist() for gq in groups[:4]]}
         if mode == "multi":  # the LAST iteration's milestones (each stamp is overwritten per iteration)
             m = {name: v for name, v in zip(MILES, mi)}
             seq = (["it_start", "rows_index"] if STEPM else []) + ["decoded", "issued", "cycled", "outcome", "obs", "masks"]
