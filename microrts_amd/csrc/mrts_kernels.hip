@@ -160,6 +160,11 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_BALANCE
 #define MRTS_BALANCE 1
 #endif
+// k_env's step body reads KDyn through the laundered pointer too (round 6: SGPR spills 153 -> 136, no VGPR spills,
+// but c3 / c5 / c2 +-0 to -0.6 %: the re-read fields wait on scalar loads where the spilled ones were a readlane)
+#ifndef MRTS_BODY_LAUNDER
+#define MRTS_BODY_LAUNDER 0
+#endif
 #ifndef MRTS_BAL_MIN_ITER
 #define MRTS_BAL_MIN_ITER 64
 #endif
@@ -5324,6 +5329,12 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
         G.nextStep();
         freshObs = true;
     }
+#if MRTS_BODY_LAUNDER
+    // the step body reads the kernel argument through the Game's per-iteration opaque pointer too (as its
+    // methods do, freshLane): the by-value argument's fields and the conditions derived from them were
+    // loaded once before the loop and held across it in spilled SGPRs — a v_readlane per use, every step
+    auto& D = *G.Dp;
+#endif
     if (HELP && !FPO) G.helpRows = helpBuf + (it & 1) * 2 * 64;
     G.lastIt = it == niter - 1;
     G.firstIt = it == 0;
