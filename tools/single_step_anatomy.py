@@ -72,6 +72,10 @@ def main():
                 t = tuple(int(x) for x in (gq - gq[0]))
                 offs[t] = offs.get(t, 0) + 1
             top = sorted(offs.items(), key=lambda kv: -kv[1])[:4]
+            xcc_of = (uniq // (8 * 2 * 64)).astype(np.int64)  # key = ((xcc * 8 + se) * 2 + sh) * 64 + cu * 4 + simd
+            out["per_xcd"] = [{"xcd": int(x), "game_end_mean_us": round(float(us(en)[xcc == x].mean()), 2),
+                               "simd_last_end_mean_us": round(float(last[xcc_of == x].mean()), 2),
+                               "simd_last_end_max_us": round(float(last[xcc_of == x].max()), 2)} for x in np.unique(xcc)]
             out["placement"] = {"simds": len(uniq), "games_per_simd_hist": sizes.tolist(),
                                 "block_offset_patterns": [[list(k), v] for k, v in top],
                                 "first_groups": [gq.tolist() for gq in groups[:4]]}
