@@ -179,12 +179,6 @@ DEV int lane_id() { return (int)threadIdx.x; }
 // the cost a game posts for the next placement: 0 = its unit count, 1 = units + own idle units at the launch's
 // last step (the estimate the SIMD rank uses: a step's decode / issue / mask / policy work grows with the idle
 // ones; round 6: c3 K = 20 kernel -0.6 %, c5 +0.4 % over 0; the estimate averaged over the launch's steps was worse)
-// 1: one permutation over all the launch's games (the LAST wave of the launch sorts them) instead of one per XCD
-// residue class: a game may change XCD, and each XCD's total load is balanced too (round 6 span data: c5's
-// per-XCD mean game end spread 4.7 %, c3's 2.4 %, from the games' own load)
-#ifndef MRTS_BAL_GLOBAL
-#define MRTS_BAL_GLOBAL 0
-#endif
 #ifndef MRTS_BAL_COST_IDLE
 #define MRTS_BAL_COST_IDLE 1
 #endif
@@ -5118,7 +5112,8 @@ DEV int balancedGame(const KDyn& D) {
 DEV void balancePerm(const KDyn& D, uint32_t* hist, int c, int GS) {
     // games stay on their XCD: block b runs on XCD b % 8 and the four blocks of a SIMD group share b % 8,
     // so the permutation only moves games between blocks of the same residue class c (the state a game
-    // left in that XCD's L2 stays near), and each class's LAST wave sorts that class alone: n / 8
+    // left in that XCD's L2 stays near; round 6: one permutation over all games, balancing the XCDs' loads
+    // too, was 1.2 % slower on c3 and -0.5 % on c5), and each class's LAST wave sorts that class alone: n / 8
     // games, n / 32 SIMD groups, the snake order as above (1/8 of the work on the launch's tail)
     // GS: games per SIMD group (c3: four game waves per SIMD; c5: MRTS_BAL_PO_GS), blocks n / GS apart
     const int n = (int)gridDim.x, l = lane_id(), Q = (int)((uint32_t)n / (8u * (uint32_t)GS)), per = n >> 9;  // per: games per lane
@@ -5166,48 +5161,6 @@ DEV void balancePerm(const KDyn& D, uint32_t* hist, int c, int GS) {
             perm[c + 8 * (q * Q + ((q & 1) ? Q - 1 - j : j))] = c + 8 * (l * per + i);
         }
     if (l == 0) D.bal[1] = (int32_t)D.fwd_stamp;  // (every class writes the same) the next launches take it
-}
-// The same over all n games at once (MRTS_BAL_GLOBAL): SIMD group k = blocks {k, k + n/GS, ...}; the sorted
-// ranks fill the groups in snake order, group k sitting on XCD k % 8, so heavy and light games spread over the
-// XCDs as well as over each XCD's SIMDs.  One wave, every game (n <= 4096: 64 per lane, two passes over the costs).
-DEV void balancePermGlobal(const KDyn& D, uint32_t* hist, int GS) {
-    const int n = (int)gridDim.x, l = lane_id(), NG = (int)((uint32_t)n / (uint32_t)GS);
-    int32_t* const cost = D.bal + BAL_COST;
-    int32_t* const perm = cost + n;
-    const uint32_t tag = D.fwd_stamp & 0xFFFFu;
-#pragma unroll
-    for (int j = 0; j < 4; j++) hist[l + 64 * j] = 0;
-    const __amdgpu_buffer_rsrc_t rs = bufRsrc(cost, (uint32_t)(n * 4));
-    wsync();
-    bool ok = true;
-    for (int g = l; g < n; g += 64) {
-        const uint32_t cv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, g * 4, 0, 17);
-        ok = ok && (cv >> 16) == tag;
-        atomicAdd(&hist[255u - (cv & 255u)], 1u);  // heaviest first
-    }
-    if (ballot(!ok)) return;  // a game has not posted: keep the old permutation
-    wsync();
-    uint32_t v[4], sum = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        v[j] = hist[4 * l + j];
-        sum += v[j];
-    }
-    const uint32_t incl = (uint32_t)wave_incl_sum((int)sum);
-    uint32_t run = incl - sum;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        hist[4 * l + j] = run;
-        run += v[j];
-    }
-    wsync();
-    for (int g = l; g < n; g += 64) {
-        const uint32_t cv = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, g * 4, 0, 17);
-        const int r = (int)atomicAdd(&hist[255u - (cv & 255u)], 1u);
-        const int q = r / NG, k = r - q * NG;
-        perm[q * NG + ((q & 1) ? NG - 1 - k : k)] = g;
-    }
-    if (l == 0) D.bal[1] = (int32_t)D.fwd_stamp;
 }
 
 // Workgroup barrier for an LDS handoff: the release / acquire fences cover LDS only, so a wave does
@@ -5711,14 +5664,12 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
             // waves of this block's class (b % 8) finished in this launch, wrapping to 0 at the last
             // (atomicInc): no reset needed, and no compare-and-swap retries (4096 contending CAS loops
             // at device scope took milliseconds)
-            const uint32_t cnt = MRTS_BAL_GLOBAL ? gridDim.x : gridDim.x / 8u;  // (global: one counter, word 10)
-            const uint32_t old = atomicInc((uint32_t*)D.bal + (MRTS_BAL_GLOBAL ? 10u : 2u + (blockIdx.x & 7u)), cnt - 1u);
-            last = old == cnt - 1u ? 1u : 0u;
+            const uint32_t old = atomicInc((uint32_t*)D.bal + 2 + (blockIdx.x & 7u), gridDim.x / 8u - 1u);
+            last = old == gridDim.x / 8u - 1u ? 1u : 0u;
         }
         if (uniu(last)) {
             wsync();
-            if (MRTS_BAL_GLOBAL) balancePermGlobal(D, (uint32_t*)smem, FIX == 16 ? 4 : MRTS_BAL_PO_GS);
-            else balancePerm(D, (uint32_t*)smem, (int)(blockIdx.x & 7u), FIX == 16 ? 4 : MRTS_BAL_PO_GS);
+            balancePerm(D, (uint32_t*)smem, (int)(blockIdx.x & 7u), FIX == 16 ? 4 : MRTS_BAL_PO_GS);
         }
     }
     PHASE(10);

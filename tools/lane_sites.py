@@ -60,8 +60,6 @@ WHY = {
     "writeMasksLanes": "as writeMasksUnits: n = popc(gone) on every lane, uniform flow",
     "balancePerm": "the last wave of an XCD class sorts in uniform flow (`if (ballot(!ok)) return` is uniform); "
                    "sum is each lane's 4-bin total",
-    "balancePermGlobal": "as balancePerm: the launch's last wave sorts in uniform flow (`if (ballot(!ok)) return` is "
-                         "uniform); sum is each lane's 4-bin total",
     "k_policy_delta": "kernel level, before any divergence: every lane's popc(dirty)",
     "k_lane_audit_probe": "the audit build's negative control (reads lane 40 from a branch only lanes 0-31 take)",
     "k_evaluate": "uniform `k < n` loop inside the uniform o0 loop; c / hpv / rv are initialised on every lane "
