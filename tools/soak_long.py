@@ -6,7 +6,9 @@ longer horizon with launches of several lengths: 1000 + 20 + 200 + 1040 + 777 + 
 game passes max_steps (2000) at least twice (auto-resets inside launches) besides its gameovers.  At each point
 every slot's observation, reward, done, masks, next action rows and state dump must equal the oracle's.
 
-  python tools/soak_long.py [c3 c5 c2] > profiles/round6/soak_long.jsonl     (GPU box; ~16 CPU threads for the oracle)
+  [SOAK_SEEDS=3] [SOAK_REPEAT=2] python tools/soak_long.py [c3 c5 c2] > profiles/round6/soak_long.jsonl
+  (GPU box; ~16 CPU threads for the oracle; SOAK_REPEAT repeats the launch sequence, SOAK_SEEDS runs up to three
+  env seeds per config)
 """
 import json
 import os
@@ -19,8 +21,9 @@ os.chdir(ROOT)
 
 from tests import test_full_size_every_game as T  # noqa: E402
 
-POINTS = (1000, 20, 200, 1040, 777, 2000, 63)
-SEEDS = {"c3": 101, "c5": 103, "c2": 107}
+POINTS = (1000, 20, 200, 1040, 777, 2000, 63) * int(os.environ.get("SOAK_REPEAT", "1"))
+SEEDS = {"c3": (101, 211, 307), "c5": (103, 223, 311), "c2": (107, 227, 313)}
+N_SEEDS = int(os.environ.get("SOAK_SEEDS", "1"))
 
 
 def heartbeat():  # a progress line every 30 s (a silent GPU-box command is taken for hung after 3 minutes)
@@ -41,17 +44,18 @@ def main():
     cfgs = sys.argv[1:] or ["c3", "c5", "c2"]
     T.POINTS = POINTS
     for cfg in cfgs:
-        mp, E, po, mu, _, uniform = T.SHAPES[cfg]
-        T.SHAPES[cfg] = (mp, E, po, mu, SEEDS[cfg], uniform)
-        t0 = time.time()
-        err = None
-        try:
-            T._every_game(cfg)
-        except AssertionError as e:
-            err = str(e)[:2000]
-        print(json.dumps({"config": cfg, "map": mp, "games": E, "env_seed": SEEDS[cfg], "points": list(POINTS),
-                          "steps": sum(POINTS), "every_game_equal": err is None, "error": err,
-                          "wall_s": round(time.time() - t0, 1)}), flush=True)
+        for seed in SEEDS[cfg][:N_SEEDS]:
+            mp, E, po, mu, _, uniform = T.SHAPES[cfg]
+            T.SHAPES[cfg] = (mp, E, po, mu, seed, uniform)
+            t0 = time.time()
+            err = None
+            try:
+                T._every_game(cfg)
+            except AssertionError as e:
+                err = str(e)[:2000]
+            print(json.dumps({"config": cfg, "map": mp, "games": E, "env_seed": seed, "points": list(POINTS),
+                              "steps": sum(POINTS), "every_game_equal": err is None, "error": err,
+                              "wall_s": round(time.time() - t0, 1)}), flush=True)
 
 
 if __name__ == "__main__":
