@@ -39,9 +39,28 @@ def heartbeat():  # a progress line every 30 s (a silent GPU-box command is take
     threading.Thread(target=beat, daemon=True).start()
 
 
+def single_step_form():
+    """SOAK_FORM=single: the same rollouts as one launch per step (DeviceVecEnv.set_multi_step(False): the
+    single-step kernels, the gameStep(action) drop-in's form, no helper wave)"""
+    from microrts_amd import DeviceVecEnv
+
+    orig = DeviceVecEnv.__init__
+
+    def init(self, *a, **k):
+        orig(self, *a, **k)
+        self.set_multi_step(False)
+
+    DeviceVecEnv.__init__ = init
+    DeviceVecEnv.fused_multi_step = True  # (the harness asserts the bench's shape; the launches are single-step)
+    DeviceVecEnv.multi_step_capable = True
+
+
 def main():
     heartbeat()
     cfgs = sys.argv[1:] or ["c3", "c5", "c2"]
+    form = os.environ.get("SOAK_FORM", "bench")
+    if form == "single":
+        single_step_form()
     T.POINTS = POINTS
     for cfg in cfgs:
         for seed in SEEDS[cfg][:N_SEEDS]:
@@ -53,7 +72,7 @@ def main():
                 T._every_game(cfg)
             except AssertionError as e:
                 err = str(e)[:2000]
-            print(json.dumps({"config": cfg, "map": mp, "games": E, "env_seed": seed, "points": list(POINTS),
+            print(json.dumps({"config": cfg, "form": form, "map": mp, "games": E, "env_seed": seed, "points": list(POINTS),
                               "steps": sum(POINTS), "every_game_equal": err is None, "error": err,
                               "wall_s": round(time.time() - t0, 1)}), flush=True)
 
