@@ -165,12 +165,6 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_BODY_LAUNDER
 #define MRTS_BODY_LAUNDER 0
 #endif
-#ifndef MRTS_PO_PRIO
-#define MRTS_PO_PRIO 0
-#endif
-#ifndef MRTS_PRIO_PO  // 0: partially observable games keep priority 0 (A/B builds)
-#define MRTS_PRIO_PO 1
-#endif
 #ifndef MRTS_BAL_MIN_ITER
 #define MRTS_BAL_MIN_ITER 64
 #endif
@@ -5346,7 +5340,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
     G.lastIt = it == niter - 1;
     G.firstIt = it == 0;
     bool snapTaken = false;
-    if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO) && !(FPO && !MRTS_PRIO_PO)) {
+    if (MODE != MODE_RESET && !(MULTI && MRTS_MULTI_NOPRIO)) {
         // Issue priority by game size: a SIMD runs several games at once and the kernel ends with its
         // slowest one, so the games with the most units (the longest serial chains) issue first.
         int q;
@@ -5360,11 +5354,9 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
                 if (it > 0) q = 3 - (rk < 3 ? rk : 3);
             }
         } else {  // units (the idle count's ballot costs the latency-bound one-game-per-SIMD c2 4.5 %)
+            // (c5, two games + their helper waves per SIMD: without any priority -9 %, the games all at 3 or all
+            // above the helpers' 0 +-0.5 % — what counts is the games issuing before the helpers, round 6)
             q = G.nu >= 36 ? 3 : G.nu >= 30 ? 2 : G.nu >= 24 ? 1 : 0;
-            // c5 (two games + two helper waves per SIMD, the helpers at priority 0): A/B variants
-            if (FPO && MRTS_PO_PRIO == 1) q = q < 1 ? 1 : q;  // every game above the helpers
-            if (FPO && MRTS_PO_PRIO == 2) q = 3;
-            if (FPO && MRTS_PO_PRIO == 3) q = G.nu >= 33 ? 3 : G.nu >= 27 ? 2 : 1;
             if (ranked) {
                 const int wq = G.nu + (int)__popcll(ballot(G.lid() < G.nu && !(G.lua & UA_PRESENT) && uplay(G.lcu) >= 0));
                 const int rk = simdRankStep(srank, (uint32_t)(wq + MRTS_RANK_C) * (uint32_t)(niter - it));
