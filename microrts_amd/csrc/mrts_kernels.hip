@@ -237,6 +237,13 @@ DEV int lane_id() { return (int)threadIdx.x; }
 #ifndef MRTS_XOR3  // Philox's xors as one three-input bit op (round 5); 0 = plain C
 #define MRTS_XOR3 1
 #endif
+// c2's helper-wave launches: the game wave issues at priority >= 1, ahead of its helper wave (at 0) — round 6:
+// c2 +1.6 % / +0.4 % (two rounds of interleaved runs; the helper at 3 instead: -4.5 %); on c5 +0.5 % / -0.6 %, so
+// c5 keeps its unit-count priorities (which already put most of its games above their helpers: without any
+// priority c5 lost 9 %)
+#ifndef MRTS_GAME_OVER_HELPER
+#define MRTS_GAME_OVER_HELPER 1
+#endif
 #ifndef MRTS_HELPER_PRIO
 #define MRTS_HELPER_PRIO 0
 #endif
@@ -5363,6 +5370,7 @@ __global__ __launch_bounds__(HELP ? 128 : 64, (HELP || FIX == 16) ? 4 : 1) void 
                 if (it > 0) q = 3 - (rk < 3 ? rk : 3);
             }
         }
+        if (HELP && !FPO && MRTS_GAME_OVER_HELPER) q = q < 1 ? 1 : q;
         if (q == 0) {
             if (it > 0) __builtin_amdgcn_s_setprio(0);
         } else if (q == 1) __builtin_amdgcn_s_setprio(1);
