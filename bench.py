@@ -626,7 +626,12 @@ def other_configs(a, timeout=240.0):
     window the builder's own figures are quoted at.  A child that fails or overruns leaves {"error": ...} there."""
     import subprocess
 
-    env = {k: v for k, v in os.environ.items() if k not in ("MASTER_ADDR", "MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    # a child is a fresh one-rank run: none of a launcher's rendezvous variables (under torch.distributed.run,
+    # TORCHELASTIC_USE_AGENT_STORE would make the child's process group wait as a client of a store that is
+    # not there)
+    launcher = ("MASTER_ADDR", "MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE")
+    env = {k: v for k, v in os.environ.items() if k not in launcher and not k.startswith("TORCHELASTIC_")}
 
     def child(cfg, extra):
         cmd = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--warmup", str(a.warmup), "--burnin", str(a.burnin)]
