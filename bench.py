@@ -616,6 +616,15 @@ def full_contract_window(a, sh, local, base, total_games, world, mdist, torch, d
     return out
 
 
+def child_env(environ):
+    """The environment of a child bench.py run: a fresh one-rank run, so none of a launcher's rendezvous variables
+    (under torch.distributed.run, TORCHELASTIC_USE_AGENT_STORE would make the child's process group wait as a
+    client of a store that is not there)."""
+    launcher = ("MASTER_ADDR", "MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE")
+    return {k: v for k, v in environ.items() if k not in launcher and not k.startswith("TORCHELASTIC_")}
+
+
 def other_configs(a, timeout=240.0):
     """the other single-GPU BASELINE configs in the driver's own line — c2 (configs[1]: 8x8, 1024
     games, unmasked uniform rows) and c5 (configs[4] per GPU: 32x32, 2048 partially observable games, masked
@@ -626,12 +635,7 @@ def other_configs(a, timeout=240.0):
     window the builder's own figures are quoted at.  A child that fails or overruns leaves {"error": ...} there."""
     import subprocess
 
-    # a child is a fresh one-rank run: none of a launcher's rendezvous variables (under torch.distributed.run,
-    # TORCHELASTIC_USE_AGENT_STORE would make the child's process group wait as a client of a store that is
-    # not there)
-    launcher = ("MASTER_ADDR", "MASTER_PORT", "RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK",
-                "GROUP_WORLD_SIZE", "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE")
-    env = {k: v for k, v in os.environ.items() if k not in launcher and not k.startswith("TORCHELASTIC_")}
+    env = child_env(os.environ)
 
     def child(cfg, extra):
         cmd = [sys.executable, os.path.abspath(__file__), "--config", cfg, "--warmup", str(a.warmup), "--burnin", str(a.burnin)]
